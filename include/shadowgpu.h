@@ -1,0 +1,241 @@
+/*
+ * shadowgpu.h — C-ABI of libshadowgpu, the MI355X (gfx950) event-scheduling core
+ * for Shadow 1.14's conservative round scheduler.
+ *
+ * Plain C, opaque handles, int status returns (0 = SG_OK), no C++ or torch types.
+ * Every entry point names the reference interface it replaces (paths relative to
+ * the Shadow source tree, src/main/...).  INTEGRATION.md shows the reference-side
+ * binding (scheduler_policy_gpu.c) a maintainer adds to use it.
+ *
+ * Two groups of entry points:
+ *   1. Host-side restatements of the reference arithmetic that feeds the device
+ *      tables (glibc rand_r streams, the seed chain, host attachment, direct-path
+ *      delay/reliability resolution, PHOLD destination weights, window logic).
+ *   2. The device engine: per-host event queues resident in HBM, one conservative
+ *      round = process (pop every event before the barrier in event_compare order,
+ *      run the PHOLD body, resolve delivery times and drops) → insert (deliver the
+ *      new events into the destination queues, barrier bump applied) → window
+ *      (MIN next-event time + min-latency runahead → next [start, end)).
+ */
+#ifndef SHADOWGPU_H
+#define SHADOWGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+typedef uint64_t sg_simtime;                /* SimulationTime, core/support/definitions.h:18 */
+#define SG_SIMTIME_INVALID UINT64_MAX       /* definitions.h:28 */
+#define SG_SIMTIME_MAX (UINT64_MAX - 1)     /* definitions.h:33 */
+#define SG_ONE_MS 1000000ULL                /* SIMTIME_ONE_MILLISECOND, definitions.h:48 */
+#define SG_RAND_MAX 2147483647              /* glibc RAND_MAX: rand_r yields 31 bits */
+
+enum sg_status {
+    SG_OK = 0,
+    SG_ERR_INVAL = 1,     /* bad argument / shape */
+    SG_ERR_NOMEM = 2,     /* host or device allocation failed */
+    SG_ERR_HIP = 3,       /* a HIP runtime call failed (see sg_last_error) */
+    SG_ERR_OVERFLOW = 4,  /* a device queue, outbox or trace buffer ran out of slots */
+    SG_ERR_STATE = 5,     /* call out of order (e.g. step before boot) */
+    SG_ERR_NODEV = 6      /* no gfx950 device visible */
+};
+
+/* Last error message of the calling thread (static storage, never NULL). */
+const char* sg_last_error(void);
+int sg_abi_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* 1. Reference arithmetic (host side)                                      */
+/* ------------------------------------------------------------------------ */
+
+/* glibc rand_r (three LCG steps, 31-bit result) on a per-host 32-bit state.
+ * Replaces random_rand, utility/random.c:32-37. */
+int32_t sg_rand_r(uint32_t* state);
+/* random_nextDouble, utility/random.c:39-43: rand_r / RAND_MAX in FP64. */
+double sg_random_next_double(uint32_t* state);
+/* random_nextUInt, utility/random.c:45-51: (uint)(nextDouble * UINT_MAX). */
+uint32_t sg_random_next_uint(uint32_t* state);
+
+/* Seed chain for `-s seed`: master Random(seed) (core/master.c:95) → slave seed
+ * (master.c:417) → slave Random (slave.c:182) → scheduler seed (slave.c:198) →
+ * one node seed per host in registration order (slave.c:301). */
+int sg_seed_chain(uint32_t seed, uint32_t n_hosts, uint32_t* slave_seed,
+                  uint32_t* scheduler_seed, uint32_t* node_seeds);
+
+enum sg_attach_rule {
+    SG_ATTACH_MODULO = 0, /* vertex = host index mod V, no RNG draw (survey probe) */
+    SG_ATTACH_RANDOM = 1  /* routing/topology.c:2327-2333: candidate round((V-1)*nextDouble) */
+};
+/* Host RNG = Random(nodeSeed) (host/host.c:176); topology_attach may consume one
+ * draw (topology.c:2327).  Writes each host's vertex and its RNG state after
+ * attachment. */
+int sg_attach_hosts(uint32_t n_hosts, uint32_t n_vertices, uint32_t rule,
+                    const uint32_t* node_seeds, uint32_t* vertex_out,
+                    uint32_t* rng_state_out);
+
+/* Largest x in [0, RAND_MAX] with (double)x / RAND_MAX <= reliability, or -1.
+ * Turns worker.c:268-273's FP64 drop test (chance <= reliability) into an exact
+ * integer compare on the raw rand_r value. */
+int32_t sg_keep_threshold(double reliability);
+
+/* Direct-path resolution for a complete V-vertex graph (topology.c:1877-1927):
+ *   reliability = 1 * (1 - loss[src]) * (1 - loss[dst]) * (1 - edge_loss)
+ *   delay_ns    = ceil(latency_ms * 1e6)                    (worker.c:275-277)
+ *   keep_max    = sg_keep_threshold(reliability)
+ *   jump_ms     = (uint64)latency_ms, the truncation of master.c:153
+ * latency_ms / edge_loss are V*V row-major (src-major); vertex_loss may be NULL
+ * (vertices without a packetloss attribute). */
+int sg_build_paths(uint32_t n_vertices, const double* latency_ms,
+                   const double* edge_loss, const double* vertex_loss,
+                   uint64_t* delay_ns, int32_t* keep_max, uint32_t* jump_ms);
+
+/* PHOLD destination weights (src/test/phold/test_phold.c:160-178): host i is the
+ * first with cumulative(i) >= r, r = rand_r / RAND_MAX, cumulative summed in
+ * FP64 in host order.  thresh[i] = largest x with x/RAND_MAX <= cumulative(i)
+ * (or -1), so "first i with x <= thresh[i]" is the exact integer restatement.
+ * An x above thresh[n-1] selects no host (the plugin sends nothing). */
+int sg_build_weight_thresholds(uint32_t n, const double* weights, int32_t* thresh_out);
+
+/* Window logic of the master (core/master.c:133-159, 450-480). */
+typedef struct sg_window_state {
+    sg_simtime min_jump;          /* master->minJumpTime */
+    sg_simtime next_min_jump;     /* master->nextMinJumpTime */
+    sg_simtime min_jump_config;   /* -r runahead in ns (master.c:97-98); 0 = unset */
+    sg_simtime end_time;          /* stoptime in ns */
+} sg_window_state;
+/* Path discovery during the round lowered the topology minimum latency to
+ * latency_ms (topology.c:1374-1385 → master_updateMinTimeJump). */
+void sg_window_note_latency(sg_window_state* st, double latency_ms);
+/* master_slaveFinishedCurrentRound: returns 1 to keep running. */
+int sg_window_next(sg_window_state* st, sg_simtime min_next_event,
+                   sg_simtime* start_out, sg_simtime* end_out);
+
+/* Deterministic synthetic topology for the PHOLD configs: symmetric V*V
+ * log-normal latency matrix (ms, self-loops included) with minimum min_ms and
+ * uniform edge loss.  Input generation only — not reference semantics. */
+int sg_topology_lognormal(uint32_t n_vertices, uint64_t seed, double median_ms,
+                          double sigma, double min_ms, double edge_loss,
+                          double* latency_ms_out, double* edge_loss_out);
+
+/* ------------------------------------------------------------------------ */
+/* 2. Device engine (synthetic PHOLD-style workload, "Mode S")               */
+/* ------------------------------------------------------------------------ */
+
+enum sg_dst_rule {
+    SG_DST_UNIFORM_FLOOR = 0, /* dst = floor(r * N), clamped to N-1 (survey probe) */
+    SG_DST_WEIGHTS = 1        /* test_phold.c:160-178 via sg_build_weight_thresholds */
+};
+enum sg_window_rule {
+    SG_WINDOW_FIXED = 0,      /* every window is [min, min + fixed_jump) */
+    SG_WINDOW_DISCOVERED = 1  /* master.c: runahead = truncated min discovered latency */
+};
+
+typedef struct sg_phold_params {
+    uint32_t n_hosts;        /* N, global (all shards) */
+    uint32_t n_vertices;     /* V */
+    uint32_t load;           /* messages each host sends when it boots (test_phold.c:234-239) */
+    uint32_t dst_rule;       /* enum sg_dst_rule */
+    uint32_t window_rule;    /* enum sg_window_rule */
+    uint32_t queue_cap;      /* event slots per host in HBM (0 = default 64) */
+    uint32_t shard_index;    /* this rank */
+    uint32_t shard_count;    /* ranks; hosts are block-partitioned */
+    sg_simtime end_time;     /* scheduler endTime (scheduler.c:343) */
+    sg_simtime bootstrap_end;/* worker_isBootstrapActive (worker.c:445-453) */
+    sg_simtime fixed_jump;   /* SG_WINDOW_FIXED */
+    sg_simtime runahead_min; /* -r in ns, SG_WINDOW_DISCOVERED */
+    uint64_t trace_capacity; /* pop records kept for trace diffs (0 = off) */
+    uint64_t exchange_cap;   /* per-peer outbox slots (multi-shard) */
+} sg_phold_params;
+
+typedef struct sg_phold_tables {        /* host pointers, copied to HBM at create */
+    const uint32_t* host_vertex;   /* [n_hosts] attachment vertex of every host */
+    const uint32_t* host_rng;      /* [n_hosts] rand_r state after attachment */
+    const uint64_t* delay_ns;      /* [V*V] */
+    const int32_t* keep_max;       /* [V*V] */
+    const uint32_t* jump_ms;       /* [V*V] */
+    const int32_t* weight_thresh;  /* [n_hosts]; may be NULL for SG_DST_UNIFORM_FLOOR */
+} sg_phold_tables;
+
+typedef struct sg_round_stats {
+    uint64_t rounds;          /* windows executed */
+    uint64_t pops;            /* committed events (executed pops, worker.c:165-176) */
+    uint64_t boots;           /* of which boot events */
+    uint64_t sends;           /* send attempts with a destination */
+    uint64_t null_dst;        /* destination draws that selected no host */
+    uint64_t drop_reliability;/* dropped by the reliability test (PDS_INET_DROPPED) */
+    uint64_t drop_endtime;    /* created but dropped at scheduler_push (t >= endTime) */
+    uint64_t bumped;          /* inter-host events moved to the barrier */
+    uint64_t same_round;      /* self events popped in the round that created them */
+    uint64_t overflow;        /* nonzero: a queue / outbox / trace ran out of slots */
+    sg_simtime window_start;  /* current window */
+    sg_simtime window_end;
+    uint64_t done;            /* 1 when start >= end (slave.c:459) */
+    sg_simtime min_jump;
+    sg_simtime next_min_jump;
+    uint64_t jmin_ms;         /* truncated min discovered latency, UINT64_MAX if none */
+    uint64_t pending;         /* events queued in HBM after the last round */
+    uint64_t trace_len;       /* pop records written */
+} sg_round_stats;
+
+typedef struct sg_trace_rec {   /* one executed pop */
+    sg_simtime time;
+    uint64_t seq;    /* srcHostEventID (event.c:38) */
+    uint32_t host;   /* destination host index (global) */
+    uint32_t src;    /* source host index (global) */
+    uint64_t pos;    /* position in the host's pop sequence */
+} sg_trace_rec;
+
+typedef struct sg_engine sg_engine;
+
+/* Allocates the HBM state for this shard's hosts and uploads the tables.
+ * hip_stream may be NULL (the engine makes its own) or a hipStream_t. */
+int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* tables,
+                     int device, void* hip_stream, sg_engine** out);
+int sg_engine_destroy(sg_engine* e);
+/* host_boot: one self event per local host at t=0 (seq 0) that sends `load`
+ * messages, then the first window [0, 1) (slave.c:431). */
+int sg_engine_boot(sg_engine* e);
+/* Single shard: runs up to max_rounds windows without host round-trips, in
+ * batches of `batch` rounds per host synchronisation; stops when done. */
+int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch);
+/* Enqueue one round (process + insert + window) without synchronising. */
+int sg_engine_enqueue_round(sg_engine* e);
+int sg_engine_sync(sg_engine* e);
+int sg_engine_stats(sg_engine* e, sg_round_stats* out);   /* synchronises */
+/* Per local host (index - first_host): trace digest, pops, rng state, event counter. */
+int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops,
+                         uint32_t* rng, uint64_t* event_counter);
+int sg_engine_host_range(sg_engine* e, uint32_t* first_host, uint32_t* n_local);
+/* Cumulative hosts-with-pops per round (active host-rounds) and staged events. */
+int sg_engine_active_hosts(sg_engine* e, uint64_t* active_host_rounds, uint64_t* emitted);
+int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
+void* sg_engine_stream(sg_engine* e);
+
+/* Multi-shard round, driven by the caller around its collectives:
+ *   step_process(e, send, send_counts) — pops + PHOLD body; events for other
+ *       shards go to send[peer * exchange_cap * 3 ...] as int64 triples
+ *       {time, seq, (dst << 32) | src}; send_counts[peer] gets their count
+ *       (device pointers, e.g. torch tensors);
+ *   step_insert(e, recv, n_recv) — local new events + n_recv received triples;
+ *   step_reduce(e, out3) — out3 = {local min next time, local min jump ms,
+ *       ~overflow} (device, reduce with MIN across ranks);
+ *   step_window(e, in3) — next window from the reduced triple. */
+int sg_engine_step_process(sg_engine* e, int64_t* send, int64_t* send_counts);
+int sg_engine_step_insert(sg_engine* e, const int64_t* recv, uint64_t n_recv);
+int sg_engine_step_reduce(sg_engine* e, uint64_t* out3);
+int sg_engine_step_window(sg_engine* e, const uint64_t* in3);
+
+/* Kernel timing of the last sg_engine_run/enqueue (HIP events on the engine
+ * stream): total ms per kernel class {process, insert, window}, and launches. */
+int sg_engine_kernel_times(sg_engine* e, double* ms3, uint64_t* launches);
+int sg_engine_set_timing(sg_engine* e, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHADOWGPU_H */

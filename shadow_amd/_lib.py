@@ -1,0 +1,136 @@
+"""ctypes binding of libshadowgpu.so (include/shadowgpu.h).
+
+The library is built in-tree by shadow_amd/build.py.  There is no fallback: a
+missing library raises, and engine creation fails loudly without a gfx950 GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libshadowgpu.so")
+
+SG_OK, SG_ERR_INVAL, SG_ERR_NOMEM, SG_ERR_HIP, SG_ERR_OVERFLOW, SG_ERR_STATE, SG_ERR_NODEV = range(7)
+SG_ATTACH_MODULO, SG_ATTACH_RANDOM = 0, 1
+SG_DST_UNIFORM_FLOOR, SG_DST_WEIGHTS = 0, 1
+SG_WINDOW_FIXED, SG_WINDOW_DISCOVERED = 0, 1
+ONE_MS = 1_000_000
+SIMTIME_MAX = (1 << 64) - 2
+RAND_MAX = 2147483647
+
+u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+class SgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libshadowgpu error {code}: {msg}")
+        self.code = code
+
+
+class PholdParams(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in
+                ("n_hosts", "n_vertices", "load", "dst_rule", "window_rule", "queue_cap",
+                 "shard_index", "shard_count")] + \
+               [(n, C.c_uint64) for n in
+                ("end_time", "bootstrap_end", "fixed_jump", "runahead_min", "trace_capacity",
+                 "exchange_cap")]
+
+
+class PholdTables(C.Structure):
+    _fields_ = [("host_vertex", C.c_void_p), ("host_rng", C.c_void_p), ("delay_ns", C.c_void_p),
+                ("keep_max", C.c_void_p), ("jump_ms", C.c_void_p), ("weight_thresh", C.c_void_p)]
+
+
+class RoundStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in
+                ("rounds", "pops", "boots", "sends", "null_dst", "drop_reliability",
+                 "drop_endtime", "bumped", "same_round", "overflow", "window_start",
+                 "window_end", "done", "min_jump", "next_min_jump", "jmin_ms", "pending",
+                 "trace_len")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class WindowState(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("min_jump", "next_min_jump", "min_jump_config", "end_time")]
+
+
+TRACE_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"),
+                        ("pos", "<u8")])
+
+_lib = None
+
+EXPORTS = [
+    "sg_last_error", "sg_abi_version", "sg_rand_r", "sg_random_next_double",
+    "sg_random_next_uint", "sg_seed_chain", "sg_attach_hosts", "sg_keep_threshold",
+    "sg_build_paths", "sg_build_weight_thresholds", "sg_window_note_latency", "sg_window_next",
+    "sg_topology_lognormal", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
+    "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
+    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace",
+    "sg_engine_stream", "sg_engine_step_process", "sg_engine_step_insert",
+    "sg_engine_step_reduce", "sg_engine_step_window", "sg_engine_kernel_times",
+    "sg_engine_set_timing",
+]
+
+
+def lib():
+    """Load libshadowgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m shadow_amd.build` "
+                           "(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    L.sg_last_error.restype = C.c_char_p
+    L.sg_rand_r.argtypes = [C.POINTER(C.c_uint32)]
+    L.sg_rand_r.restype = C.c_int32
+    L.sg_random_next_double.argtypes = [C.POINTER(C.c_uint32)]
+    L.sg_random_next_double.restype = C.c_double
+    L.sg_random_next_uint.argtypes = [C.POINTER(C.c_uint32)]
+    L.sg_random_next_uint.restype = C.c_uint32
+    L.sg_seed_chain.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                C.POINTER(C.c_uint32), u32p]
+    L.sg_attach_hosts.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, u32p]
+    L.sg_keep_threshold.argtypes = [C.c_double]
+    L.sg_keep_threshold.restype = C.c_int32
+    L.sg_build_paths.argtypes = [C.c_uint32, f64p, f64p, C.c_void_p, u64p, i32p, u32p]
+    L.sg_build_weight_thresholds.argtypes = [C.c_uint32, f64p, i32p]
+    L.sg_window_note_latency.argtypes = [C.POINTER(WindowState), C.c_double]
+    L.sg_window_note_latency.restype = None
+    L.sg_window_next.argtypes = [C.POINTER(WindowState), C.c_uint64, C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_uint64)]
+    L.sg_topology_lognormal.argtypes = [C.c_uint32, C.c_uint64, C.c_double, C.c_double,
+                                        C.c_double, C.c_double, f64p, f64p]
+    L.sg_engine_create.argtypes = [C.POINTER(PholdParams), C.POINTER(PholdTables), C.c_int,
+                                   C.c_void_p, C.POINTER(C.c_void_p)]
+    for f in ("sg_engine_destroy", "sg_engine_boot", "sg_engine_enqueue_round", "sg_engine_sync"):
+        getattr(L, f).argtypes = [C.c_void_p]
+    L.sg_engine_run.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+    L.sg_engine_stats.argtypes = [C.c_void_p, C.POINTER(RoundStats)]
+    L.sg_engine_host_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.sg_engine_host_range.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.sg_engine_active_hosts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.sg_engine_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.sg_engine_stream.argtypes = [C.c_void_p]
+    L.sg_engine_stream.restype = C.c_void_p
+    L.sg_engine_step_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.sg_engine_step_insert.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    L.sg_engine_step_reduce.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_engine_step_window.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_engine_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    L.sg_engine_set_timing.argtypes = [C.c_void_p, C.c_int]
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != SG_OK:
+        raise SgError(rc, lib().sg_last_error().decode(errors="replace"))

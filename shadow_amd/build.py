@@ -1,0 +1,76 @@
+"""In-tree build of libshadowgpu.so (gfx950) and the C policy harness.
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
+container; the .so files travel to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(ROOT, "include")
+BUILD = os.path.join(ROOT, "build")
+LIB = os.path.join(PKG, "libshadowgpu.so")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+C_FLAGS = ["-O2", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+           "-Wextra", "-Wno-unused-parameter", "-I" + INC]
+HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
+             "-fno-fast-math", "-Wall", "-I" + INC]
+
+C_SOURCES = ["sg_host.c"]
+HIP_SOURCES = ["sg_engine.hip"]
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build step failed: " + " ".join(cmd))
+    return r
+
+
+def _stale(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hdrs = [os.path.join(INC, f) for f in os.listdir(INC) if f.endswith(".h")]
+    hdrs += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    objs = []
+    for src in C_SOURCES:
+        path = os.path.join(CSRC, src)
+        if not os.path.exists(path):
+            continue
+        obj = os.path.join(BUILD, src + ".o")
+        if force or _stale(obj, [path] + hdrs):
+            _run(["gcc"] + C_FLAGS + ["-c", path, "-o", obj], verbose)
+        objs.append(obj)
+    for src in HIP_SOURCES:
+        path = os.path.join(CSRC, src)
+        if not os.path.exists(path):
+            continue
+        obj = os.path.join(BUILD, src + ".o")
+        if force or _stale(obj, [path] + hdrs):
+            _run([HIPCC] + HIP_FLAGS + ["-c", path, "-o", obj], verbose)
+        objs.append(obj)
+    if force or _stale(LIB, objs):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-lpthread"],
+             verbose)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

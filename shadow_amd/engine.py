@@ -1,0 +1,140 @@
+"""Python handle on the HBM-resident round engine (libshadowgpu, Mode S)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Engine:
+    """One shard of a PHOLD simulation resident on one MI355X.
+
+    Single shard: ``boot(); run(max_rounds)``.  Multi-shard: the distributed
+    driver (shadow_amd.dist) calls the step_* methods around its collectives.
+    """
+
+    def __init__(self, cfg: dict, *, device: int = 0, shard_index: int = 0, shard_count: int = 1,
+                 queue_cap: int = 0, trace_capacity: int = 0, exchange_cap: int = 0,
+                 stream: int | None = None):
+        lib = L.lib()
+        p = L.PholdParams()
+        p.n_hosts = cfg["n_hosts"]
+        p.n_vertices = cfg["n_vertices"]
+        p.load = cfg["load"]
+        p.dst_rule = cfg["dst_rule"]
+        p.window_rule = cfg["window_rule"]
+        p.queue_cap = queue_cap
+        p.shard_index = shard_index
+        p.shard_count = shard_count
+        p.end_time = cfg["end_time"]
+        p.bootstrap_end = cfg.get("bootstrap_end", 0)
+        p.fixed_jump = cfg.get("fixed_jump", 0)
+        p.runahead_min = cfg.get("runahead_min", 0)
+        p.trace_capacity = trace_capacity
+        p.exchange_cap = exchange_cap
+        self.params = p
+        self._arrays = [np.ascontiguousarray(cfg["host_vertex"], np.uint32),
+                        np.ascontiguousarray(cfg["host_rng"], np.uint32),
+                        np.ascontiguousarray(cfg["delay_ns"], np.uint64),
+                        np.ascontiguousarray(cfg["keep_max"], np.int32),
+                        np.ascontiguousarray(cfg["jump_ms"], np.uint32)]
+        wt = cfg.get("weight_thresh")
+        self._wt = None if wt is None else np.ascontiguousarray(wt, np.int32)
+        t = L.PholdTables(*[a.ctypes.data for a in self._arrays],
+                          None if self._wt is None else self._wt.ctypes.data)
+        h = C.c_void_p()
+        L.check(lib.sg_engine_create(C.byref(p), C.byref(t), device, stream, C.byref(h)))
+        self.h = h
+        lo, n = C.c_uint32(), C.c_uint32()
+        L.check(lib.sg_engine_host_range(h, C.byref(lo), C.byref(n)))
+        self.first_host, self.n_local = lo.value, n.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib().sg_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # -------------------------------------------------------- single shard
+    def boot(self):
+        L.check(L.lib().sg_engine_boot(self.h))
+
+    def run(self, max_rounds: int = 1 << 62, batch: int = 32):
+        L.check(L.lib().sg_engine_run(self.h, max_rounds, batch))
+
+    def enqueue_round(self):
+        L.check(L.lib().sg_engine_enqueue_round(self.h))
+
+    def sync(self):
+        L.check(L.lib().sg_engine_sync(self.h))
+
+    @property
+    def stream(self) -> int:
+        return L.lib().sg_engine_stream(self.h) or 0
+
+    # ------------------------------------------------------------- results
+    def stats(self) -> dict:
+        s = L.RoundStats()
+        L.check(L.lib().sg_engine_stats(self.h, C.byref(s)))
+        return s.as_dict()
+
+    def active_hosts(self):
+        a, e = C.c_uint64(), C.c_uint64()
+        L.check(L.lib().sg_engine_active_hosts(self.h, C.byref(a), C.byref(e)))
+        return a.value, e.value
+
+    def host_state(self) -> dict:
+        n = self.n_local
+        d, p, e = (np.zeros(n, np.uint64) for _ in range(3))
+        r = np.zeros(n, np.uint32)
+        L.check(L.lib().sg_engine_host_state(self.h, d.ctypes.data, p.ctypes.data, r.ctypes.data,
+                                             e.ctypes.data))
+        return {"digest": d, "pops": p, "rng": r, "ev": e}
+
+    def trace(self) -> np.ndarray:
+        n = C.c_uint64()
+        L.check(L.lib().sg_engine_trace(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, L.TRACE_DTYPE)
+        if n.value:
+            L.check(L.lib().sg_engine_trace(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out
+
+    def set_timing(self, on: bool):
+        L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
+
+    def kernel_times(self):
+        ms = (C.c_double * 3)()
+        n = (C.c_uint64 * 3)()
+        L.check(L.lib().sg_engine_kernel_times(self.h, ms, n))
+        return {"process": (ms[0], n[0]), "insert": (ms[1], n[1]), "window": (ms[2], n[2])}
+
+    # ---------------------------------------------------------- multi shard
+    def step_process(self, send_ptr: int, send_counts_ptr: int):
+        L.check(L.lib().sg_engine_step_process(self.h, send_ptr, send_counts_ptr))
+
+    def step_insert(self, recv_ptr: int, n_recv: int):
+        L.check(L.lib().sg_engine_step_insert(self.h, recv_ptr or None, n_recv))
+
+    def step_reduce(self, out3_ptr: int):
+        L.check(L.lib().sg_engine_step_reduce(self.h, out3_ptr))
+
+    def step_window(self, in3_ptr: int):
+        L.check(L.lib().sg_engine_step_window(self.h, in3_ptr))
+
+
+def probe_hash(trace: np.ndarray) -> tuple[int, int]:
+    """The survey probe's chained trace hash over message pops (boot pops skipped),
+    hosts in index order, each host's pops in pop order."""
+    t = np.sort(trace, order=["host", "pos"])
+    msg = ~((t["src"] == t["host"]) & (t["seq"] == 0))
+    t = t[msg]
+    h = 5381
+    M = (1 << 64) - 1
+    for tm, src, seq, host in zip(t["time"].tolist(), t["src"].tolist(), t["seq"].tolist(),
+                                  t["host"].tolist()):
+        h = ((h * 1000003) & M) ^ ((tm * 31 + src * 7 + seq + host) & M)
+    return h, int(msg.sum())

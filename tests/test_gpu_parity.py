@@ -1,0 +1,134 @@
+"""GPU parity: the HIP round engine against the CPU oracle on identical inputs.
+
+Bit-exact bar: per-host trace digests (order-sensitive over every pop's
+(time, src, srcHostEventID)), per-host pop counts, final rand_r states and
+event-id counters, the global counters and the window sequence's end state.
+Full traces are compared record by record where they are small.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from shadow_amd import phold
+from shadow_amd import _lib as L
+from shadow_amd.engine import Engine, probe_hash
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _run_both(cfg, trace=0, max_rounds=1 << 62, queue_cap=0):
+    eng = Engine(cfg, trace_capacity=trace, queue_cap=queue_cap)
+    eng.boot()
+    eng.run(max_rounds)
+    orc = O.Sim(cfg, trace_capacity=trace)
+    orc.boot()
+    orc.run(max_rounds)
+    return eng, orc
+
+
+def _assert_same(eng, orc):
+    g, o = eng.host_state(), orc.host_state()
+    for k in ("pops", "rng", "ev", "digest"):
+        bad = np.nonzero(g[k] != o[k])[0]
+        assert bad.size == 0, f"{k} differs at hosts {bad[:8]}"
+    gs, os_ = eng.stats(), orc.stats()
+    for k in ("rounds", "pops", "boots", "sends", "null_dst", "drop_reliability",
+              "drop_endtime", "bumped", "same_round", "pending", "window_start", "window_end",
+              "done", "jmin_ms"):
+        assert gs[k] == os_[k], (k, gs[k], os_[k])
+    assert gs["overflow"] == 0
+    return gs
+
+
+@pytest.mark.parametrize("jump", [5, 10])
+def test_probe_trace_hash_matches_reference(jump):
+    """The survey ran the reference's own scheduler.c + host_single/host_steal on
+    this workload and recorded these trace hashes (tests/golden/probe_hashes.json)."""
+    gold = json.load(open(os.path.join(GOLDEN, "probe_hashes.json")))[f"jump_{jump}ms"]
+    cfg = phold.probe_config(n_hosts=1000, jump_ms=jump)
+    eng = Engine(cfg, trace_capacity=1_300_000)
+    eng.boot()
+    eng.run()
+    tr = eng.trace()
+    h, n = probe_hash(tr)
+    assert n == gold["messages"]
+    assert f"{h:016x}" == gold["hash"]
+    orc = O.Sim(cfg, trace_capacity=1_300_000)
+    orc.boot()
+    orc.run()
+    _assert_same(eng, orc)
+
+
+@pytest.mark.parametrize("variant", ["lossy", "weights_uniform", "weights_skewed", "runahead",
+                                     "bootstrap", "fixed_wide", "floor_rule", "one_host",
+                                     "tiny_latency"])
+def test_tiny_variants(variant):
+    kw = {}
+    if variant == "weights_skewed":
+        kw["weights"] = np.linspace(0.1, 5.0, 96) ** 2
+    cfg = {
+        "lossy": lambda: phold.tiny_config(n_hosts=96, loss=0.2),
+        "weights_uniform": lambda: phold.tiny_config(n_hosts=96),
+        "weights_skewed": lambda: phold.tiny_config(n_hosts=96, **kw),
+        "runahead": lambda: phold.tiny_config(n_hosts=96, runahead_ms=7),
+        "bootstrap": lambda: dict(phold.tiny_config(n_hosts=96, loss=0.5), bootstrap_end=100_000_000),
+        "fixed_wide": lambda: phold.tiny_config(n_hosts=96, window_rule=L.SG_WINDOW_FIXED) | {"fixed_jump": 25 * L.ONE_MS},
+        "floor_rule": lambda: phold.tiny_config(n_hosts=96, dst_rule=L.SG_DST_UNIFORM_FLOOR),
+        "one_host": lambda: phold.tiny_config(n_hosts=1, V=1, load=3),
+        "tiny_latency": lambda: phold.tiny_config(n_hosts=64, min_ms=0.2),
+    }[variant]()
+    eng, orc = _run_both(cfg, trace=400_000)
+    gs = _assert_same(eng, orc)
+    assert gs["pops"] > 0
+    gt = np.sort(eng.trace(), order=["host", "pos"])
+    ot = np.sort(orc.trace(), order=["host", "pos"])
+    assert gt.shape == ot.shape
+    for f in ("time", "seq", "host", "src", "pos"):
+        assert np.array_equal(gt[f], ot[f]), f
+
+
+def test_c2_shape_parity():
+    """configs[1] shape (uniform 50 ms mesh, weights rule) at 10k hosts for 2 s."""
+    cfg = phold.c2_config(n_hosts=10_000, end_time_s=2.0)
+    eng, orc = _run_both(cfg)
+    gs = _assert_same(eng, orc)
+    assert gs["pops"] > 10_000 * 16 * 30
+
+
+def test_c4_shape_prefix_parity():
+    """configs[3] shape (log-normal latency, runahead 1 ms) at 100k hosts, 40 rounds."""
+    cfg = phold.c4_config(n_hosts=100_000)
+    eng, orc = _run_both(cfg, max_rounds=40)
+    _assert_same(eng, orc)
+
+
+def test_lossy_c5_shape_prefix_parity():
+    cfg = phold.c5_config(n_hosts=20_000)
+    eng, orc = _run_both(cfg, max_rounds=60)
+    gs = _assert_same(eng, orc)
+    assert gs["drop_reliability"] > 0
+
+
+def test_full_size_c4_invariants():
+    """1M hosts: size-independent properties — events are conserved (no loss,
+    nothing reaches endTime yet), the pending count stays N*load, every host's
+    pops equal its event-id counter minus its sends in flight, and the first
+    rounds' digests equal the oracle's (checksum of checksums)."""
+    cfg = phold.c4_config(n_hosts=1_000_000)
+    eng = Engine(cfg)
+    eng.boot()
+    eng.run(12)
+    st = eng.stats()
+    assert st["overflow"] == 0
+    assert st["pending"] == 1_000_000 * 16 - st["null_dst"]
+    assert st["sends"] + st["null_dst"] == st["pops"] - st["boots"] + st["boots"] * 16
+    orc = O.Sim(cfg)
+    orc.boot()
+    orc.run(12)
+    g, o = eng.host_state(), orc.host_state()
+    assert int(g["digest"].sum(dtype=np.uint64)) == int(o["digest"].sum(dtype=np.uint64))
+    assert np.array_equal(g["digest"], o["digest"])
