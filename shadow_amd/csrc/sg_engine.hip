@@ -43,7 +43,8 @@ enum Ctr {
     C_POPS = 0, C_BOOTS, C_SENDS, C_NULL, C_DROPREL, C_DROPEND, C_BUMPED, C_SAME,
     C_ACTIVE, C_EMIT, NCTR
 };
-constexpr int NPART = NCTR + 1;  // + jmin
+// per-workgroup partials: counters, then three minima
+constexpr int P_JMIN = NCTR, P_EMIN = NCTR + 1, P_RMIN = NCTR + 2, NPART = NCTR + 3;
 
 struct RoundState {
     uint64_t S, E, done, rounds;
@@ -76,8 +77,7 @@ struct Dev {
     uint64_t* pops;           // [L]
     uint64_t* digest;         // [L]
     // per 256-host block
-    uint64_t* blockmin;       // [nblocks]
-    uint64_t* part;           // [nblocks][NPART]
+    uint64_t* part;           // [NPART][nblocks]
     uint32_t* blockcnt;       // [nblocks] staged events
     uint32_t* peercnt;        // [nblocks][G]
     uint32_t* peeroff;        // [nblocks][G]
@@ -197,7 +197,6 @@ __global__ void k_boot(Dev d) {
         d.pops[lh] = 0;
         d.digest[lh] = 0;
     }
-    if (threadIdx.x == 0) d.blockmin[blockIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         RoundState* rs = d.rs;
         rs->S = 0;  // slave.c:431
@@ -214,10 +213,108 @@ __global__ void k_boot(Dev d) {
     }
 }
 
+struct Acc {
+    uint64_t ctr[NCTR];
+    uint64_t jmin;   // min truncated latency of attempted sends
+    uint64_t emin;   // min time of staged (emitted) events
+    bool overflow;
+};
+
+struct HostCtx {
+    uint32_t h, vh, lh;
+    uint32_t rng;
+    uint64_t ev, pops, dig;
+};
+
+// Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
+// Self events that fall inside the window go back to the host's own queue
+// through `append` (they are popped later this round); everything else is
+// staged in the workgroup's region for k_insert / k_pack.
+template <class Append>
+__device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx& c, Acc& a,
+                                              uint64_t bt, uint32_t bs, uint64_t bq,
+                                              uint32_t* s_emit, uint32_t* s_peer, Append append) {
+    c.dig += digest_mix(c.pops, bt, bs, bq);
+    if (d.trace) {
+        const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
+        if (ts < d.trace_cap) {
+            sg_trace_rec r;
+            r.time = bt;
+            r.seq = bq;
+            r.host = c.h;
+            r.src = bs;
+            r.pos = c.pops;
+            d.trace[ts] = r;
+        } else {
+            a.overflow = true;
+        }
+    }
+    ++c.pops;
+    ++a.ctr[C_POPS];
+    const bool boot = (bs == c.h && bq == 0);
+    a.ctr[C_BOOTS] += boot;
+    const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+    for (uint32_t m = 0; m < nsend; ++m) {
+        const int32_t x = dev_rand_r(c.rng);
+        const uint32_t dst = choose_dst(d, x);
+        if (dst >= d.N) {
+            ++a.ctr[C_NULL];
+            continue;
+        }
+        ++a.ctr[C_SENDS];
+        const size_t pair = (size_t)c.vh * d.V + d.vertex[dst];
+        const uint64_t jm = d.jump[pair];  // path discovery (topology.c:1374-1385)
+        a.jmin = jm < a.jmin ? jm : a.jmin;
+        const int32_t ch = dev_rand_r(c.rng);  // worker.c:268-269
+        if (!(bt < d.bootstrap_end || ch <= d.keep[pair])) {
+            ++a.ctr[C_DROPREL];
+            continue;
+        }
+        uint64_t tn = bt + d.delay[pair];  // worker.c:275-277
+        const uint64_t sq = c.ev++;        // event.c:38
+        if (tn >= d.end_time) {            // scheduler.c:343-346
+            ++a.ctr[C_DROPEND];
+            continue;
+        }
+        if (dst == c.h && tn < E) {
+            ++a.ctr[C_SAME];
+            if (!append(tn, sq)) a.overflow = true;
+            continue;
+        }
+        if (dst != c.h && tn < E) {  // host_single.c:180-184
+            tn = E;
+            ++a.ctr[C_BUMPED];
+        }
+        const uint32_t slot = atomicAdd(s_emit, 1u);
+        if (slot >= d.bcap) {
+            a.overflow = true;
+            continue;
+        }
+        const size_t so = (size_t)blockIdx.x * d.bcap + slot;
+        d.st_time[so] = tn;
+        d.st_seq[so] = sq;
+        d.st_dst[so] = dst;
+        d.st_src[so] = c.h;
+        if (d.G > 1) atomicAdd(&s_peer[owner_of(d, dst)], 1u);
+        a.emin = tn < a.emin ? tn : a.emin;
+        ++a.ctr[C_EMIT];
+    }
+}
+
+__device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uint64_t bt, uint32_t bs,
+                                         uint64_t bq) {
+    // event_compare with equal dst (event.c:122-148)
+    return t < bt || (t == bt && (s < bs || (s == bs && q < bq)));
+}
+
+// One lane per host.  MASKED (queue_cap <= 64): the host's queue times are read
+// once with independent loads, the slots before the barrier kept in a 64-bit
+// mask; selection visits only those slots.  Otherwise every pop rescans.
+template <bool MASKED>
 __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     __shared__ uint32_t s_emit;
     __shared__ uint32_t s_peer[MAXG];
-    __shared__ uint64_t s_red[BLOCK / 64][NPART + 1];
+    __shared__ uint64_t s_red[BLOCK / 64][NPART];
     const RoundState* rs = d.rs;
     if (rs->done) return;
     const uint64_t E = rs->E;
@@ -227,185 +324,176 @@ __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     if (threadIdx.x < MAXG) s_peer[threadIdx.x] = 0;
     __syncthreads();
 
-    uint64_t ctr[NCTR];
+    Acc a;
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) ctr[i] = 0;
-    uint64_t jmin = UINT64_MAX;
+    for (int i = 0; i < NCTR; ++i) a.ctr[i] = 0;
+    a.jmin = UINT64_MAX;
+    a.emin = SIMTIME_MAX;
+    a.overflow = false;
     uint64_t newmin = SIMTIME_MAX;
-    bool overflow = false;
 
     if (lh < L) {
         const uint64_t hm = d.hmin[lh];
         newmin = hm;
         if (hm < E) {
-            const uint32_t h = d.lo + lh;
-            const uint32_t vh = d.vertex[h];
+            HostCtx c;
+            c.lh = lh;
+            c.h = d.lo + lh;
+            c.vh = d.vertex[c.h];
+            c.rng = d.rng[lh];
+            c.ev = d.evc[lh];
+            c.pops = d.pops[lh];
+            c.dig = d.digest[lh];
             uint32_t cnt = d.bag_cnt[lh];
-            uint32_t rng = d.rng[lh];
-            uint64_t ev = d.evc[lh];
-            uint64_t pops = d.pops[lh];
-            uint64_t dig = d.digest[lh];
-            ctr[C_ACTIVE] = 1;
-            const uint64_t base_bstride = L;
-            for (;;) {
-                // select the event_compare-minimum queued event before the barrier
-                int best = -1;
-                uint64_t bt = 0, bq = 0;
-                uint32_t bs = 0;
-                uint64_t rest_min = SIMTIME_MAX;
-                for (uint32_t j = 0; j < cnt; ++j) {
-                    const size_t k = (size_t)j * base_bstride + lh;
-                    const uint64_t t = d.bag_time[k];
-                    if (t < E) {
-                        if (best < 0 || t <= bt) {
-                            const uint32_t s = d.bag_src[k];
-                            const uint64_t q = d.bag_seq[k];
-                            if (best < 0 || t < bt || s < bs || (s == bs && q < bq)) {
+            a.ctr[C_ACTIVE] = 1;
+            const size_t stride = L;
+            uint64_t* __restrict__ bt_ = d.bag_time;
+            uint64_t* __restrict__ bq_ = d.bag_seq;
+            uint32_t* __restrict__ bs_ = d.bag_src;
+            if (MASKED) {
+                uint64_t due = 0, rest_min = SIMTIME_MAX;
+                for (uint32_t base = 0; base < cnt; base += 8) {
+                    uint64_t t[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) t[i] = bt_[(size_t)(base + i) * stride + lh];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const bool live = base + i < cnt;
+                        const bool isdue = live && t[i] < E;
+                        due |= (uint64_t)isdue << (base + i);
+                        if (live && !isdue && t[i] < rest_min) rest_min = t[i];
+                    }
+                }
+                // non-due slots only move (never leave) while popping: rest_min is final
+                newmin = rest_min;
+                auto append = [&](uint64_t tn, uint64_t sq) -> bool {
+                    if (cnt >= d.CAP) return false;
+                    const size_t kn = (size_t)cnt * stride + lh;
+                    bt_[kn] = tn;
+                    bq_[kn] = sq;
+                    bs_[kn] = c.h;
+                    due |= 1ULL << cnt;
+                    ++cnt;
+                    return true;
+                };
+                while (due) {
+                    uint64_t m = due;
+                    uint32_t best = 0;
+                    uint64_t bt = SIMTIME_MAX + 1, bq = 0;
+                    uint32_t bs = 0;
+                    while (m) {
+                        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                        m &= m - 1;
+                        const size_t k = (size_t)j * stride + lh;
+                        const uint64_t t = bt_[k];
+                        const uint32_t s = bs_[k];
+                        const uint64_t q = bq_[k];
+                        if (key_less(t, s, q, bt, bs, bq)) {
+                            best = j;
+                            bt = t;
+                            bs = s;
+                            bq = q;
+                        }
+                    }
+                    // remove `best`: the last slot fills the hole
+                    const uint32_t last = cnt - 1;
+                    due &= ~(1ULL << best);
+                    if (best != last) {
+                        const size_t kb = (size_t)best * stride + lh, kl = (size_t)last * stride + lh;
+                        bt_[kb] = bt_[kl];
+                        bq_[kb] = bq_[kl];
+                        bs_[kb] = bs_[kl];
+                        const uint64_t lastbit = (due >> last) & 1ULL;
+                        due &= ~(1ULL << last);
+                        due |= lastbit << best;
+                    }
+                    cnt = last;
+                    execute_event(d, E, c, a, bt, bs, bq, &s_emit, s_peer, append);
+                }
+            } else {
+                auto append = [&](uint64_t tn, uint64_t sq) -> bool {
+                    if (cnt >= d.CAP) return false;
+                    const size_t kn = (size_t)cnt * stride + lh;
+                    bt_[kn] = tn;
+                    bq_[kn] = sq;
+                    bs_[kn] = c.h;
+                    ++cnt;
+                    return true;
+                };
+                for (;;) {
+                    int best = -1;
+                    uint64_t bt = 0, bq = 0;
+                    uint32_t bs = 0;
+                    uint64_t rest_min = SIMTIME_MAX;
+                    for (uint32_t j = 0; j < cnt; ++j) {
+                        const size_t k = (size_t)j * stride + lh;
+                        const uint64_t t = bt_[k];
+                        if (t < E) {
+                            const uint32_t s = bs_[k];
+                            const uint64_t q = bq_[k];
+                            if (best < 0 || key_less(t, s, q, bt, bs, bq)) {
                                 best = (int)j;
                                 bt = t;
                                 bs = s;
                                 bq = q;
                             }
+                        } else if (t < rest_min) {
+                            rest_min = t;
                         }
-                    } else if (t < rest_min) {
-                        rest_min = t;
                     }
-                }
-                if (best < 0) {
-                    newmin = rest_min;
-                    break;
-                }
-                // remove: last slot fills the hole
-                --cnt;
-                if ((uint32_t)best != cnt) {
-                    const size_t kb = (size_t)best * base_bstride + lh;
-                    const size_t kl = (size_t)cnt * base_bstride + lh;
-                    d.bag_time[kb] = d.bag_time[kl];
-                    d.bag_seq[kb] = d.bag_seq[kl];
-                    d.bag_src[kb] = d.bag_src[kl];
-                }
-                // execute the event (worker.c:165-176)
-                dig += digest_mix(pops, bt, bs, bq);
-                if (d.trace) {
-                    const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
-                    if (ts < d.trace_cap) {
-                        sg_trace_rec r;
-                        r.time = bt;
-                        r.seq = bq;
-                        r.host = h;
-                        r.src = bs;
-                        r.pos = pops;
-                        d.trace[ts] = r;
-                    } else {
-                        overflow = true;
+                    if (best < 0) {
+                        newmin = rest_min;
+                        break;
                     }
-                }
-                ++pops;
-                ++ctr[C_POPS];
-                const bool boot = (bs == h && bq == 0);
-                ctr[C_BOOTS] += boot;
-                const uint32_t nsend = boot ? d.load : 1u;
-                for (uint32_t m = 0; m < nsend; ++m) {
-                    const int32_t x = dev_rand_r(rng);
-                    const uint32_t dst = choose_dst(d, x);
-                    if (dst >= d.N) {
-                        ++ctr[C_NULL];
-                        continue;
+                    --cnt;
+                    if ((uint32_t)best != cnt) {
+                        const size_t kb = (size_t)best * stride + lh, kl = (size_t)cnt * stride + lh;
+                        bt_[kb] = bt_[kl];
+                        bq_[kb] = bq_[kl];
+                        bs_[kb] = bs_[kl];
                     }
-                    ++ctr[C_SENDS];
-                    const size_t pair = (size_t)vh * d.V + d.vertex[dst];
-                    const uint64_t jm = d.jump[pair];
-                    jmin = jm < jmin ? jm : jmin;
-                    const int32_t c = dev_rand_r(rng);
-                    if (!(bt < d.bootstrap_end || c <= d.keep[pair])) {
-                        ++ctr[C_DROPREL];
-                        continue;
-                    }
-                    uint64_t tn = bt + d.delay[pair];
-                    const uint64_t sq = ev++;
-                    if (tn >= d.end_time) {  // scheduler.c:343-346
-                        ++ctr[C_DROPEND];
-                        continue;
-                    }
-                    if (dst == h && tn < E) {
-                        // self event inside the window: popped later this round
-                        ++ctr[C_SAME];
-                        if (cnt >= d.CAP) {
-                            overflow = true;
-                            continue;
-                        }
-                        const size_t kn = (size_t)cnt * base_bstride + lh;
-                        d.bag_time[kn] = tn;
-                        d.bag_seq[kn] = sq;
-                        d.bag_src[kn] = h;
-                        ++cnt;
-                        continue;
-                    }
-                    if (dst != h && tn < E) {  // host_single.c:180-184
-                        tn = E;
-                        ++ctr[C_BUMPED];
-                    }
-                    const uint32_t slot = atomicAdd(&s_emit, 1u);
-                    if (slot >= d.bcap) {
-                        overflow = true;
-                        continue;
-                    }
-                    const size_t so = (size_t)blockIdx.x * d.bcap + slot;
-                    d.st_time[so] = tn;
-                    d.st_seq[so] = sq;
-                    d.st_dst[so] = dst;
-                    d.st_src[so] = h;
-                    if (d.G > 1) atomicAdd(&s_peer[owner_of(d, dst)], 1u);
-                    ++ctr[C_EMIT];
+                    execute_event(d, E, c, a, bt, bs, bq, &s_emit, s_peer, append);
                 }
             }
             d.bag_cnt[lh] = cnt;
-            d.rng[lh] = rng;
-            d.evc[lh] = ev;
-            d.pops[lh] = pops;
-            d.digest[lh] = dig;
+            d.rng[lh] = c.rng;
+            d.evc[lh] = c.ev;
+            d.pops[lh] = c.pops;
+            d.digest[lh] = c.dig;
             d.hmin[lh] = newmin;
         }
     }
 
-    // block reductions: min next time, discovery min, counters
+    // workgroup partials (transposed [field][block] for a coalesced k_reduce)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t m = wave_min(newmin);
-    uint64_t jm = wave_min(jmin);
-    uint64_t vals[NCTR];
+    uint64_t v[NPART];
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) vals[i] = wave_sum(ctr[i]);
+    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum(a.ctr[i]);
+    v[P_JMIN] = wave_min(a.jmin);
+    v[P_EMIN] = wave_min(a.emin);
+    v[P_RMIN] = wave_min(newmin);
     if (lane == 0) {
-        s_red[wid][0] = m;
-        s_red[wid][1] = jm;
 #pragma unroll
-        for (int i = 0; i < NCTR; ++i) s_red[wid][2 + i] = vals[i];
+        for (int i = 0; i < NPART; ++i) s_red[wid][i] = v[i];
     }
-    if (overflow) atomicOr((unsigned long long*)&d.rs->overflow, 1ULL);
+    if (a.overflow) atomicOr((unsigned long long*)&d.rs->overflow, 1ULL);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t bm = s_red[0][0], bj = s_red[0][1];
-        uint64_t acc[NCTR];
-        for (int i = 0; i < NCTR; ++i) acc[i] = s_red[0][2 + i];
+    if (threadIdx.x < NPART) {
+        const int i = threadIdx.x;
+        uint64_t r = s_red[0][i];
         for (int w = 1; w < BLOCK / 64; ++w) {
-            bm = s_red[w][0] < bm ? s_red[w][0] : bm;
-            bj = s_red[w][1] < bj ? s_red[w][1] : bj;
-            for (int i = 0; i < NCTR; ++i) acc[i] += s_red[w][2 + i];
+            const uint64_t x = s_red[w][i];
+            r = i < NCTR ? r + x : (x < r ? x : r);
         }
-        d.blockmin[blockIdx.x] = bm;
-        uint64_t* p = d.part + (size_t)blockIdx.x * NPART;
-        for (int i = 0; i < NCTR; ++i) p[i] = acc[i];
-        p[NCTR] = bj;
-        const uint32_t ne = s_emit < d.bcap ? s_emit : d.bcap;
-        d.blockcnt[blockIdx.x] = ne;
+        d.part[(size_t)i * d.nblocks + blockIdx.x] = r;
     }
+    if (threadIdx.x == 0) d.blockcnt[blockIdx.x] = s_emit < d.bcap ? s_emit : d.bcap;
     if (d.G > 1 && threadIdx.x < d.G) d.peercnt[(size_t)blockIdx.x * d.G + threadIdx.x] = s_peer[threadIdx.x];
 }
 
 // Multi-shard: exclusive prefix of per-block peer counts (one workgroup).
 __global__ void k_peer_scan(Dev d, int64_t* send_counts) {
     if (d.rs->done) return;
-    __shared__ uint64_t s_tot[MAXG];
     const uint32_t p = threadIdx.x;
     if (p < d.G) {
         uint64_t run = 0;
@@ -414,7 +502,6 @@ __global__ void k_peer_scan(Dev d, int64_t* send_counts) {
             d.peeroff[k] = (uint32_t)run;
             run += d.peercnt[k];
         }
-        s_tot[p] = run;
         send_counts[p] = p == d.g ? 0 : (int64_t)(run < d.xcap ? run : d.xcap);
         if (p != d.g && run > d.xcap) atomicOr((unsigned long long*)&d.rs->overflow, 2ULL);
     }
@@ -454,7 +541,6 @@ __device__ __forceinline__ void deliver(const Dev& d, uint64_t t, uint64_t seq, 
     d.bag_seq[k] = seq;
     d.bag_src[k] = src;
     atomicMin((unsigned long long*)&d.hmin[dl], (unsigned long long)t);
-    atomicMin((unsigned long long*)&d.blockmin[dl / BLOCK], (unsigned long long)t);
 }
 
 // Staged events of this shard's own hosts → destination queues.
@@ -485,56 +571,10 @@ __global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* rec
     }
 }
 
-// Local MIN next time / discovery min / counters (one workgroup of 1024).
-__global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3) {
-    if (d.rs->done) return;
-    __shared__ uint64_t s_m[16], s_j[16], s_c[16][NCTR];
-    uint64_t m = SIMTIME_MAX, j = UINT64_MAX, c[NCTR];
-    for (int i = 0; i < NCTR; ++i) c[i] = 0;
-    for (uint32_t b = threadIdx.x; b < d.nblocks; b += 1024) {
-        const uint64_t bm = d.blockmin[b];
-        m = bm < m ? bm : m;
-        const uint64_t* p = d.part + (size_t)b * NPART;
-        for (int i = 0; i < NCTR; ++i) c[i] += p[i];
-        j = p[NCTR] < j ? p[NCTR] : j;
-    }
-    m = wave_min(m);
-    j = wave_min(j);
-    for (int i = 0; i < NCTR; ++i) c[i] = wave_sum(c[i]);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-        s_m[wid] = m;
-        s_j[wid] = j;
-        for (int i = 0; i < NCTR; ++i) s_c[wid][i] = c[i];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) {
-            m = s_m[w] < m ? s_m[w] : m;
-            j = s_j[w] < j ? s_j[w] : j;
-        }
-        m = s_m[0] < m ? s_m[0] : m;
-        j = s_j[0] < j ? s_j[0] : j;
-        RoundState* rs = d.rs;
-        for (int i = 0; i < NCTR; ++i) {
-            uint64_t t = 0;
-            for (int w = 0; w < 16; ++w) t += s_c[w][i];
-            rs->ctr[i] += t;
-        }
-        j = rs->jmin < j ? rs->jmin : j;
-        rs->jmin = j;
-        out3[0] = m;
-        out3[1] = j;
-        out3[2] = ~rs->overflow;
-    }
-}
-
-// master_slaveFinishedCurrentRound (master.c:450-480) on the reduced triple.
-__global__ void k_window(Dev d, const uint64_t* in3) {
+// master_slaveFinishedCurrentRound (master.c:450-480) on a reduced triple.
+__device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t not_overflow) {
     RoundState* rs = d.rs;
-    if (rs->done) return;
-    const uint64_t minNext = in3[0], jmin = in3[1];
-    rs->overflow |= ~in3[2];
+    rs->overflow |= ~not_overflow;
     rs->rounds += 1;
     rs->last_min = minNext;
     uint64_t jump;
@@ -547,11 +587,61 @@ __global__ void k_window(Dev d, const uint64_t* in3) {
         if (d.runahead_min > 0 && jump < d.runahead_min) jump = d.runahead_min;
     }
     const uint64_t start = minNext;
-    uint64_t end = minNext + jump;
+    uint64_t end = minNext + jump;  // unsigned wrap as in the reference
     if (end > d.end_time) end = d.end_time;
     rs->S = start;
     rs->E = end;
     rs->done = start < end ? 0 : 1;
+}
+
+// Local MIN next time (remaining ∪ staged), discovery min, counters; with
+// apply != 0 (single shard) also the next window.  One workgroup of 1024.
+__global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3, int apply) {
+    if (d.rs->done) return;
+    __shared__ uint64_t s_v[16][NPART];
+    uint64_t v[NPART];
+#pragma unroll
+    for (int i = 0; i < NPART; ++i) v[i] = i < NCTR ? 0 : UINT64_MAX;
+    const size_t NB = d.nblocks;
+    for (uint32_t b = threadIdx.x; b < NB; b += 1024) {
+#pragma unroll
+        for (int i = 0; i < NPART; ++i) {
+            const uint64_t x = d.part[(size_t)i * NB + b];
+            v[i] = i < NCTR ? v[i] + x : (x < v[i] ? x : v[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NPART; ++i) v[i] = i < NCTR ? wave_sum(v[i]) : wave_min(v[i]);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NPART; ++i) s_v[wid][i] = v[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t r[NPART];
+        for (int i = 0; i < NPART; ++i) {
+            r[i] = s_v[0][i];
+            for (int w = 1; w < 16; ++w) {
+                const uint64_t x = s_v[w][i];
+                r[i] = i < NCTR ? r[i] + x : (x < r[i] ? x : r[i]);
+            }
+        }
+        RoundState* rs = d.rs;
+        for (int i = 0; i < NCTR; ++i) rs->ctr[i] += r[i];
+        const uint64_t j = rs->jmin < r[P_JMIN] ? rs->jmin : r[P_JMIN];
+        rs->jmin = j;
+        const uint64_t m = r[P_EMIN] < r[P_RMIN] ? r[P_EMIN] : r[P_RMIN];
+        out3[0] = m;
+        out3[1] = j;
+        out3[2] = ~rs->overflow;
+        if (apply) apply_window(d, m, j, ~rs->overflow);
+    }
+}
+
+__global__ void k_window(Dev d, const uint64_t* in3) {
+    if (d.rs->done) return;
+    apply_window(d, in3[0], in3[1], in3[2]);
 }
 
 __global__ void k_pending(Dev d, unsigned long long* out) {
@@ -696,6 +786,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.L = d.bounds[d.g + 1] - d.lo;
     d.CAP = p.queue_cap ? p.queue_cap : 64;
     if (d.CAP < p.load) d.CAP = p.load;  // a boot event may queue `load` self events
+    d.CAP = (d.CAP + 7u) & ~7u;           // the masked scan reads slots in groups of 8
     d.load = p.load;
     d.dst_rule = p.dst_rule;
     d.window_rule = p.window_rule;
@@ -748,7 +839,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(d.evc, L);
     ALLOC(d.pops, L);
     ALLOC(d.digest, L);
-    ALLOC(d.blockmin, NB);
     ALLOC(d.part, NB * NPART);
     ALLOC(d.blockcnt, NB);
     ALLOC(d.peercnt, NB * G);
@@ -838,7 +928,10 @@ int sg_engine_boot(sg_engine* e) {
 static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
     return timed_launch(e, 0, [&] {
-        hipLaunchKernelGGL(k_process, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+        if (d.CAP <= 64)
+            hipLaunchKernelGGL(k_process<true>, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+        else
+            hipLaunchKernelGGL(k_process<false>, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
     });
 }
 
@@ -863,8 +956,7 @@ int sg_engine_enqueue_round(sg_engine* e) {
     if ((rc = enqueue_local_insert(e))) return rc;
     const Dev& d = e->d;
     return timed_launch(e, 2, [&] {
-        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, d, d.red3);
-        hipLaunchKernelGGL(k_window, dim3(1), dim3(1), 0, e->stream, d, (const uint64_t*)d.red3);
+        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, d, d.red3, 1);
     });
 }
 
@@ -1009,7 +1101,7 @@ int sg_engine_step_insert(sg_engine* e, const int64_t* recv, uint64_t n_recv) {
 
 int sg_engine_step_reduce(sg_engine* e, uint64_t* out3) {
     if (!e || !out3) return SG_ERR_INVAL;
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, e->d, out3);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, e->d, out3, 0);
     HIPCHK(hipGetLastError());
     return SG_OK;
 }

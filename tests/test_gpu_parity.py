@@ -132,3 +132,19 @@ def test_full_size_c4_invariants():
     g, o = eng.host_state(), orc.host_state()
     assert int(g["digest"].sum(dtype=np.uint64)) == int(o["digest"].sum(dtype=np.uint64))
     assert np.array_equal(g["digest"], o["digest"])
+
+
+@pytest.mark.parametrize("cap", [8, 128])
+def test_queue_capacity_paths(cap):
+    """queue_cap <= 64 runs the masked selection, > 64 the rescanning one; a cap
+    of 8 (below PHOLD's per-host peak) must fail loudly, never silently."""
+    cfg = phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.5)
+    if cap == 8:
+        eng = Engine(cfg, queue_cap=cap)
+        eng.boot()
+        with pytest.raises(L.SgError) as ei:
+            eng.run()
+        assert ei.value.code == L.SG_ERR_OVERFLOW
+        return
+    eng, orc = _run_both(cfg, trace=200_000, queue_cap=cap)
+    _assert_same(eng, orc)
