@@ -346,7 +346,8 @@ static void record_window(orc_sim* s) {
 }
 
 int orc_round_process(orc_sim* s) {
-    if (!s->booted || s->done) return -1;
+    if (!s->booted) return -1;
+    if (s->done) return 0; /* rounds after the end are no-ops, as on the device */
     record_window(s);
     uint64_t E = s->E;
     for (uint32_t li = 0; li < s->p.n_local; li++) {
@@ -388,6 +389,7 @@ uint64_t orc_local_jmin(orc_sim* s) { return s->jmin; }
 
 /* master_slaveFinishedCurrentRound (master.c:450-480). */
 int orc_window_apply(orc_sim* s, uint64_t global_min, uint64_t global_jmin) {
+    if (s->done) return 0;
     if (s->p.window_rule == ORC_WINDOW_DISCOVERED && global_jmin != UINT64_MAX) {
         /* topology.c:1374-1385 → master_updateMinTimeJump (master.c:148-159):
          * nextMinJumpTime = (SimulationTime)minPathLatency * 1ms; the running
