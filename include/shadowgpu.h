@@ -235,6 +235,102 @@ int sg_engine_step_window(sg_engine* e, const uint64_t* in3);
 int sg_engine_kernel_times(sg_engine* e, double* ms3, uint64_t* launches);
 int sg_engine_set_timing(sg_engine* e, int enabled);
 
+/* ------------------------------------------------------------------------ */
+/* 3. The `gpu` SchedulerPolicy ("Mode P", the drop-in boundary)            */
+/* ------------------------------------------------------------------------ */
+/* Replaces a SchedulerPolicy's data + function pointers
+ * (core/scheduler/scheduler_policy.h:31-51) for a new SP_PARALLEL_GPU type;
+ * INTEGRATION.md gives the Shadow-side scheduler_policy_gpu.c that maps
+ * Host* / Event* onto these calls.  Threads are identified by an opaque token
+ * (pthread_self() in Shadow).  Events are identified by an opaque nonzero
+ * handle (the Event* in Shadow); the policy never dereferences it.
+ *
+ * Per round: push stages inter-host (and future self) events per thread with
+ * no lock; self events before the barrier go to a per-host CPU heap (they must
+ * be popped in this round, host_single.c:237-267).  The last worker to call
+ * next_time flushes the staged events to HBM (k_pol_insert) and reduces the
+ * MIN next time on the device.  The first pop of the next round extracts, on
+ * the device, every queued event before the new barrier sorted per host in
+ * event_compare order (k_pol_extract); pops merge that run with the host's CPU
+ * heap. */
+typedef struct sg_policy sg_policy;
+
+typedef struct sg_policy_params {
+    uint32_t n_threads;   /* worker threads that call push/pop/next_time (nWorkers) */
+    uint32_t max_hosts;   /* hosts that will be added */
+    uint32_t queue_cap;   /* initial HBM event slots per host (0 = 64; grows on demand) */
+    int device;           /* HIP device */
+} sg_policy_params;
+
+int sg_policy_create(const sg_policy_params* params, sg_policy** out);
+int sg_policy_destroy(sg_policy* p);
+/* addHost (host_single.c:120-140): host_id is the host's GQuark, which orders
+ * hosts in event_compare (host.c:439-445). */
+int sg_policy_add_host(sg_policy* p, uint32_t host_id, uint64_t thread_token);
+/* getAssignedHosts (host_single.c:146-165): host ids of the thread's hosts. */
+int sg_policy_thread_hosts(sg_policy* p, uint64_t thread_token, uint32_t* ids_out,
+                           uint32_t capacity, uint32_t* n_out);
+/* push (host_single.c:167-208): returns in *time_out the event's time after the
+ * barrier bump; the caller stores it in the event (event_setTime). */
+int sg_policy_push(sg_policy* p, uint64_t thread_token, uint64_t handle, sg_simtime time,
+                   uint32_t src_host_id, uint32_t dst_host_id, uint64_t src_event_id,
+                   sg_simtime barrier, sg_simtime* time_out);
+/* pop (host_single.c:210-271): *handle_out = 0 when the thread has no event
+ * before the barrier. */
+int sg_policy_pop(sg_policy* p, uint64_t thread_token, sg_simtime barrier, uint64_t* handle_out);
+/* getNextTime (host_single.c:273-305): every worker calls it once per round
+ * after the execute barrier; returns the MIN next event time (SG_SIMTIME_MAX
+ * when every queue is empty). */
+int sg_policy_next_time(sg_policy* p, uint64_t thread_token, sg_simtime* next_out);
+/* Events still queued (for unref at free, host_single.c:104). */
+int sg_policy_remaining(sg_policy* p, uint64_t* handles_out, uint64_t capacity, uint64_t* n_out);
+
+/* ------------------------------------------------------------------------ */
+/* 4. Shadow-style round driver for running a policy outside Shadow          */
+/* ------------------------------------------------------------------------ */
+/* A C restatement of scheduler.c's round API + worker.c's loop (threads, the
+ * execute / collect / prepare barriers, scheduler_push's endTime drop) that
+ * drives any policy through the SchedulerPolicy-shaped vtable below, with the
+ * synthetic PHOLD body executed by the CPU workers.  In Shadow itself
+ * scheduler.c and worker.c play this role. */
+typedef struct sg_hevent {
+    sg_simtime time;
+    uint64_t seq;    /* srcHostEventID */
+    uint32_t src;    /* host index */
+    uint32_t dst;
+} sg_hevent;
+
+typedef struct sg_sched_policy_ops {   /* mirrors struct _SchedulerPolicy */
+    void* data;
+    void (*add_host)(void* data, uint32_t host, uint64_t thread_token);
+    uint32_t (*get_assigned_hosts)(void* data, uint64_t thread_token, uint32_t* out, uint32_t cap);
+    void (*push)(void* data, sg_hevent* ev, uint32_t src, uint32_t dst, sg_simtime barrier);
+    sg_hevent* (*pop)(void* data, sg_simtime barrier);
+    sg_simtime (*get_next_time)(void* data);
+    void (*free)(void* data);
+} sg_sched_policy_ops;
+
+typedef struct sg_sched_result {
+    uint64_t rounds, pops, sends, drop_reliability, drop_endtime, bumped;
+    double seconds;          /* wall time of the round loop (worker.c:165-176 semantics) */
+    sg_simtime last_window_start, last_window_end;
+} sg_sched_result;
+
+/* The gpu policy as a vtable (data = a new sg_policy on `device`); release it
+ * with ops->free(ops->data) (the SchedulerPolicy free, scheduler.c:276). */
+int sg_policy_ops_gpu(uint32_t n_threads, uint32_t max_hosts, int device, sg_sched_policy_ops* out);
+/* First error the gpu vtable's callbacks hit (their signatures return void). */
+int sg_policy_ops_gpu_error(const sg_sched_policy_ops* ops);
+
+/* Run the PHOLD workload with n_workers threads (>= 1) under `ops` (not freed).
+ * max_rounds bounds the run; per-host digests / pops / rng / event counters
+ * are written if the pointers are non-NULL.  Host->thread assignment is the
+ * reference's shuffle (scheduler.c:437-531) seeded from the seed chain. */
+int sg_sched_run_phold(const sg_phold_params* params, const sg_phold_tables* tables,
+                       uint32_t n_workers, uint32_t scheduler_seed, const sg_sched_policy_ops* ops,
+                       uint64_t max_rounds, sg_sched_result* result, uint64_t* digest,
+                       uint64_t* pops, uint32_t* rng, uint64_t* event_counter);
+
 #ifdef __cplusplus
 }
 #endif

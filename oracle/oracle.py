@@ -248,3 +248,17 @@ class Sim:
 
 def digest_mix(pos, time, src, seq) -> int:
     return lib().orc_digest_mix(pos, time, src, seq)
+
+
+# --------------------------------------------------- CPU policies (baseline) --
+def cpu_policy_ops(steal: bool, n_threads: int, n_hosts: int):
+    """host_steal / host_single restatements (oracle/host_steal.c) as a
+    shadow_amd.policy.PolicyOps vtable, for the Shadow-style round driver."""
+    from shadow_amd.policy import PolicyOps
+    L = lib()
+    L.orc_policy_ops_cpu.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(PolicyOps)]
+    ops = PolicyOps()
+    if L.orc_policy_ops_cpu(int(steal), n_threads, n_hosts, C.byref(ops)) != 0:
+        raise RuntimeError("orc_policy_ops_cpu failed")
+    ops._owner = "cpu"
+    return ops

@@ -76,7 +76,9 @@ EXPORTS = [
     "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace",
     "sg_engine_stream", "sg_engine_step_process", "sg_engine_step_insert",
     "sg_engine_step_reduce", "sg_engine_step_window", "sg_engine_kernel_times",
-    "sg_engine_set_timing",
+    "sg_engine_set_timing", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
+    "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
+    "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
 ]
 
 

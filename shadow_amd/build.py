@@ -22,10 +22,10 @@ ARCH = "gfx950"
 C_FLAGS = ["-O2", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
            "-Wextra", "-Wno-unused-parameter", "-I" + INC]
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
-             "-fno-fast-math", "-Wall", "-I" + INC]
+             "-fno-fast-math", "-Wall", "-I" + INC, "-I" + CSRC]
 
-C_SOURCES = ["sg_host.c"]
-HIP_SOURCES = ["sg_engine.hip"]
+C_SOURCES = ["sg_host.c", "sg_policy.c", "sg_sched.c"]
+HIP_SOURCES = ["sg_engine.hip", "sg_policy_dev.hip"]
 
 
 def _run(cmd, verbose):

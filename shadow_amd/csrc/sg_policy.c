@@ -1,0 +1,442 @@
+/*
+ * sg_policy.c — host half of the `gpu` SchedulerPolicy (include/shadowgpu.h §3).
+ *
+ * Semantics follow scheduler_policy_host_single.c (the host-family policies
+ * whose per-host pop sequences are independent of the worker count):
+ *   push     barrier bump for inter-host events (host_single.c:180-184); self
+ *            events before the barrier stay on the CPU in a per-host heap because
+ *            they must be popped in this same round; everything else is staged
+ *            in the pushing thread's arena (no lock) for the end-of-round flush.
+ *   pop      per thread, hosts in assignment order (host_single.c:222-267): the
+ *            host's device-extracted run merged with its CPU heap, in
+ *            event_compare order (event.c:110-153), while time < barrier.
+ *   next     every worker arrives (after scheduler.c:386's execute barrier); the
+ *            last one delivers all staged events to HBM and reduces the MIN
+ *            (host_single.c:273-305, scheduler.c:393-398).
+ *   prepare  the first pop with a new barrier extracts, on the device, every
+ *            queued event before it, sorted per host.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "sg_policy_dev.h"
+#include "shadowgpu.h"
+
+void sg_set_error(const char* fmt, ...);
+
+/* ---------------------------------------------------------------- heap --- */
+typedef struct sheap {      /* same-round self events of one host: src = dst */
+    sgp_rec* a;
+    uint32_t n, cap;
+} sheap;
+
+static int rec_less(const sgp_rec* a, const sgp_rec* b) { /* event_compare, equal dst */
+    if (a->time != b->time) return a->time < b->time;
+    if (a->src_id != b->src_id) return a->src_id < b->src_id;
+    return a->seq < b->seq;
+}
+
+static int sheap_push(sheap* h, const sgp_rec* r) {
+    if (h->n == h->cap) {
+        uint32_t nc = h->cap ? 2 * h->cap : 8;
+        sgp_rec* na = (sgp_rec*)realloc(h->a, (size_t)nc * sizeof *na);
+        if (!na) return -1;
+        h->a = na;
+        h->cap = nc;
+    }
+    uint32_t i = h->n++;
+    h->a[i] = *r;
+    while (i) {
+        uint32_t p = (i - 1) / 2;
+        if (!rec_less(&h->a[i], &h->a[p])) break;
+        sgp_rec t = h->a[i];
+        h->a[i] = h->a[p];
+        h->a[p] = t;
+        i = p;
+    }
+    return 0;
+}
+
+static void sheap_pop(sheap* h) {
+    h->a[0] = h->a[--h->n];
+    uint32_t i = 0;
+    for (;;) {
+        uint32_t c = 2 * i + 1;
+        if (c >= h->n) break;
+        if (c + 1 < h->n && rec_less(&h->a[c + 1], &h->a[c])) c++;
+        if (!rec_less(&h->a[c], &h->a[i])) break;
+        sgp_rec t = h->a[i];
+        h->a[i] = h->a[c];
+        h->a[c] = t;
+        i = c;
+    }
+}
+
+/* ---------------------------------------------------------------- state -- */
+typedef struct host_rt {
+    uint32_t id;              /* GQuark */
+    uint32_t thread;          /* owning thread slot */
+    uint32_t run_off, run_len, run_pos;
+    pthread_mutex_t lock;
+    sheap selfq;
+    int in_self_list;
+} host_rt;
+
+typedef struct thread_rt {
+    uint64_t token;
+    uint32_t* hosts;
+    uint32_t n, cap, cursor;
+    sg_simtime cur_barrier;
+    sgp_rec* arena;
+    uint64_t na, ca;
+} thread_rt;
+
+struct sg_policy {
+    sg_policy_params prm;
+    sgp_dev* dev;
+    host_rt* hosts;
+    uint32_t n_hosts;
+    uint32_t* map_key;        /* open addressing: host id -> index + 1 */
+    uint32_t* map_val;
+    uint32_t map_cap;
+    thread_rt* threads;
+    uint32_t n_threads;
+    pthread_mutex_t foreign_lock; /* pushes from threads that own no host */
+    sgp_rec* foreign;
+    uint64_t nf, cf;
+    /* round state */
+    pthread_mutex_t m;
+    pthread_cond_t cv;
+    sg_simtime prepared;      /* barrier the current runs were extracted for */
+    int preparing;
+    uint32_t arrivals;
+    uint64_t gen;
+    sg_simtime next_min;
+    int error;
+    const sgp_rec* runs;
+    uint32_t* self_list;      /* hosts whose CPU heap may hold events */
+    uint32_t n_self;
+    pthread_mutex_t self_lock;
+};
+
+static uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+static int64_t host_index(const sg_policy* p, uint32_t id) {
+    uint32_t mask = p->map_cap - 1, i = hash32(id) & mask;
+    for (;;) {
+        uint32_t v = p->map_val[i];
+        if (v == 0) return -1;
+        if (p->map_key[i] == id) return (int64_t)v - 1;
+        i = (i + 1) & mask;
+    }
+}
+
+static thread_rt* thread_of(sg_policy* p, uint64_t token) {
+    for (uint32_t i = 0; i < p->n_threads; i++)
+        if (p->threads[i].token == token) return &p->threads[i];
+    return NULL;
+}
+
+int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
+    if (!prm || !out || prm->n_threads == 0 || prm->max_hosts == 0) {
+        sg_set_error("sg_policy_create: bad parameters");
+        return SG_ERR_INVAL;
+    }
+    *out = NULL;
+    sg_policy* p = (sg_policy*)calloc(1, sizeof *p);
+    if (!p) return SG_ERR_NOMEM;
+    p->prm = *prm;
+    p->hosts = (host_rt*)calloc(prm->max_hosts, sizeof(host_rt));
+    p->map_cap = 16;
+    while (p->map_cap < 2 * prm->max_hosts) p->map_cap <<= 1;
+    p->map_key = (uint32_t*)calloc(p->map_cap, 4);
+    p->map_val = (uint32_t*)calloc(p->map_cap, 4);
+    p->threads = (thread_rt*)calloc(prm->n_threads + 1, sizeof(thread_rt));
+    p->self_list = (uint32_t*)malloc((size_t)prm->max_hosts * 4);
+    if (!p->hosts || !p->map_key || !p->map_val || !p->threads || !p->self_list) {
+        sg_policy_destroy(p);
+        return SG_ERR_NOMEM;
+    }
+    int rc = sgp_dev_create(prm->device, prm->max_hosts, prm->queue_cap, &p->dev);
+    if (rc) {
+        sg_policy_destroy(p);
+        return rc;
+    }
+    pthread_mutex_init(&p->m, NULL);
+    pthread_cond_init(&p->cv, NULL);
+    pthread_mutex_init(&p->foreign_lock, NULL);
+    pthread_mutex_init(&p->self_lock, NULL);
+    p->prepared = SG_SIMTIME_INVALID;
+    *out = p;
+    return SG_OK;
+}
+
+int sg_policy_destroy(sg_policy* p) {
+    if (!p) return SG_OK;
+    if (p->dev) sgp_dev_destroy(p->dev);
+    if (p->hosts)
+        for (uint32_t i = 0; i < p->n_hosts; i++) {
+            free(p->hosts[i].selfq.a);
+            pthread_mutex_destroy(&p->hosts[i].lock);
+        }
+    if (p->threads)
+        for (uint32_t i = 0; i < p->n_threads; i++) {
+            free(p->threads[i].hosts);
+            free(p->threads[i].arena);
+        }
+    free(p->hosts);
+    free(p->map_key);
+    free(p->map_val);
+    free(p->threads);
+    free(p->foreign);
+    free(p->self_list);
+    free(p);
+    return SG_OK;
+}
+
+int sg_policy_add_host(sg_policy* p, uint32_t host_id, uint64_t token) {
+    if (!p || p->n_hosts >= p->prm.max_hosts || host_index(p, host_id) >= 0) {
+        sg_set_error("sg_policy_add_host: capacity exceeded or duplicate host %u", host_id);
+        return SG_ERR_INVAL;
+    }
+    thread_rt* t = thread_of(p, token);
+    if (!t) {
+        if (p->n_threads >= p->prm.n_threads) {
+            sg_set_error("sg_policy_add_host: more than %u worker threads", p->prm.n_threads);
+            return SG_ERR_INVAL;
+        }
+        t = &p->threads[p->n_threads++];
+        t->token = token;
+    }
+    if (t->n == t->cap) {
+        uint32_t nc = t->cap ? 2 * t->cap : 64;
+        uint32_t* nh = (uint32_t*)realloc(t->hosts, (size_t)nc * 4);
+        if (!nh) return SG_ERR_NOMEM;
+        t->hosts = nh;
+        t->cap = nc;
+    }
+    uint32_t idx = p->n_hosts++;
+    host_rt* h = &p->hosts[idx];
+    memset(h, 0, sizeof *h);
+    h->id = host_id;
+    h->thread = (uint32_t)(t - p->threads);
+    pthread_mutex_init(&h->lock, NULL);
+    t->hosts[t->n++] = idx;
+    uint32_t mask = p->map_cap - 1, i = hash32(host_id) & mask;
+    while (p->map_val[i]) i = (i + 1) & mask;
+    p->map_key[i] = host_id;
+    p->map_val[i] = idx + 1;
+    return SG_OK;
+}
+
+int sg_policy_thread_hosts(sg_policy* p, uint64_t token, uint32_t* ids, uint32_t cap, uint32_t* n) {
+    thread_rt* t = thread_of(p, token);
+    uint32_t c = t ? t->n : 0;
+    for (uint32_t i = 0; i < c && i < cap; i++) ids[i] = p->hosts[t->hosts[i]].id;
+    if (n) *n = c;
+    return SG_OK;
+}
+
+static int arena_push(sgp_rec** a, uint64_t* n, uint64_t* c, const sgp_rec* r) {
+    if (*n == *c) {
+        uint64_t nc = *c ? 2 * *c : 1024;
+        sgp_rec* na = (sgp_rec*)realloc(*a, nc * sizeof(sgp_rec));
+        if (!na) return -1;
+        *a = na;
+        *c = nc;
+    }
+    (*a)[(*n)++] = *r;
+    return 0;
+}
+
+int sg_policy_push(sg_policy* p, uint64_t token, uint64_t handle, sg_simtime time, uint32_t src_id,
+                   uint32_t dst_id, uint64_t src_event_id, sg_simtime barrier, sg_simtime* time_out) {
+    int64_t di = host_index(p, dst_id);
+    if (di < 0 || handle == 0) {
+        sg_set_error("sg_policy_push: unknown destination host %u or null handle", dst_id);
+        return SG_ERR_INVAL;
+    }
+    if (src_id != dst_id && time < barrier) time = barrier; /* host_single.c:180-184 */
+    if (time_out) *time_out = time;
+    sgp_rec r = {time, src_event_id, handle, src_id, (uint32_t)di};
+    if (src_id == dst_id && time < barrier) {
+        host_rt* h = &p->hosts[di];
+        pthread_mutex_lock(&h->lock);
+        int rc = sheap_push(&h->selfq, &r);
+        int add = !h->in_self_list;
+        h->in_self_list = 1;
+        pthread_mutex_unlock(&h->lock);
+        if (add) {
+            pthread_mutex_lock(&p->self_lock);
+            p->self_list[p->n_self++] = (uint32_t)di;
+            pthread_mutex_unlock(&p->self_lock);
+        }
+        return rc ? SG_ERR_NOMEM : SG_OK;
+    }
+    thread_rt* t = thread_of(p, token);
+    int rc;
+    if (t) {
+        rc = arena_push(&t->arena, &t->na, &t->ca, &r);
+    } else {
+        pthread_mutex_lock(&p->foreign_lock);
+        rc = arena_push(&p->foreign, &p->nf, &p->cf, &r);
+        pthread_mutex_unlock(&p->foreign_lock);
+    }
+    return rc ? SG_ERR_NOMEM : SG_OK;
+}
+
+/* Extract the runs for `barrier` once; other threads wait for the leader. */
+static int prepare(sg_policy* p, sg_simtime barrier) {
+    pthread_mutex_lock(&p->m);
+    while (p->prepared != barrier && p->preparing) pthread_cond_wait(&p->cv, &p->m);
+    if (p->prepared != barrier && !p->error) {
+        p->preparing = 1;
+        pthread_mutex_unlock(&p->m);
+        const sgp_rec* runs;
+        const uint32_t *off, *cnt;
+        uint64_t total;
+        int rc = sgp_dev_extract(p->dev, barrier, &runs, &off, &cnt, &total);
+        if (rc == 0) {
+            p->runs = runs;
+            for (uint32_t i = 0; i < p->n_hosts; i++) {
+                p->hosts[i].run_off = off[i];
+                p->hosts[i].run_len = cnt[i];
+                p->hosts[i].run_pos = 0;
+            }
+        }
+        pthread_mutex_lock(&p->m);
+        if (rc) p->error = rc;
+        p->prepared = barrier;
+        p->preparing = 0;
+        pthread_cond_broadcast(&p->cv);
+    }
+    int err = p->error;
+    pthread_mutex_unlock(&p->m);
+    return err;
+}
+
+int sg_policy_pop(sg_policy* p, uint64_t token, sg_simtime barrier, uint64_t* handle_out) {
+    *handle_out = 0;
+    if (__atomic_load_n(&p->prepared, __ATOMIC_ACQUIRE) != barrier) {
+        int rc = prepare(p, barrier);
+        if (rc) return rc;
+    }
+    thread_rt* t = thread_of(p, token);
+    if (!t) return SG_OK; /* this thread was assigned no host */
+    if (barrier > t->cur_barrier) { /* host_single.c:222-235: all hosts unprocessed again */
+        t->cur_barrier = barrier;
+        t->cursor = 0;
+    }
+    while (t->cursor < t->n) {
+        host_rt* h = &p->hosts[t->hosts[t->cursor]];
+        pthread_mutex_lock(&h->lock);
+        const sgp_rec* a = h->run_pos < h->run_len ? &p->runs[h->run_off + h->run_pos] : NULL;
+        const sgp_rec* b = (h->selfq.n && h->selfq.a[0].time < barrier) ? &h->selfq.a[0] : NULL;
+        uint64_t handle = 0;
+        if (a && (!b || rec_less(a, b))) {
+            handle = a->handle;
+            h->run_pos++;
+        } else if (b) {
+            handle = b->handle;
+            sheap_pop(&h->selfq);
+        }
+        pthread_mutex_unlock(&h->lock);
+        if (handle) {
+            *handle_out = handle;
+            return SG_OK;
+        }
+        t->cursor++; /* host done for this round (host_single.c:266) */
+    }
+    return SG_OK;
+}
+
+/* Last arriver: deliver every staged event (and left-over CPU heap entries) to
+ * HBM, then reduce the MIN. */
+static int flush(sg_policy* p) {
+    uint64_t total = p->nf;
+    for (uint32_t i = 0; i < p->n_threads; i++) total += p->threads[i].na;
+    for (uint32_t k = 0; k < p->n_self; k++) total += p->hosts[p->self_list[k]].selfq.n;
+    sgp_rec* all = (sgp_rec*)malloc((total ? total : 1) * sizeof(sgp_rec));
+    if (!all) return SG_ERR_NOMEM;
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < p->n_threads; i++) {
+        thread_rt* t = &p->threads[i];
+        memcpy(all + n, t->arena, t->na * sizeof(sgp_rec));
+        n += t->na;
+        t->na = 0;
+    }
+    memcpy(all + n, p->foreign, p->nf * sizeof(sgp_rec));
+    n += p->nf;
+    p->nf = 0;
+    for (uint32_t k = 0; k < p->n_self; k++) {
+        host_rt* h = &p->hosts[p->self_list[k]];
+        memcpy(all + n, h->selfq.a, h->selfq.n * sizeof(sgp_rec));
+        n += h->selfq.n;
+        h->selfq.n = 0;
+        h->in_self_list = 0;
+    }
+    p->n_self = 0;
+    int rc = sgp_dev_insert(p->dev, all, n);
+    free(all);
+    if (rc) return rc;
+    return sgp_dev_min(p->dev, &p->next_min);
+}
+
+int sg_policy_next_time(sg_policy* p, uint64_t token, sg_simtime* next_out) {
+    (void)token;
+    pthread_mutex_lock(&p->m);
+    uint64_t my_gen = p->gen;
+    if (++p->arrivals == p->prm.n_threads) {
+        int rc = flush(p);
+        if (rc) p->error = rc;
+        p->arrivals = 0;
+        p->gen++;
+        p->prepared = SG_SIMTIME_INVALID; /* queues changed: runs must be re-extracted */
+        pthread_cond_broadcast(&p->cv);
+    } else {
+        while (p->gen == my_gen) pthread_cond_wait(&p->cv, &p->m);
+    }
+    int err = p->error;
+    *next_out = p->next_min;
+    pthread_mutex_unlock(&p->m);
+    return err;
+}
+
+int sg_policy_remaining(sg_policy* p, uint64_t* handles, uint64_t cap, uint64_t* n_out) {
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < p->n_threads; i++)
+        for (uint64_t k = 0; k < p->threads[i].na; k++, n++)
+            if (n < cap) handles[n] = p->threads[i].arena[k].handle;
+    for (uint64_t k = 0; k < p->nf; k++, n++)
+        if (n < cap) handles[n] = p->foreign[k].handle;
+    for (uint32_t i = 0; i < p->n_hosts; i++) {
+        host_rt* h = &p->hosts[i];
+        for (uint32_t k = 0; k < h->selfq.n; k++, n++)
+            if (n < cap) handles[n] = h->selfq.a[k].handle;
+        for (uint32_t k = h->run_pos; k < h->run_len; k++, n++)
+            if (n < cap) handles[n] = p->runs[h->run_off + k].handle;
+    }
+    uint64_t nd = 0;
+    sgp_rec* tmp = NULL;
+    int rc = sgp_dev_all(p->dev, NULL, 0, &nd);
+    if (rc) return rc;
+    if (nd) {
+        tmp = (sgp_rec*)malloc(nd * sizeof(sgp_rec));
+        if (!tmp) return SG_ERR_NOMEM;
+        rc = sgp_dev_all(p->dev, tmp, nd, &nd);
+        for (uint64_t k = 0; k < nd; k++, n++)
+            if (n < cap) handles[n] = tmp[k].handle;
+        free(tmp);
+    }
+    if (n_out) *n_out = n;
+    return rc;
+}

@@ -1,0 +1,370 @@
+/*
+ * sg_sched.c — Shadow-style round driver (include/shadowgpu.h §4) and the
+ * `gpu` policy as a SchedulerPolicy-shaped vtable.
+ *
+ * Restates, for running a policy outside Shadow:
+ *   scheduler_new/start/continueNextRound/awaitNextRound/finish
+ *                          core/scheduler/scheduler.c:115-221, 604-672
+ *   scheduler_push/pop     scheduler.c:339-414 (endTime drop; execute / collect /
+ *                          prepare barriers; MIN of getNextTime under a lock)
+ *   host assignment        scheduler.c:437-531 (Fisher-Yates on the scheduler
+ *                          Random, then round-robin over the workers)
+ *   worker loop            core/worker.c:149-216
+ *   round loop / windows   core/slave.c:413-466, core/master.c:133-159, 450-480
+ * with the synthetic PHOLD body (shadow_amd/phold.py) run by the CPU workers.
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "shadowgpu.h"
+
+void sg_set_error(const char* fmt, ...);
+
+typedef struct drv drv;
+
+typedef struct wctx {
+    drv* d;
+    uint32_t index;
+    pthread_t th;
+    uint64_t token;
+    uint64_t pops, sends, dropr, drope;
+    uint64_t jmin;
+    sg_simtime now;
+} wctx;
+
+struct drv {
+    sg_phold_params P;
+    const sg_phold_tables* T;
+    uint32_t N, V;
+    uint32_t* rng;
+    uint64_t *evc, *pops, *digest;
+    const sg_sched_policy_ops* ops;
+    uint32_t nw;
+    wctx* w;
+    pthread_barrier_t start_b, exec_b, collect_b, prepare_b;
+    volatile int running;
+    sg_simtime round_end;  /* scheduler->currentRound.endTime */
+    sg_simtime min_next;
+    pthread_mutex_t glock;
+    uint64_t bumped;       /* counted by the driver's own bump detection */
+};
+
+static uint64_t digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
+#define FMIX(z) (z ^= z >> 33, z *= 0xff51afd7ed558ccdULL, z ^= z >> 33, z *= 0xc4ceb9fe1a85ec53ULL, z ^= z >> 33)
+    uint64_t z = pos + 0x9E3779B97F4A7C15ULL;
+    FMIX(z);
+    z ^= time;
+    FMIX(z);
+    z ^= (uint64_t)src;
+    FMIX(z);
+    z ^= seq;
+    FMIX(z);
+    return z;
+#undef FMIX
+}
+
+static uint32_t choose_dst(const drv* d, int32_t x) {
+    const uint32_t N = d->N;
+    if (d->P.dst_rule == SG_DST_UNIFORM_FLOOR) {
+        double r = (double)x / (double)SG_RAND_MAX;
+        uint32_t v = (uint32_t)floor(r * N);
+        return v >= N ? N - 1 : v;
+    }
+    const int32_t* w = d->T->weight_thresh;
+    if (x > w[N - 1]) return N;
+    uint32_t lo = 0, hi = N - 1;
+    while (lo < hi) {
+        uint32_t mid = lo + (hi - lo) / 2;
+        if (x <= w[mid]) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+/* scheduler_push (scheduler.c:339-357) */
+static void sched_push(drv* d, wctx* w, sg_hevent* e, uint32_t src, uint32_t dst) {
+    if (e->time >= d->P.end_time) {
+        free(e);
+        w->drope++;
+        return;
+    }
+    sg_simtime before = e->time;
+    d->ops->push(d->ops->data, e, src, dst, d->round_end);
+    if (src != dst && before < d->round_end) __atomic_add_fetch(&d->bumped, 1, __ATOMIC_RELAXED);
+}
+
+/* event_execute → the PHOLD task (worker.c:165-176) */
+static void execute(drv* d, wctx* w, sg_hevent* e) {
+    const uint32_t h = e->dst;
+    w->now = e->time;
+    d->digest[h] += digest_mix(d->pops[h]++, e->time, e->src, e->seq);
+    w->pops++;
+    const int boot = (e->src == h && e->seq == 0);
+    const uint32_t nsend = boot ? d->P.load : 1;
+    for (uint32_t m = 0; m < nsend; m++) {
+        int32_t x = sg_rand_r(&d->rng[h]);
+        uint32_t dst = choose_dst(d, x);
+        if (dst >= d->N) continue;
+        w->sends++;
+        size_t pair = (size_t)d->T->host_vertex[h] * d->V + d->T->host_vertex[dst];
+        uint64_t jm = d->T->jump_ms[pair];
+        if (jm < w->jmin) w->jmin = jm;
+        int32_t c = sg_rand_r(&d->rng[h]);
+        if (!(e->time < d->P.bootstrap_end || c <= d->T->keep_max[pair])) {
+            w->dropr++;
+            continue;
+        }
+        sg_hevent* n = (sg_hevent*)malloc(sizeof *n);
+        n->time = e->time + d->T->delay_ns[pair];
+        n->seq = d->evc[h]++;
+        n->src = h;
+        n->dst = dst;
+        sched_push(d, w, n, h, dst);
+    }
+}
+
+/* scheduler_pop (scheduler.c:359-414) */
+static sg_hevent* sched_pop(drv* d) {
+    while (d->running) {
+        sg_hevent* e = d->ops->pop(d->ops->data, d->round_end);
+        if (e) return e;
+        pthread_barrier_wait(&d->exec_b);
+        sg_simtime t = d->ops->get_next_time(d->ops->data);
+        pthread_mutex_lock(&d->glock);
+        if (t < d->min_next) d->min_next = t;
+        pthread_mutex_unlock(&d->glock);
+        pthread_barrier_wait(&d->collect_b);
+        pthread_barrier_wait(&d->prepare_b);
+    }
+    return NULL;
+}
+
+static void* worker_run(void* arg) {
+    wctx* w = (wctx*)arg;
+    drv* d = w->d;
+    w->token = (uint64_t)pthread_self();
+    pthread_barrier_wait(&d->start_b); /* scheduler_awaitStart */
+    /* _scheduler_startHosts → worker_bootHosts: one boot self event per host */
+    uint32_t* mine = (uint32_t*)malloc((size_t)d->N * 4);
+    uint32_t n = d->ops->get_assigned_hosts(d->ops->data, w->token, mine, d->N);
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t h = mine[i];
+        sg_hevent* e = (sg_hevent*)malloc(sizeof *e);
+        e->time = 0;
+        e->seq = d->evc[h]++;
+        e->src = h;
+        e->dst = h;
+        sched_push(d, w, e, h, h);
+    }
+    free(mine);
+    pthread_barrier_wait(&d->prepare_b);
+    sg_hevent* e;
+    while ((e = sched_pop(d)) != NULL) {
+        execute(d, w, e);
+        free(e);
+    }
+    return NULL;
+}
+
+int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint32_t n_workers,
+                       uint32_t scheduler_seed, const sg_sched_policy_ops* ops, uint64_t max_rounds,
+                       sg_sched_result* res, uint64_t* digest, uint64_t* pops, uint32_t* rng,
+                       uint64_t* event_counter) {
+    if (!P || !T || !ops || n_workers == 0 || P->n_hosts == 0 ||
+        (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh)) {
+        sg_set_error("sg_sched_run_phold: bad arguments");
+        return SG_ERR_INVAL;
+    }
+    drv D;
+    memset(&D, 0, sizeof D);
+    drv* d = &D;
+    d->P = *P;
+    d->T = T;
+    d->N = P->n_hosts;
+    d->V = P->n_vertices;
+    d->ops = ops;
+    d->nw = n_workers;
+    d->rng = (uint32_t*)malloc((size_t)d->N * 4);
+    d->evc = (uint64_t*)calloc(d->N, 8);
+    d->pops = (uint64_t*)calloc(d->N, 8);
+    d->digest = (uint64_t*)calloc(d->N, 8);
+    d->w = (wctx*)calloc(n_workers, sizeof(wctx));
+    uint32_t* order = (uint32_t*)malloc((size_t)d->N * 4);
+    if (!d->rng || !d->evc || !d->pops || !d->digest || !d->w || !order) {
+        sg_set_error("sg_sched_run_phold: out of memory");
+        return SG_ERR_NOMEM;
+    }
+    memcpy(d->rng, T->host_rng, (size_t)d->N * 4);
+    pthread_barrier_init(&d->start_b, NULL, n_workers + 1);
+    pthread_barrier_init(&d->exec_b, NULL, n_workers + 1);
+    pthread_barrier_init(&d->collect_b, NULL, n_workers + 1);
+    pthread_barrier_init(&d->prepare_b, NULL, n_workers + 1);
+    pthread_mutex_init(&d->glock, NULL);
+    d->round_end = P->end_time; /* scheduler.c:130 */
+    d->min_next = SG_SIMTIME_MAX;
+    d->running = 1;
+    for (uint32_t i = 0; i < n_workers; i++) {
+        d->w[i].d = d;
+        d->w[i].index = i;
+        d->w[i].jmin = UINT64_MAX;
+        pthread_create(&d->w[i].th, NULL, worker_run, &d->w[i]);
+    }
+    /* _scheduler_assignHosts (scheduler.c:488-531) */
+    for (uint32_t i = 0; i < d->N; i++) order[i] = i;
+    if (n_workers > 1 && d->N > 1) {
+        uint32_t r = scheduler_seed;
+        for (uint32_t i = 0; i < d->N - 1; i++) { /* scheduler.c:454-466 */
+            double f = sg_random_next_double(&r);
+            double range = (double)(d->N - i);
+            uint32_t j = (uint32_t)floor(f * range);
+            if (j == d->N - i) j--;
+            uint32_t t = order[i];
+            order[i] = order[i + j];
+            order[i + j] = t;
+        }
+    }
+    for (uint32_t k = 0; k < d->N; k++)
+        ops->add_host(ops->data, order[k], (uint64_t)d->w[n_workers > 1 ? k % n_workers : 0].th);
+    free(order);
+
+    struct timespec t0, t1;
+    pthread_barrier_wait(&d->start_b); /* scheduler_start */
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    sg_window_state ws;
+    memset(&ws, 0, sizeof ws);
+    ws.end_time = P->end_time;
+    ws.min_jump_config = P->window_rule == SG_WINDOW_FIXED ? 0 : P->runahead_min;
+    if (P->window_rule == SG_WINDOW_FIXED) ws.next_min_jump = P->fixed_jump;
+    sg_simtime start = 0, end = 1; /* slave.c:431 */
+    uint64_t rounds = 0;
+    int keep = 1;
+    while (keep) {
+        /* scheduler_continueNextRound */
+        d->round_end = end;
+        d->min_next = SG_SIMTIME_MAX;
+        pthread_barrier_wait(&d->prepare_b);
+        /* scheduler_awaitNextRound */
+        pthread_barrier_wait(&d->exec_b);
+        pthread_barrier_wait(&d->collect_b);
+        rounds++;
+        uint64_t jmin = UINT64_MAX;
+        for (uint32_t i = 0; i < n_workers; i++)
+            if (d->w[i].jmin < jmin) jmin = d->w[i].jmin;
+        if (P->window_rule == SG_WINDOW_DISCOVERED && jmin != UINT64_MAX)
+            ws.next_min_jump = jmin * SG_ONE_MS; /* topology.c:1374-1385 → master.c:153 */
+        keep = sg_window_next(&ws, d->min_next, &start, &end);
+        if (rounds >= max_rounds) keep = 0;
+    }
+    /* scheduler_finish */
+    d->running = 0;
+    pthread_barrier_wait(&d->prepare_b);
+    for (uint32_t i = 0; i < n_workers; i++) pthread_join(d->w[i].th, NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (res) {
+        memset(res, 0, sizeof *res);
+        res->rounds = rounds;
+        for (uint32_t i = 0; i < n_workers; i++) {
+            res->pops += d->w[i].pops;
+            res->sends += d->w[i].sends;
+            res->drop_reliability += d->w[i].dropr;
+            res->drop_endtime += d->w[i].drope;
+        }
+        res->bumped = d->bumped;
+        res->seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        res->last_window_start = start;
+        res->last_window_end = end;
+    }
+    if (digest) memcpy(digest, d->digest, (size_t)d->N * 8);
+    if (pops) memcpy(pops, d->pops, (size_t)d->N * 8);
+    if (rng) memcpy(rng, d->rng, (size_t)d->N * 4);
+    if (event_counter) memcpy(event_counter, d->evc, (size_t)d->N * 8);
+    pthread_barrier_destroy(&d->start_b);
+    pthread_barrier_destroy(&d->exec_b);
+    pthread_barrier_destroy(&d->collect_b);
+    pthread_barrier_destroy(&d->prepare_b);
+    free(d->rng);
+    free(d->evc);
+    free(d->pops);
+    free(d->digest);
+    free(d->w);
+    return SG_OK;
+}
+
+/* ------------------------------------------------------- gpu policy ops -- */
+typedef struct gpu_ops {
+    sg_policy* p;
+    int error;
+} gpu_ops;
+
+static void g_add_host(void* data, uint32_t host, uint64_t token) {
+    gpu_ops* g = (gpu_ops*)data;
+    if (sg_policy_add_host(g->p, host + 1, token) && !g->error) g->error = SG_ERR_INVAL;
+}
+static uint32_t g_hosts(void* data, uint64_t token, uint32_t* out, uint32_t cap) {
+    gpu_ops* g = (gpu_ops*)data;
+    uint32_t n = 0;
+    sg_policy_thread_hosts(g->p, token, out, cap, &n);
+    for (uint32_t i = 0; i < n && i < cap; i++) out[i] -= 1; /* ids are index + 1 */
+    return n < cap ? n : cap;
+}
+static void g_push(void* data, sg_hevent* e, uint32_t src, uint32_t dst, sg_simtime barrier) {
+    gpu_ops* g = (gpu_ops*)data;
+    sg_simtime t = e->time;
+    int rc = sg_policy_push(g->p, (uint64_t)pthread_self(), (uint64_t)(uintptr_t)e, e->time, src + 1,
+                            dst + 1, e->seq, barrier, &t);
+    if (rc && !g->error) g->error = rc;
+    e->time = t; /* event_setTime */
+}
+static sg_hevent* g_pop(void* data, sg_simtime barrier) {
+    gpu_ops* g = (gpu_ops*)data;
+    uint64_t h = 0;
+    int rc = sg_policy_pop(g->p, (uint64_t)pthread_self(), barrier, &h);
+    if (rc && !g->error) g->error = rc;
+    return (sg_hevent*)(uintptr_t)h;
+}
+static sg_simtime g_next(void* data) {
+    gpu_ops* g = (gpu_ops*)data;
+    sg_simtime t = SG_SIMTIME_MAX;
+    int rc = sg_policy_next_time(g->p, (uint64_t)pthread_self(), &t);
+    if (rc && !g->error) g->error = rc;
+    return t;
+}
+static void g_free(void* data) {
+    gpu_ops* g = (gpu_ops*)data;
+    uint64_t n = 0;
+    if (sg_policy_remaining(g->p, NULL, 0, &n) == SG_OK && n) {
+        uint64_t* hs = (uint64_t*)malloc(n * 8);
+        if (hs && sg_policy_remaining(g->p, hs, n, &n) == SG_OK)
+            for (uint64_t i = 0; i < n; i++) free((void*)(uintptr_t)hs[i]);
+        free(hs);
+    }
+    sg_policy_destroy(g->p);
+    free(g);
+}
+
+int sg_policy_ops_gpu(uint32_t n_threads, uint32_t max_hosts, int device, sg_sched_policy_ops* out) {
+    gpu_ops* g = (gpu_ops*)calloc(1, sizeof *g);
+    if (!g) return SG_ERR_NOMEM;
+    sg_policy_params prm = {n_threads, max_hosts, 0, device};
+    int rc = sg_policy_create(&prm, &g->p);
+    if (rc) {
+        free(g);
+        return rc;
+    }
+    out->data = g;
+    out->add_host = g_add_host;
+    out->get_assigned_hosts = g_hosts;
+    out->push = g_push;
+    out->pop = g_pop;
+    out->get_next_time = g_next;
+    out->free = g_free;
+    return SG_OK;
+}
+
+/* First error recorded by the gpu ops adapter (0 if none). */
+int sg_policy_ops_gpu_error(const sg_sched_policy_ops* ops) {
+    return ops && ops->data ? ((gpu_ops*)ops->data)->error : SG_ERR_INVAL;
+}

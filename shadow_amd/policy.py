@@ -1,0 +1,105 @@
+"""The `gpu` SchedulerPolicy (Mode P) and the Shadow-style round driver.
+
+``run_phold(cfg, n_workers, ops)`` runs the PHOLD workload with real CPU worker
+threads (the reference's scheduler.c / worker.c structure, restated in
+sg_sched.c) under a policy vtable: ``gpu_ops()`` gives the drop-in `gpu`
+policy whose queues, sort and MIN live on the MI355X.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class HEvent(C.Structure):
+    _fields_ = [("time", C.c_uint64), ("seq", C.c_uint64), ("src", C.c_uint32), ("dst", C.c_uint32)]
+
+
+ADD_HOST = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint64)
+GET_HOSTS = C.CFUNCTYPE(C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint32)
+PUSH = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(HEvent), C.c_uint32, C.c_uint32, C.c_uint64)
+POP = C.CFUNCTYPE(C.POINTER(HEvent), C.c_void_p, C.c_uint64)
+NEXT = C.CFUNCTYPE(C.c_uint64, C.c_void_p)
+FREE = C.CFUNCTYPE(None, C.c_void_p)
+
+
+class PolicyOps(C.Structure):
+    """sg_sched_policy_ops — mirrors struct _SchedulerPolicy (scheduler_policy.h:40-51)."""
+    _fields_ = [("data", C.c_void_p), ("add_host", ADD_HOST), ("get_assigned_hosts", GET_HOSTS),
+                ("push", PUSH), ("pop", POP), ("get_next_time", NEXT), ("free", FREE)]
+
+
+class SchedResult(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("rounds", "pops", "sends", "drop_reliability",
+                                          "drop_endtime", "bumped")] + \
+               [("seconds", C.c_double), ("last_window_start", C.c_uint64),
+                ("last_window_end", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: (float if n == "seconds" else int)(getattr(self, n)) for n, _ in self._fields_}
+
+
+def _bind():
+    lib = L.lib()
+    if not getattr(lib, "_policy_bound", False):
+        lib.sg_policy_ops_gpu.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(PolicyOps)]
+        lib.sg_policy_ops_gpu_error.argtypes = [C.POINTER(PolicyOps)]
+        lib.sg_sched_run_phold.argtypes = [C.POINTER(L.PholdParams), C.POINTER(L.PholdTables),
+                                           C.c_uint32, C.c_uint32, C.POINTER(PolicyOps), C.c_uint64,
+                                           C.POINTER(SchedResult), C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p]
+        lib._policy_bound = True
+    return lib
+
+
+def gpu_ops(n_workers: int, n_hosts: int, device: int = 0) -> PolicyOps:
+    ops = PolicyOps()
+    L.check(_bind().sg_policy_ops_gpu(n_workers, n_hosts, device, C.byref(ops)))
+    ops._owner = "gpu"
+    return ops
+
+
+def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 62,
+              scheduler_seed: int | None = None, free_ops: bool = True) -> dict:
+    """Run PHOLD under `ops` with n_workers CPU workers; returns per-host state
+    (digest, pops, rng, ev) and the driver's counters/timing."""
+    lib = _bind()
+    from .phold import seed_chain
+    if scheduler_seed is None:
+        scheduler_seed = seed_chain(cfg.get("seed", 1), 0)[1]  # slave.c:198
+    p = L.PholdParams()
+    p.n_hosts = cfg["n_hosts"]
+    p.n_vertices = cfg["n_vertices"]
+    p.load = cfg["load"]
+    p.dst_rule = cfg["dst_rule"]
+    p.window_rule = cfg["window_rule"]
+    p.end_time = cfg["end_time"]
+    p.bootstrap_end = cfg.get("bootstrap_end", 0)
+    p.fixed_jump = cfg.get("fixed_jump", 0)
+    p.runahead_min = cfg.get("runahead_min", 0)
+    arrs = [np.ascontiguousarray(cfg["host_vertex"], np.uint32),
+            np.ascontiguousarray(cfg["host_rng"], np.uint32),
+            np.ascontiguousarray(cfg["delay_ns"], np.uint64),
+            np.ascontiguousarray(cfg["keep_max"], np.int32),
+            np.ascontiguousarray(cfg["jump_ms"], np.uint32)]
+    wt = cfg.get("weight_thresh")
+    wt = None if wt is None else np.ascontiguousarray(wt, np.int32)
+    t = L.PholdTables(*[a.ctypes.data for a in arrs], None if wt is None else wt.ctypes.data)
+    n = cfg["n_hosts"]
+    dig, pops, ev = (np.zeros(n, np.uint64) for _ in range(3))
+    rng = np.zeros(n, np.uint32)
+    res = SchedResult()
+    rc = lib.sg_sched_run_phold(C.byref(p), C.byref(t), n_workers, scheduler_seed, C.byref(ops),
+                                max_rounds, C.byref(res), dig.ctypes.data, pops.ctypes.data,
+                                rng.ctypes.data, ev.ctypes.data)
+    err = lib.sg_policy_ops_gpu_error(C.byref(ops)) if getattr(ops, "_owner", "") == "gpu" else 0
+    if free_ops:
+        ops.free(ops.data)
+    L.check(rc)
+    L.check(err)
+    out = res.as_dict()
+    out.update(digest=dig, pops_per_host=pops, rng=rng, ev=ev)
+    return out

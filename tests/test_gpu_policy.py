@@ -1,0 +1,46 @@
+"""GPU: the drop-in `gpu` SchedulerPolicy (Mode P) — CPU worker threads execute
+the events, per-host queues / sort / MIN live in HBM — under the Shadow-style
+round driver; per-host traces must equal the oracle's, for any worker count."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from shadow_amd import phold, policy
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind,workers", [("tiny_lossy", 1), ("tiny_lossy", 4),
+                                          ("probe10_bumps", 3), ("c2_small", 8),
+                                          ("self_heavy", 2), ("runahead", 5)])
+def test_gpu_policy_matches_oracle(kind, workers):
+    cfg = {
+        "tiny_lossy": lambda: phold.tiny_config(n_hosts=200, V=6, load=4, end_time_s=0.4, loss=0.1),
+        "probe10_bumps": lambda: phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.5),
+        "c2_small": lambda: phold.c2_config(n_hosts=2000, end_time_s=0.6),
+        # 4 hosts: a quarter of all sends are self events, many inside the window
+        "self_heavy": lambda: phold.probe_config(n_hosts=4, jump_ms=20, end_time_s=0.5),
+        "runahead": lambda: phold.tiny_config(n_hosts=120, runahead_ms=6, end_time_s=0.3),
+    }[kind]()
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs, st = ref.host_state(), ref.stats()
+    r = policy.run_phold(cfg, workers, policy.gpu_ops(workers, cfg["n_hosts"]))
+    assert np.array_equal(r["digest"], rs["digest"])
+    assert np.array_equal(r["pops_per_host"], rs["pops"])
+    assert np.array_equal(r["rng"], rs["rng"])
+    assert np.array_equal(r["ev"], rs["ev"])
+    for k in ("rounds", "pops", "sends", "drop_reliability", "drop_endtime", "bumped"):
+        assert r[k] == st[k], k
+
+
+def test_gpu_policy_queue_growth():
+    """More events queued per host than the initial HBM slots: the policy grows
+    its queues and stays exact."""
+    cfg = phold.probe_config(n_hosts=6, jump_ms=5, load=200, end_time_s=0.3)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    r = policy.run_phold(cfg, 2, policy.gpu_ops(2, cfg["n_hosts"]))
+    assert np.array_equal(r["digest"], ref.host_state()["digest"])
