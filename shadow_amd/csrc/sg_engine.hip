@@ -13,15 +13,23 @@
 //   k_pack     (multi-shard) moves staged events owned by other shards into the
 //              per-peer outbox for the RCCL all-to-all.
 //   k_insert   delivers staged / received events into destination queues and
-//              maintains each host's and each 256-host block's minimum time.
-//   k_reduce   MIN next event time (host_single.c:273-305, scheduler.c:393-398)
-//              and the minimum discovered latency (topology.c:1374-1385).
-//   k_window   master_slaveFinishedCurrentRound (master.c:450-480).
+//              keeps each host's earliest queued time.
+//   k_reduce   MIN next event time (host_single.c:273-305, scheduler.c:393-398),
+//              the minimum discovered latency (topology.c:1374-1385) and, for a
+//              single shard, the next window (master.c:450-480).
 //
-// Queue layout: slot-major SoA, slot j of local host h at [j * L + h], so lanes
-// of a wave (consecutive hosts) read consecutive addresses.  Compiled with
-// -ffp-contract=off: the only FP is the FP64 destination rule, which must round
-// exactly as the reference does.
+// HBM layout:
+//   queue slot   16 B {time, key}, key = src << 40 | srcHostEventID: with the
+//                destination implied by the queue, event_compare is the
+//                lexicographic order of (time, key)
+//   queues       host-major, slot j of local host h at [h * CAP + j]: a round
+//                reads only the queues of hosts with an event before the barrier
+//   per pair     16 B {ceil delay ns, keep threshold, truncated ms}: one random
+//                access per send
+//   per host     8 B {weight threshold, vertex} (read-only, all N hosts) and
+//                32 B {rand_r state, event counter, pops, digest} (local hosts)
+// Compiled with -ffp-contract=off: the only FP is the FP64 floor destination
+// rule, which must round exactly as the reference does.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -38,13 +46,35 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int MAXG = 64;  // max shards
 constexpr uint64_t SIMTIME_MAX = UINT64_MAX - 1;
+constexpr int SRC_SHIFT = 40;
+constexpr uint64_t SEQ_MASK = (1ULL << SRC_SHIFT) - 1;
 
 enum Ctr {
     C_POPS = 0, C_BOOTS, C_SENDS, C_NULL, C_DROPREL, C_DROPEND, C_BUMPED, C_SAME,
     C_ACTIVE, C_EMIT, NCTR
 };
-// per-workgroup partials: counters, then three minima
-constexpr int P_JMIN = NCTR, P_EMIN = NCTR + 1, P_RMIN = NCTR + 2, NPART = NCTR + 3;
+enum Mins { M_JMIN = 0, M_EMIN, M_RMIN, NMIN };
+
+struct Slot {
+    uint64_t t;   // event time
+    uint64_t k;   // src << 40 | srcHostEventID
+};
+struct HostInfo {
+    int32_t wt;       // PHOLD weight threshold (test_phold.c:160-178)
+    uint32_t vertex;  // attachment vertex
+};
+struct PairRec {
+    uint64_t delay;   // ceil(latency_ms * 1e6)   (worker.c:275-277)
+    int32_t keep;     // max rand_r value kept     (worker.c:268-273)
+    uint32_t jump;    // (uint64)latency_ms        (master.c:153)
+};
+struct HostState {
+    uint32_t rng;     // host Random (host.c:176)
+    uint32_t pad;
+    uint64_t evc;     // eventIDCounter (host.c:397-400)
+    uint64_t pops;
+    uint64_t digest;
+};
 
 struct RoundState {
     uint64_t S, E, done, rounds;
@@ -56,40 +86,25 @@ struct RoundState {
 };
 
 struct Dev {
-    // configuration
     uint32_t N, V, L, lo, CAP, load, dst_rule, window_rule, G, g, nblocks, bcap;
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap;
     uint32_t bounds[MAXG + 1];
-    // tables
-    const uint32_t* vertex;   // [N]
-    const int32_t* wthresh;   // [N]
-    const uint64_t* delay;    // [V*V]
-    const int32_t* keep;      // [V*V]
-    const uint32_t* jump;     // [V*V]
-    // per local host
-    uint64_t* bag_time;       // [CAP*L]
-    uint64_t* bag_seq;        // [CAP*L]
-    uint32_t* bag_src;        // [CAP*L]
+    const HostInfo* hinfo;    // [N]
+    const PairRec* pairs;     // [V*V]
+    Slot* bag;                // [L][CAP]
     uint32_t* bag_cnt;        // [L]
     uint64_t* hmin;           // [L]
-    uint32_t* rng;            // [L]
-    uint64_t* evc;            // [L]
-    uint64_t* pops;           // [L]
-    uint64_t* digest;         // [L]
-    // per 256-host block
-    uint64_t* part;           // [NPART][nblocks]
+    HostState* hs;            // [L]
+    uint64_t* pmin;           // [NMIN][nblocks], this round
+    uint64_t* pcum;           // [NCTR][nblocks], cumulative
     uint32_t* blockcnt;       // [nblocks] staged events
     uint32_t* peercnt;        // [nblocks][G]
     uint32_t* peeroff;        // [nblocks][G]
-    // staging (per block region of bcap events)
-    uint64_t* st_time;
-    uint64_t* st_seq;
+    Slot* st;                 // staging, bcap per block
     uint32_t* st_dst;
-    uint32_t* st_src;
-    // trace
     sg_trace_rec* trace;
     RoundState* rs;
-    uint64_t* red3;           // local reduce output {min, jmin, ~overflow}
+    uint64_t* red3;           // single-shard reduce output
 };
 
 __device__ __forceinline__ int32_t dev_rand_r(uint32_t& state) {
@@ -125,42 +140,59 @@ __device__ __forceinline__ uint64_t digest_mix(uint64_t pos, uint64_t t, uint32_
     return fmix64(z ^ seq);
 }
 
-// Destination draw. Returns N when no host is selected (test_phold.c:176-177).
-__device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x) {
+// Destination draw; returns N when no host is selected (test_phold.c:176-177)
+// and the chosen host's info record.
+__device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
     const uint32_t N = d.N;
+    const HostInfo* w = d.hinfo;
     if (d.dst_rule == SG_DST_UNIFORM_FLOOR) {
         double r = (double)x / 2147483647.0;
         double f = floor(r * (double)N);
         uint32_t dd = (uint32_t)f;
-        return dd >= N ? N - 1 : dd;
+        dd = dd >= N ? N - 1 : dd;
+        info = w[dd];
+        return dd;
     }
-    // first i with x <= wthresh[i] (non-decreasing): guess from the uniform
+    // first i with x <= wt[i] (non-decreasing): guess from the uniform
     // position, walk a few steps, bisect the rest.
-    const int32_t* w = d.wthresh;
-    if (x > w[N - 1]) return N;
     uint32_t g = (uint32_t)(((uint64_t)(uint32_t)x * N) >> 31);
     if (g >= N) g = N - 1;
-    if (x <= w[g]) {
+    HostInfo cur = w[g];
+    if (x <= cur.wt) {
         for (int k = 0; k < 8; ++k) {
-            if (g == 0 || x > w[g - 1]) return g;
+            if (g == 0) break;
+            const HostInfo prev = w[g - 1];
+            if (x > prev.wt) break;
             --g;
+            cur = prev;
         }
-        uint32_t lo = 0, hi = g;  // answer in [lo, hi]
-        while (lo < hi) {
-            uint32_t mid = lo + (hi - lo) / 2;
-            if (x <= w[mid]) hi = mid; else lo = mid + 1;
+        if (g > 0 && x <= w[g - 1].wt) {
+            uint32_t lo = 0, hi = g - 1;  // answer in [lo, hi]
+            while (lo < hi) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
+            }
+            g = lo;
+            cur = w[g];
         }
-        return lo;
+        info = cur;
+        return g;
     }
+    if (x > w[N - 1].wt) return N;
     for (int k = 0; k < 8; ++k) {
         ++g;
-        if (x <= w[g]) return g;
+        cur = w[g];
+        if (x <= cur.wt) {
+            info = cur;
+            return g;
+        }
     }
     uint32_t lo = g + 1, hi = N - 1;
     while (lo < hi) {
-        uint32_t mid = lo + (hi - lo) / 2;
-        if (x <= w[mid]) hi = mid; else lo = mid + 1;
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
     }
+    info = w[lo];
     return lo;
 }
 
@@ -183,20 +215,39 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
     return v;
 }
 
+// event_compare with equal dst (event.c:122-148) on (time, src<<40|seq).
+// Bitwise, not short-circuit, and the running minimum is updated through one
+// select mask: ROCm 7.2 mis-compiled the branchy form inside the selection
+// loop (the winning slot index was not updated on a time tie).
+__device__ __forceinline__ bool key_less(uint64_t t, uint64_t k, uint64_t bt, uint64_t bk) {
+    return (t < bt) | ((t == bt) & (k < bk));
+}
+struct Best {
+    uint64_t t, k;
+    uint32_t slot;
+};
+__device__ __forceinline__ void best_take(Best& b, uint64_t t, uint64_t k, uint32_t slot) {
+    const bool take = key_less(t, k, b.t, b.k);
+    b.t = take ? t : b.t;
+    b.k = take ? k : b.k;
+    b.slot = take ? slot : b.slot;
+}
+
 __global__ void k_boot(Dev d) {
     const uint32_t lh = blockIdx.x * BLOCK + threadIdx.x;
     if (lh < d.L) {
         const uint32_t h = d.lo + lh;
         // worker_bootHosts: self event at t=0 carrying id 0 (event.c:38)
-        d.bag_time[lh] = 0;
-        d.bag_seq[lh] = 0;
-        d.bag_src[lh] = h;
+        d.bag[(size_t)lh * d.CAP] = Slot{0, (uint64_t)h << SRC_SHIFT};
         d.bag_cnt[lh] = 1;
         d.hmin[lh] = 0;
-        d.evc[lh] = 1;
-        d.pops[lh] = 0;
-        d.digest[lh] = 0;
+        HostState s = d.hs[lh];
+        s.evc = 1;
+        s.pops = 0;
+        s.digest = 0;
+        d.hs[lh] = s;
     }
+    if (threadIdx.x < NCTR) d.pcum[(size_t)threadIdx.x * d.nblocks + blockIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         RoundState* rs = d.rs;
         rs->S = 0;  // slave.c:431
@@ -221,9 +272,8 @@ struct Acc {
 };
 
 struct HostCtx {
-    uint32_t h, vh, lh;
-    uint32_t rng;
-    uint64_t ev, pops, dig;
+    uint32_t h, vh;
+    HostState s;
 };
 
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
@@ -231,54 +281,57 @@ struct HostCtx {
 // through `append` (they are popped later this round); everything else is
 // staged in the workgroup's region for k_insert / k_pack.
 template <class Append>
-__device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx& c, Acc& a,
-                                              uint64_t bt, uint32_t bs, uint64_t bq,
-                                              uint32_t* s_emit, uint32_t* s_peer, Append append) {
-    c.dig += digest_mix(c.pops, bt, bs, bq);
+__device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx& c, Acc& a, uint64_t bt,
+                                              uint64_t bk, uint32_t* s_emit, uint32_t* s_peer,
+                                              Append append) {
+    const uint32_t bsrc = (uint32_t)(bk >> SRC_SHIFT);
+    const uint64_t bseq = bk & SEQ_MASK;
+    c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
     if (d.trace) {
         const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
         if (ts < d.trace_cap) {
             sg_trace_rec r;
             r.time = bt;
-            r.seq = bq;
+            r.seq = bseq;
             r.host = c.h;
-            r.src = bs;
-            r.pos = c.pops;
+            r.src = bsrc;
+            r.pos = c.s.pops;
             d.trace[ts] = r;
         } else {
             a.overflow = true;
         }
     }
-    ++c.pops;
+    ++c.s.pops;
     ++a.ctr[C_POPS];
-    const bool boot = (bs == c.h && bq == 0);
+    const bool boot = (bsrc == c.h && bseq == 0);
     a.ctr[C_BOOTS] += boot;
     const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
     for (uint32_t m = 0; m < nsend; ++m) {
-        const int32_t x = dev_rand_r(c.rng);
-        const uint32_t dst = choose_dst(d, x);
+        const int32_t x = dev_rand_r(c.s.rng);
+        HostInfo di;
+        const uint32_t dst = choose_dst(d, x, di);
         if (dst >= d.N) {
             ++a.ctr[C_NULL];
             continue;
         }
         ++a.ctr[C_SENDS];
-        const size_t pair = (size_t)c.vh * d.V + d.vertex[dst];
-        const uint64_t jm = d.jump[pair];  // path discovery (topology.c:1374-1385)
-        a.jmin = jm < a.jmin ? jm : a.jmin;
-        const int32_t ch = dev_rand_r(c.rng);  // worker.c:268-269
-        if (!(bt < d.bootstrap_end || ch <= d.keep[pair])) {
+        const PairRec pr = d.pairs[(size_t)c.vh * d.V + di.vertex];
+        a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
+        const int32_t ch = dev_rand_r(c.s.rng);          // worker.c:268-269
+        if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
             ++a.ctr[C_DROPREL];
             continue;
         }
-        uint64_t tn = bt + d.delay[pair];  // worker.c:275-277
-        const uint64_t sq = c.ev++;        // event.c:38
-        if (tn >= d.end_time) {            // scheduler.c:343-346
+        uint64_t tn = bt + pr.delay;        // worker.c:275-277
+        const uint64_t sq = c.s.evc++;      // event.c:38
+        if (tn >= d.end_time) {             // scheduler.c:343-346
             ++a.ctr[C_DROPEND];
             continue;
         }
+        const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | sq;
         if (dst == c.h && tn < E) {
             ++a.ctr[C_SAME];
-            if (!append(tn, sq)) a.overflow = true;
+            if (!append(tn, key)) a.overflow = true;
             continue;
         }
         if (dst != c.h && tn < E) {  // host_single.c:180-184
@@ -291,30 +344,23 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx&
             continue;
         }
         const size_t so = (size_t)blockIdx.x * d.bcap + slot;
-        d.st_time[so] = tn;
-        d.st_seq[so] = sq;
+        d.st[so] = Slot{tn, key};
         d.st_dst[so] = dst;
-        d.st_src[so] = c.h;
         if (d.G > 1) atomicAdd(&s_peer[owner_of(d, dst)], 1u);
         a.emin = tn < a.emin ? tn : a.emin;
         ++a.ctr[C_EMIT];
     }
 }
 
-__device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uint64_t bt, uint32_t bs,
-                                         uint64_t bq) {
-    // event_compare with equal dst (event.c:122-148)
-    return t < bt || (t == bt && (s < bs || (s == bs && q < bq)));
-}
-
-// One lane per host.  MASKED (queue_cap <= 64): the host's queue times are read
-// once with independent loads, the slots before the barrier kept in a 64-bit
-// mask; selection visits only those slots.  Otherwise every pop rescans.
+// One lane per host.  MASKED (queue_cap <= 64): the queue is read once with
+// independent 16-B loads, the minimum event before the barrier and the last
+// slot are kept from that scan, further due slots are tracked in a 64-bit
+// mask.  Otherwise every pop rescans the queue.
 template <bool MASKED>
 __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     __shared__ uint32_t s_emit;
     __shared__ uint32_t s_peer[MAXG];
-    __shared__ uint64_t s_red[BLOCK / 64][NPART];
+    __shared__ uint64_t s_red[BLOCK / 64][NCTR + NMIN];
     const RoundState* rs = d.rs;
     if (rs->done) return;
     const uint64_t E = rs->E;
@@ -337,155 +383,130 @@ __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
         newmin = hm;
         if (hm < E) {
             HostCtx c;
-            c.lh = lh;
             c.h = d.lo + lh;
-            c.vh = d.vertex[c.h];
-            c.rng = d.rng[lh];
-            c.ev = d.evc[lh];
-            c.pops = d.pops[lh];
-            c.dig = d.digest[lh];
+            c.s = d.hs[lh];
+            c.vh = d.hinfo[c.h].vertex;
             uint32_t cnt = d.bag_cnt[lh];
+            // k_insert counts deliveries past capacity (flagged as overflow and
+            // reported at the next sync); never read beyond the queue
+            cnt = cnt < d.CAP ? cnt : d.CAP;
             a.ctr[C_ACTIVE] = 1;
-            const size_t stride = L;
-            uint64_t* __restrict__ bt_ = d.bag_time;
-            uint64_t* __restrict__ bq_ = d.bag_seq;
-            uint32_t* __restrict__ bs_ = d.bag_src;
+            Slot* bag = d.bag + (size_t)lh * d.CAP;  // this host's queue, contiguous
             if (MASKED) {
                 uint64_t due = 0, rest_min = SIMTIME_MAX;
+                Best b{UINT64_MAX, 0, 0};
+                Slot lastslot{0, 0};
                 for (uint32_t base = 0; base < cnt; base += 8) {
-                    uint64_t t[8];
+                    Slot s[8];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) t[i] = bt_[(size_t)(base + i) * stride + lh];
+                    for (int i = 0; i < 8; ++i) s[i] = bag[base + i];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const bool live = base + i < cnt;
-                        const bool isdue = live && t[i] < E;
-                        due |= (uint64_t)isdue << (base + i);
-                        if (live && !isdue && t[i] < rest_min) rest_min = t[i];
+                        const uint32_t j = base + i;
+                        const bool live = j < cnt;
+                        const bool isdue = live & (s[i].t < E);
+                        due |= (uint64_t)isdue << j;
+                        const uint64_t rt = (live & !isdue) ? s[i].t : SIMTIME_MAX;
+                        rest_min = rt < rest_min ? rt : rest_min;
+                        best_take(b, isdue ? s[i].t : UINT64_MAX, s[i].k, j);
+                        const bool is_last = j + 1 == cnt;
+                        lastslot.t = is_last ? s[i].t : lastslot.t;
+                        lastslot.k = is_last ? s[i].k : lastslot.k;
                     }
                 }
-                // non-due slots only move (never leave) while popping: rest_min is final
+                // slots after the barrier only move (never leave) while popping
                 newmin = rest_min;
-                auto append = [&](uint64_t tn, uint64_t sq) -> bool {
+                bool fresh = true;  // b / lastslot still describe the scanned queue
+                auto append = [&](uint64_t tn, uint64_t key) -> bool {
                     if (cnt >= d.CAP) return false;
-                    const size_t kn = (size_t)cnt * stride + lh;
-                    bt_[kn] = tn;
-                    bq_[kn] = sq;
-                    bs_[kn] = c.h;
+                    bag[cnt] = Slot{tn, key};
                     due |= 1ULL << cnt;
                     ++cnt;
                     return true;
                 };
                 while (due) {
-                    uint64_t m = due;
-                    uint32_t best = 0;
-                    uint64_t bt = SIMTIME_MAX + 1, bq = 0;
-                    uint32_t bs = 0;
-                    while (m) {
-                        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-                        m &= m - 1;
-                        const size_t k = (size_t)j * stride + lh;
-                        const uint64_t t = bt_[k];
-                        const uint32_t s = bs_[k];
-                        const uint64_t q = bq_[k];
-                        if (key_less(t, s, q, bt, bs, bq)) {
-                            best = j;
-                            bt = t;
-                            bs = s;
-                            bq = q;
+                    if (!fresh) {
+                        b = Best{UINT64_MAX, 0, 0};
+                        uint64_t m = due;
+                        while (m) {
+                            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                            m &= m - 1;
+                            const Slot s = bag[j];
+                            best_take(b, s.t, s.k, j);
                         }
                     }
+                    const uint32_t best = b.slot;
+                    const uint64_t bt = b.t, bk = b.k;
                     // remove `best`: the last slot fills the hole
                     const uint32_t last = cnt - 1;
                     due &= ~(1ULL << best);
                     if (best != last) {
-                        const size_t kb = (size_t)best * stride + lh, kl = (size_t)last * stride + lh;
-                        bt_[kb] = bt_[kl];
-                        bq_[kb] = bq_[kl];
-                        bs_[kb] = bs_[kl];
+                        const Slot ls = fresh ? lastslot : bag[last];
+                        bag[best] = ls;
                         const uint64_t lastbit = (due >> last) & 1ULL;
                         due &= ~(1ULL << last);
                         due |= lastbit << best;
                     }
                     cnt = last;
-                    execute_event(d, E, c, a, bt, bs, bq, &s_emit, s_peer, append);
+                    fresh = false;
+                    execute_event(d, E, c, a, bt, bk, &s_emit, s_peer, append);
                 }
             } else {
-                auto append = [&](uint64_t tn, uint64_t sq) -> bool {
+                auto append = [&](uint64_t tn, uint64_t key) -> bool {
                     if (cnt >= d.CAP) return false;
-                    const size_t kn = (size_t)cnt * stride + lh;
-                    bt_[kn] = tn;
-                    bq_[kn] = sq;
-                    bs_[kn] = c.h;
+                    bag[cnt] = Slot{tn, key};
                     ++cnt;
                     return true;
                 };
                 for (;;) {
-                    int best = -1;
-                    uint64_t bt = 0, bq = 0;
-                    uint32_t bs = 0;
+                    Best b{UINT64_MAX, 0, UINT32_MAX};
                     uint64_t rest_min = SIMTIME_MAX;
                     for (uint32_t j = 0; j < cnt; ++j) {
-                        const size_t k = (size_t)j * stride + lh;
-                        const uint64_t t = bt_[k];
-                        if (t < E) {
-                            const uint32_t s = bs_[k];
-                            const uint64_t q = bq_[k];
-                            if (best < 0 || key_less(t, s, q, bt, bs, bq)) {
-                                best = (int)j;
-                                bt = t;
-                                bs = s;
-                                bq = q;
-                            }
-                        } else if (t < rest_min) {
-                            rest_min = t;
+                        const Slot s = bag[j];
+                        if (s.t < E) {
+                            best_take(b, s.t, s.k, j);
+                        } else if (s.t < rest_min) {
+                            rest_min = s.t;
                         }
                     }
-                    if (best < 0) {
+                    if (b.slot == UINT32_MAX) {
                         newmin = rest_min;
                         break;
                     }
                     --cnt;
-                    if ((uint32_t)best != cnt) {
-                        const size_t kb = (size_t)best * stride + lh, kl = (size_t)cnt * stride + lh;
-                        bt_[kb] = bt_[kl];
-                        bq_[kb] = bq_[kl];
-                        bs_[kb] = bs_[kl];
-                    }
-                    execute_event(d, E, c, a, bt, bs, bq, &s_emit, s_peer, append);
+                    if (b.slot != cnt) bag[b.slot] = bag[cnt];
+                    execute_event(d, E, c, a, b.t, b.k, &s_emit, s_peer, append);
                 }
             }
             d.bag_cnt[lh] = cnt;
-            d.rng[lh] = c.rng;
-            d.evc[lh] = c.ev;
-            d.pops[lh] = c.pops;
-            d.digest[lh] = c.dig;
+            d.hs[lh] = c.s;
             d.hmin[lh] = newmin;
         }
     }
 
-    // workgroup partials (transposed [field][block] for a coalesced k_reduce)
+    // workgroup partials: cumulative counters and this round's three minima
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t v[NPART];
+    uint64_t v[NCTR + NMIN];
 #pragma unroll
     for (int i = 0; i < NCTR; ++i) v[i] = wave_sum(a.ctr[i]);
-    v[P_JMIN] = wave_min(a.jmin);
-    v[P_EMIN] = wave_min(a.emin);
-    v[P_RMIN] = wave_min(newmin);
+    v[NCTR + M_JMIN] = wave_min(a.jmin);
+    v[NCTR + M_EMIN] = wave_min(a.emin);
+    v[NCTR + M_RMIN] = wave_min(newmin);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < NPART; ++i) s_red[wid][i] = v[i];
+        for (int i = 0; i < NCTR + NMIN; ++i) s_red[wid][i] = v[i];
     }
     if (a.overflow) atomicOr((unsigned long long*)&d.rs->overflow, 1ULL);
     __syncthreads();
-    if (threadIdx.x < NPART) {
+    if (threadIdx.x < NCTR + NMIN) {
         const int i = threadIdx.x;
         uint64_t r = s_red[0][i];
         for (int w = 1; w < BLOCK / 64; ++w) {
             const uint64_t x = s_red[w][i];
             r = i < NCTR ? r + x : (x < r ? x : r);
         }
-        d.part[(size_t)i * d.nblocks + blockIdx.x] = r;
+        if (i < NCTR) d.pcum[(size_t)i * d.nblocks + blockIdx.x] += r;
+        else d.pmin[(size_t)(i - NCTR) * d.nblocks + blockIdx.x] = r;
     }
     if (threadIdx.x == 0) d.blockcnt[blockIdx.x] = s_emit < d.bcap ? s_emit : d.bcap;
     if (d.G > 1 && threadIdx.x < d.G) d.peercnt[(size_t)blockIdx.x * d.G + threadIdx.x] = s_peer[threadIdx.x];
@@ -507,7 +528,7 @@ __global__ void k_peer_scan(Dev d, int64_t* send_counts) {
     }
 }
 
-// Multi-shard: staged events for other shards → outbox triples.
+// Multi-shard: staged events for other shards → outbox triples {time, key, dst}.
 __global__ __launch_bounds__(BLOCK) void k_pack(Dev d, int64_t* send) {
     if (d.rs->done) return;
     __shared__ uint32_t s_slot[MAXG];
@@ -522,25 +543,26 @@ __global__ __launch_bounds__(BLOCK) void k_pack(Dev d, int64_t* send) {
         if (p == d.g) continue;
         const uint64_t slot = (uint64_t)d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
         if (slot >= d.xcap) continue;  // flagged by k_peer_scan
+        const Slot s = d.st[so];
         int64_t* o = send + ((size_t)p * d.xcap + slot) * 3;
-        o[0] = (int64_t)d.st_time[so];
-        o[1] = (int64_t)d.st_seq[so];
-        o[2] = (int64_t)(((uint64_t)dst << 32) | d.st_src[so]);
+        o[0] = (int64_t)s.t;
+        o[1] = (int64_t)s.k;
+        o[2] = (int64_t)dst;
     }
 }
 
-__device__ __forceinline__ void deliver(const Dev& d, uint64_t t, uint64_t seq, uint32_t dst, uint32_t src) {
+__device__ __forceinline__ void deliver(const Dev& d, const Slot s, uint32_t dst) {
     const uint32_t dl = dst - d.lo;
     const uint32_t slot = atomicAdd(&d.bag_cnt[dl], 1u);
     if (slot >= d.CAP) {
         atomicOr((unsigned long long*)&d.rs->overflow, 4ULL);
         return;
     }
-    const size_t k = (size_t)slot * d.L + dl;
-    d.bag_time[k] = t;
-    d.bag_seq[k] = seq;
-    d.bag_src[k] = src;
-    atomicMin((unsigned long long*)&d.hmin[dl], (unsigned long long)t);
+    d.bag[(size_t)dl * d.CAP + slot] = s;
+    // the earliest-time word only decreases here: skip the atomic when it is
+    // already at or below this event
+    if (s.t < __hip_atomic_load(&d.hmin[dl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin((unsigned long long*)&d.hmin[dl], (unsigned long long)s.t);
 }
 
 // Staged events of this shard's own hosts → destination queues.
@@ -552,7 +574,7 @@ __global__ __launch_bounds__(BLOCK) void k_insert(Dev d) {
         const size_t so = (size_t)b * d.bcap + i;
         const uint32_t dst = d.st_dst[so];
         if (dst - d.lo >= d.L) continue;  // another shard's host
-        deliver(d, d.st_time[so], d.st_seq[so], dst, d.st_src[so]);
+        deliver(d, d.st[so], dst);
     }
 }
 
@@ -561,13 +583,12 @@ __global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* rec
     if (d.rs->done) return;
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
         const int64_t* r = recv + i * 3;
-        const uint64_t w = (uint64_t)r[2];
-        const uint32_t dst = (uint32_t)(w >> 32);
+        const uint32_t dst = (uint32_t)r[2];
         if (dst - d.lo >= d.L) {
             atomicOr((unsigned long long*)&d.rs->overflow, 8ULL);
             continue;
         }
-        deliver(d, (uint64_t)r[0], (uint64_t)r[1], dst, (uint32_t)(w & 0xffffffffu));
+        deliver(d, Slot{(uint64_t)r[0], (uint64_t)r[1]}, dst);
     }
 }
 
@@ -594,44 +615,40 @@ __device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint
     rs->done = start < end ? 0 : 1;
 }
 
-// Local MIN next time (remaining ∪ staged), discovery min, counters; with
-// apply != 0 (single shard) also the next window.  One workgroup of 1024.
+// Local MIN next time (remaining ∪ staged) and discovery min; with apply != 0
+// (single shard) also the next window.  One workgroup of 1024.
 __global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3, int apply) {
     if (d.rs->done) return;
-    __shared__ uint64_t s_v[16][NPART];
-    uint64_t v[NPART];
+    __shared__ uint64_t s_v[16][NMIN];
+    uint64_t v[NMIN];
 #pragma unroll
-    for (int i = 0; i < NPART; ++i) v[i] = i < NCTR ? 0 : UINT64_MAX;
+    for (int i = 0; i < NMIN; ++i) v[i] = UINT64_MAX;
     const size_t NB = d.nblocks;
     for (uint32_t b = threadIdx.x; b < NB; b += 1024) {
 #pragma unroll
-        for (int i = 0; i < NPART; ++i) {
-            const uint64_t x = d.part[(size_t)i * NB + b];
-            v[i] = i < NCTR ? v[i] + x : (x < v[i] ? x : v[i]);
+        for (int i = 0; i < NMIN; ++i) {
+            const uint64_t x = d.pmin[(size_t)i * NB + b];
+            v[i] = x < v[i] ? x : v[i];
         }
     }
 #pragma unroll
-    for (int i = 0; i < NPART; ++i) v[i] = i < NCTR ? wave_sum(v[i]) : wave_min(v[i]);
+    for (int i = 0; i < NMIN; ++i) v[i] = wave_min(v[i]);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < NPART; ++i) s_v[wid][i] = v[i];
+        for (int i = 0; i < NMIN; ++i) s_v[wid][i] = v[i];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint64_t r[NPART];
-        for (int i = 0; i < NPART; ++i) {
+        uint64_t r[NMIN];
+        for (int i = 0; i < NMIN; ++i) {
             r[i] = s_v[0][i];
-            for (int w = 1; w < 16; ++w) {
-                const uint64_t x = s_v[w][i];
-                r[i] = i < NCTR ? r[i] + x : (x < r[i] ? x : r[i]);
-            }
+            for (int w = 1; w < 16; ++w) r[i] = s_v[w][i] < r[i] ? s_v[w][i] : r[i];
         }
         RoundState* rs = d.rs;
-        for (int i = 0; i < NCTR; ++i) rs->ctr[i] += r[i];
-        const uint64_t j = rs->jmin < r[P_JMIN] ? rs->jmin : r[P_JMIN];
+        const uint64_t j = rs->jmin < r[M_JMIN] ? rs->jmin : r[M_JMIN];
         rs->jmin = j;
-        const uint64_t m = r[P_EMIN] < r[P_RMIN] ? r[P_EMIN] : r[P_RMIN];
+        const uint64_t m = r[M_EMIN] < r[M_RMIN] ? r[M_EMIN] : r[M_RMIN];
         out3[0] = m;
         out3[1] = j;
         out3[2] = ~rs->overflow;
@@ -644,11 +661,27 @@ __global__ void k_window(Dev d, const uint64_t* in3) {
     apply_window(d, in3[0], in3[1], in3[2]);
 }
 
-__global__ void k_pending(Dev d, unsigned long long* out) {
-    uint64_t s = 0;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < d.L; i += gridDim.x * BLOCK) s += d.bag_cnt[i];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)s);
+// Cumulative counters (stats on demand) and pending events.
+__global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pending) {
+    __shared__ uint64_t s_c[16][NCTR + 1];
+    uint64_t c[NCTR + 1];
+    for (int i = 0; i <= NCTR; ++i) c[i] = 0;
+    for (uint32_t b = threadIdx.x; b < d.nblocks; b += 1024)
+        for (int i = 0; i < NCTR; ++i) c[i] += d.pcum[(size_t)i * d.nblocks + b];
+    for (uint32_t h = threadIdx.x; h < d.L; h += 1024) {
+        const uint32_t n = d.bag_cnt[h];
+        c[NCTR] += n < d.CAP ? n : d.CAP;
+    }
+    for (int i = 0; i <= NCTR; ++i) c[i] = wave_sum(c[i]);
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i <= NCTR; ++i) s_c[threadIdx.x >> 6][i] = c[i];
+    __syncthreads();
+    if (threadIdx.x <= NCTR) {
+        uint64_t t = 0;
+        for (int w = 0; w < 16; ++w) t += s_c[w][threadIdx.x];
+        if (threadIdx.x < NCTR) d.rs->ctr[threadIdx.x] = t;
+        else *pending = t;
+    }
 }
 
 }  // namespace
@@ -747,11 +780,11 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     *out = nullptr;
     const sg_phold_params& p = *params;
     const uint32_t G = p.shard_count ? p.shard_count : 1;
-    if (p.n_hosts == 0 || p.n_vertices == 0 || G > MAXG || p.shard_index >= G || G > p.n_hosts ||
-        !t->host_vertex || !t->host_rng || !t->delay_ns || !t->keep_max || !t->jump_ms ||
-        (p.dst_rule == SG_DST_WEIGHTS && !t->weight_thresh) || p.dst_rule > 1 || p.window_rule > 1 ||
-        p.load == 0) {
-        sg_set_error("sg_engine_create: invalid parameters");
+    if (p.n_hosts == 0 || p.n_hosts > (1u << (64 - SRC_SHIFT)) || p.n_vertices == 0 || G > MAXG ||
+        p.shard_index >= G || G > p.n_hosts || !t->host_vertex || !t->host_rng || !t->delay_ns ||
+        !t->keep_max || !t->jump_ms || (p.dst_rule == SG_DST_WEIGHTS && !t->weight_thresh) ||
+        p.dst_rule > 1 || p.window_rule > 1 || p.load == 0) {
+        sg_set_error("sg_engine_create: invalid parameters (n_hosts must be in [1, 2^24])");
         return SG_ERR_INVAL;
     }
     int ndev = 0;
@@ -815,38 +848,23 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
             return rc;                                 \
         }                                              \
     } while (0)
-    uint32_t* vtx;
-    int32_t* wt;
-    uint64_t* dl;
-    int32_t* kp;
-    uint32_t* jp;
-    ALLOC(vtx, N);
-    ALLOC(wt, N);
-    ALLOC(dl, VV);
-    ALLOC(kp, VV);
-    ALLOC(jp, VV);
-    d.vertex = vtx;
-    d.wthresh = wt;
-    d.delay = dl;
-    d.keep = kp;
-    d.jump = jp;
-    ALLOC(d.bag_time, S);
-    ALLOC(d.bag_seq, S);
-    ALLOC(d.bag_src, S);
+    HostInfo* hinfo;
+    PairRec* pairs;
+    ALLOC(hinfo, N);
+    ALLOC(pairs, VV);
+    d.hinfo = hinfo;
+    d.pairs = pairs;
+    ALLOC(d.bag, S);
     ALLOC(d.bag_cnt, L);
     ALLOC(d.hmin, L);
-    ALLOC(d.rng, L);
-    ALLOC(d.evc, L);
-    ALLOC(d.pops, L);
-    ALLOC(d.digest, L);
-    ALLOC(d.part, NB * NPART);
+    ALLOC(d.hs, L);
+    ALLOC(d.pmin, NB * NMIN);
+    ALLOC(d.pcum, NB * NCTR);
     ALLOC(d.blockcnt, NB);
     ALLOC(d.peercnt, NB * G);
     ALLOC(d.peeroff, NB * G);
-    ALLOC(d.st_time, ST);
-    ALLOC(d.st_seq, ST);
+    ALLOC(d.st, ST);
     ALLOC(d.st_dst, ST);
-    ALLOC(d.st_src, ST);
     ALLOC(d.rs, 1);
     ALLOC(d.red3, 4);
     if (d.trace_cap) ALLOC(d.trace, d.trace_cap);
@@ -869,14 +887,27 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         sg_set_error("hipHostMalloc failed");
         return SG_ERR_NOMEM;
     }
+    // pack the tables on the host
+    std::vector<HostInfo> hi(N);
+    for (size_t i = 0; i < N; ++i) {
+        hi[i].vertex = t->host_vertex[i];
+        hi[i].wt = t->weight_thresh ? t->weight_thresh[i] : 0;
+        if (hi[i].vertex >= d.V) {
+            sg_engine_destroy(e);
+            sg_set_error("sg_engine_create: host %zu attached to vertex %u >= %u", i, hi[i].vertex, d.V);
+            return SG_ERR_INVAL;
+        }
+    }
+    std::vector<PairRec> pr(VV);
+    for (size_t i = 0; i < VV; ++i) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
+    std::vector<HostState> hs(L);
+    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[d.lo + i], 0, 0, 0, 0};
     hipError_t err = hipSuccess;
-    err = err != hipSuccess ? err : hipMemcpy(vtx, t->host_vertex, N * 4, hipMemcpyHostToDevice);
-    if (t->weight_thresh) err = err != hipSuccess ? err : hipMemcpy(wt, t->weight_thresh, N * 4, hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(dl, t->delay_ns, VV * 8, hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(kp, t->keep_max, VV * 4, hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(jp, t->jump_ms, VV * 4, hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(d.rng, t->host_rng + d.lo, L * 4, hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemcpy(d.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemset(d.rs, 0, sizeof(RoundState));
+    err = err != hipSuccess ? err : hipMemset(d.pcum, 0, NB * NCTR * 8);
     if (err != hipSuccess) {
         sg_set_error("table upload failed: %s", hipGetErrorString(err));
         sg_engine_destroy(e);
@@ -1000,8 +1031,7 @@ int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch) {
 int sg_engine_stats(sg_engine* e, sg_round_stats* out) {
     if (!e || !out) return SG_ERR_INVAL;
     unsigned long long* dp = (unsigned long long*)e->d.red3 + 3;
-    HIPCHK(hipMemsetAsync(dp, 0, 8, e->stream));
-    hipLaunchKernelGGL(k_pending, dim3(256), dim3(BLOCK), 0, e->stream, e->d, dp);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(1024), 0, e->stream, e->d, dp);
     HIPCHK(hipGetLastError());
     uint64_t pend = 0;
     HIPCHK(hipMemcpyAsync(&pend, dp, 8, hipMemcpyDeviceToHost, e->stream));
@@ -1032,7 +1062,8 @@ int sg_engine_stats(sg_engine* e, sg_round_stats* out) {
 
 int sg_engine_active_hosts(sg_engine* e, uint64_t* active, uint64_t* emitted) {
     if (!e) return SG_ERR_INVAL;
-    int rc = read_rs(e);
+    sg_round_stats s;
+    int rc = sg_engine_stats(e, &s);
     if (rc) return rc;
     if (active) *active = e->h_rs->ctr[C_ACTIVE];
     if (emitted) *emitted = e->h_rs->ctr[C_EMIT];
@@ -1043,11 +1074,17 @@ int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops, uint32_
                          uint64_t* event_counter) {
     if (!e) return SG_ERR_INVAL;
     const size_t L = e->d.L;
-    if (digest) HIPCHK(hipMemcpyAsync(digest, e->d.digest, L * 8, hipMemcpyDeviceToHost, e->stream));
-    if (pops) HIPCHK(hipMemcpyAsync(pops, e->d.pops, L * 8, hipMemcpyDeviceToHost, e->stream));
-    if (rng) HIPCHK(hipMemcpyAsync(rng, e->d.rng, L * 4, hipMemcpyDeviceToHost, e->stream));
-    if (event_counter) HIPCHK(hipMemcpyAsync(event_counter, e->d.evc, L * 8, hipMemcpyDeviceToHost, e->stream));
-    return sg_engine_sync(e);
+    std::vector<HostState> hs(L);
+    HIPCHK(hipMemcpyAsync(hs.data(), e->d.hs, L * sizeof(HostState), hipMemcpyDeviceToHost, e->stream));
+    int rc = sg_engine_sync(e);
+    if (rc) return rc;
+    for (size_t i = 0; i < L; ++i) {
+        if (digest) digest[i] = hs[i].digest;
+        if (pops) pops[i] = hs[i].pops;
+        if (rng) rng[i] = hs[i].rng;
+        if (event_counter) event_counter[i] = hs[i].evc;
+    }
+    return SG_OK;
 }
 
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out) {

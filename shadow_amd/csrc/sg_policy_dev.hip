@@ -80,7 +80,8 @@ __global__ void k_pcopy(Q to, Q from) {
 
 __device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uint64_t bt, uint32_t bs,
                                          uint64_t bq) {
-    return t < bt || (t == bt && (s < bs || (s == bs && q < bq)));
+    // bitwise, not short-circuit (see sg_engine.hip key_less)
+    return (t < bt) | ((t == bt) & ((s < bs) | ((s == bs) & (q < bq))));
 }
 
 __global__ __launch_bounds__(BLOCK) void k_pextract(Q q, uint64_t barrier, sgp_rec* out, uint32_t* off,

@@ -51,7 +51,7 @@ def test_inprocess_shards_match_oracle(world, kind):
         assert np.array_equal(np.concatenate([h[k] for h in hs]), rs[k]), k
     st = [s.stats() for s in shards]
     want = ref.stats()
-    assert all(x["overflow"] == 0 for x in st)
+    assert all(x["overflow"] == 0 for x in st), [hex(x["overflow"]) for x in st]
     for k in ("pops", "sends", "drop_reliability", "drop_endtime", "bumped", "same_round"):
         assert sum(x[k] for x in st) == want[k], k
-    assert all(x["rounds"] == want["rounds"] for x in st)
+    assert all(x["rounds"] == want["rounds"] for x in st), ([x["rounds"] for x in st], want["rounds"], [(x["window_start"], x["window_end"], x["done"]) for x in st], (want["window_start"], want["window_end"]))
