@@ -214,6 +214,8 @@ int sg_engine_host_range(sg_engine* e, uint32_t* first_host, uint32_t* n_local);
 /* Cumulative hosts-with-pops per round (active host-rounds) and staged events. */
 int sg_engine_active_hosts(sg_engine* e, uint64_t* active_host_rounds, uint64_t* emitted);
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
+/* Executed windows {start, end} per round (recorded when trace_capacity > 0). */
+int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);
 void* sg_engine_stream(sg_engine* e);
 
 /* Multi-shard round, driven by the caller around its collectives:

@@ -172,11 +172,15 @@ class Sim:
                               None if self._wt is None else self._wt.ctypes.data)
         if not self.h:
             raise RuntimeError(L.orc_error().decode())
+        self._destroy = L.orc_destroy  # held so interpreter shutdown can still free
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._destroy(self.h)
+            self.h = None
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().orc_destroy(self.h)
-            self.h = None
+        self.close()
 
     def boot(self):
         assert lib().orc_boot(self.h) == 0

@@ -73,7 +73,7 @@ EXPORTS = [
     "sg_build_paths", "sg_build_weight_thresholds", "sg_window_note_latency", "sg_window_next",
     "sg_topology_lognormal", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
-    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace",
+    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_step_process", "sg_engine_step_insert",
     "sg_engine_step_reduce", "sg_engine_step_window", "sg_engine_kernel_times",
     "sg_engine_set_timing", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
@@ -121,6 +121,7 @@ def lib():
     L.sg_engine_host_range.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.sg_engine_active_hosts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sg_engine_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.sg_engine_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_stream.argtypes = [C.c_void_p]
     L.sg_engine_stream.restype = C.c_void_p
     L.sg_engine_step_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]

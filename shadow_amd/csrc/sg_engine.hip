@@ -103,6 +103,8 @@ struct Dev {
     Slot* st;                 // staging, bcap per block
     uint32_t* st_dst;
     sg_trace_rec* trace;
+    uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
+    uint64_t wlog_cap;
     RoundState* rs;
     uint64_t* red3;           // single-shard reduce output
 };
@@ -596,6 +598,10 @@ __global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* rec
 __device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t not_overflow) {
     RoundState* rs = d.rs;
     rs->overflow |= ~not_overflow;
+    if (d.wlog && rs->rounds < d.wlog_cap) {  // the window just executed
+        d.wlog[2 * rs->rounds] = rs->S;
+        d.wlog[2 * rs->rounds + 1] = rs->E;
+    }
     rs->rounds += 1;
     rs->last_min = minNext;
     uint64_t jump;
@@ -868,6 +874,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(d.rs, 1);
     ALLOC(d.red3, 4);
     if (d.trace_cap) ALLOC(d.trace, d.trace_cap);
+    d.wlog_cap = d.trace_cap ? 1u << 20 : 0;
+    if (d.wlog_cap) ALLOC(d.wlog, 2 * d.wlog_cap);
 #undef ALLOC
 
     if (hip_stream) {
@@ -1097,6 +1105,19 @@ int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t
     if (out && capacity) {
         uint64_t m = n < capacity ? n : capacity;
         if (m) HIPCHK(hipMemcpy(out, e->d.trace, m * sizeof(sg_trace_rec), hipMemcpyDeviceToHost));
+    }
+    return SG_OK;
+}
+
+int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out) {
+    if (!e) return SG_ERR_INVAL;
+    int rc = read_rs(e);
+    if (rc) return rc;
+    uint64_t n = e->h_rs->rounds < e->d.wlog_cap ? e->h_rs->rounds : e->d.wlog_cap;
+    if (n_out) *n_out = n;
+    if (out_pairs && capacity && n) {
+        const uint64_t m = n < capacity ? n : capacity;
+        HIPCHK(hipMemcpy(out_pairs, e->d.wlog, m * 16, hipMemcpyDeviceToHost));
     }
     return SG_OK;
 }

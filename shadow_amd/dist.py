@@ -18,6 +18,7 @@ signed MIN reduction orders them as unsigned.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import time
 
@@ -47,19 +48,27 @@ class EngineShard:
         from .engine import Engine
         self.dev = torch.device("cuda", device)
         torch.cuda.set_device(self.dev)
-        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        # a dedicated stream: engine kernels, torch ops and the collectives of a
+        # round are all ordered on it (torch's default stream has handle 0,
+        # which the C-ABI reads as "make your own stream")
+        self.stream = torch.cuda.Stream(device=self.dev)
+        stream = self.stream.cuda_stream
         n_local = owner_bounds(cfg["n_hosts"], world)[rank + 1] - owner_bounds(cfg["n_hosts"], world)[rank]
         if exchange_cap is None:
             # the boot round stages load events per host: size for it
             exchange_cap = max(4096, n_local * cfg["load"])
         self.cap = exchange_cap
         self.world = world
+        self.eng_args = (rank, world)
         self.eng = Engine(cfg, device=device, shard_index=rank, shard_count=world,
                           queue_cap=queue_cap, exchange_cap=exchange_cap, stream=stream)
         self.send = torch.empty((world, exchange_cap, 3), dtype=torch.int64, device=self.dev)
         self.send_counts = torch.zeros(world, dtype=torch.int64, device=self.dev)
         self.red = torch.zeros(3, dtype=torch.int64, device=self.dev)
         self.recv = torch.empty((0, 3), dtype=torch.int64, device=self.dev)
+
+    def stream_ctx(self):
+        return torch.cuda.stream(self.stream)
 
     def boot(self):
         self.eng.boot()
@@ -86,7 +95,7 @@ class EngineShard:
         return self.eng.stats()
 
     def sync(self):
-        torch.cuda.synchronize(self.dev)
+        self.stream.synchronize()
 
 
 def _flip(t: torch.Tensor) -> torch.Tensor:
@@ -119,12 +128,14 @@ def run_round(shard, world: int):
 
 
 def run(shard, world: int, max_rounds: int = 1 << 62, check_every: int = 16) -> int:
+    ctx = shard.stream_ctx() if hasattr(shard, "stream_ctx") else contextlib.nullcontext()
     r = 0
-    while r < max_rounds:
-        run_round(shard, world)
-        r += 1
-        if r % check_every == 0 and shard.done():
-            break
+    with ctx:
+        while r < max_rounds:
+            run_round(shard, world)
+            r += 1
+            if r % check_every == 0 and shard.done():
+                break
     return r
 
 
@@ -151,13 +162,16 @@ def bench(args):
     shard.sync()
     s0 = shard.stats()
     dist.barrier()
+    shard.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(shard, world, args.steps, check_every=1 << 30)
+    shard.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dist.barrier()
     s1 = shard.stats()
+    shard.sync()
     t = torch.tensor([dt], dtype=torch.float64, device=shard.dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     pops = torch.tensor([s1["pops"] - s0["pops"], s1["rounds"] - s0["rounds"], s1["overflow"]],

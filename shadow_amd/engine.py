@@ -103,6 +103,14 @@ class Engine:
             L.check(L.lib().sg_engine_trace(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out
 
+    def windows(self) -> np.ndarray:
+        n = C.c_uint64()
+        L.check(L.lib().sg_engine_windows(self.h, None, 0, C.byref(n)))
+        out = np.zeros(2 * n.value, np.uint64)
+        if n.value:
+            L.check(L.lib().sg_engine_windows(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out.reshape(-1, 2)
+
     def set_timing(self, on: bool):
         L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
 

@@ -18,12 +18,20 @@ def _flip(t):
 @pytest.mark.parametrize("world,kind", [(2, "tiny"), (3, "probe10"), (4, "c4small")])
 def test_inprocess_shards_match_oracle(world, kind):
     from shadow_amd.dist import EngineShard
+    from shadow_amd.engine import Engine
     cfg = {"tiny": lambda: phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1),
            "probe10": lambda: phold.probe_config(n_hosts=400, jump_ms=10, end_time_s=0.5),
            "c4small": lambda: phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)}[kind]()
     shards = [EngineShard(cfg, r, world, 0) for r in range(world)]
-    for s in shards:
+    stream = torch.cuda.Stream()
+    for s in shards:  # one stream for everything, as one rank's round would be
+        s.eng.close()
+        s.stream = stream
+        s.eng = Engine(cfg, device=0, shard_index=s.eng_args[0], shard_count=world,
+                       exchange_cap=s.cap, stream=stream.cuda_stream)
         s.boot()
+    ctx = torch.cuda.stream(stream)
+    ctx.__enter__()
     rounds = 0
     while True:
         sends = [s.process() for s in shards]
@@ -42,6 +50,7 @@ def test_inprocess_shards_match_oracle(world, kind):
         if rounds % 8 == 0 and shards[0].done():
             break
         assert rounds < 100_000
+    ctx.__exit__(None, None, None)
     ref = O.Sim(cfg)
     ref.boot()
     ref.run()
