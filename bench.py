@@ -15,8 +15,9 @@ Also reported:
                committed event + 24 B per active host-round)
                per launch / its average launch time (HIP events on the engine
                stream), against 8 TB/s HBM.
-  cpu_baseline the CPU restatement (oracle/) of the same workload timed on this
-               machine's host cores on a bounded sample of rounds (rank 0, N=1).
+  cpu_baseline the CPU reference policy (oracle/host_steal.c, the host_steal
+               restatement) on the same workload, timed on this machine's host
+               cores over a bounded sample of rounds (rank 0, N=1).
 """
 from __future__ import annotations
 
@@ -30,6 +31,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# PMC HBM bytes per launch of the dominant kernel for this default workload:
+# rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
+# MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
+# from inside a timed run, so the bench quotes the committed measurement.
+PMC_JSON = os.path.join(ROOT, "profiles", "r01", "bench_default", "pmc.json")
+DOMINANT = "k_process<true>"
+
+
+def pmc_traffic(n_hosts):
+    if n_hosts != 1_000_000 or not os.path.exists(PMC_JSON):
+        return None, None
+    k = json.load(open(PMC_JSON))["kernels"].get(DOMINANT)
+    if not k:
+        return None, None
+    return k["traffic_bytes"], os.path.relpath(PMC_JSON, ROOT)
 ALG_BYTES_PER_EVENT = 64
 ALG_BYTES_PER_ACTIVE_HOST = 24
 
@@ -42,25 +58,45 @@ def parse():
     ap.add_argument("--hosts", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rounds", type=int, default=12)
+    ap.add_argument("--cpu-workers", type=int,
+                    default=min(16, len(os.sched_getaffinity(0))),
+                    help="CPU baseline worker threads (the GPU box's share is 16 cores)")
     ap.add_argument("--batch", type=int, default=32, help="rounds enqueued per host sync")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, warmup, rounds):
-    """Oracle (CPU restatement, 1 thread) on the same workload: boot + warmup
-    rounds untimed, then `rounds` rounds timed."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, warmup, rounds, workers):
+    """The CPU reference policy: oracle/host_steal.c — the
+    C restatement of scheduler_policy_host_steal.c — under the Shadow-style
+    round driver (sg_sched.c, worker.c:149-216 semantics), same PHOLD workload.
+    Boot + `warmup` rounds untimed, the next `rounds` rounds timed, at
+    -w `workers` and at -w 1."""
     from oracle import oracle as O
-    s = O.Sim(cfg)
-    s.boot()
-    s.run(warmup)
-    p0 = s.stats()["pops"]
-    t0 = time.perf_counter()
-    s.run(rounds)
-    dt = time.perf_counter() - t0
-    p1 = s.stats()["pops"]
-    return {"value": (p1 - p0) / dt, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/orc.c host-round restatement, same config, rounds "
-                      f"{warmup}..{warmup + rounds} ({p1 - p0} events, {dt:.2f} s, 1 thread)"}
+    from shadow_amd import policy
+
+    def one(w):
+        ops = O.cpu_policy_ops(True, w, cfg["n_hosts"])
+        r = policy.run_phold(cfg, w, ops, max_rounds=warmup + rounds, mark_round=warmup)
+        return r["marked_pops"] / r["marked_seconds"], r
+
+    v, r = one(workers)
+    v1, _ = one(1) if workers > 1 else (v, r)
+    return {"value": v, "unit": "events/s", "cores": workers, "kind": "port",
+            "single_thread_value": v1, "cpu_model": _cpu_model(),
+            "sample": f"oracle/host_steal.c (host_steal restatement) -w {workers} under the "
+                      f"Shadow round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} "
+                      f"timed ({r['marked_pops']} events, {r['marked_seconds']:.2f} s); "
+                      f"single_thread_value is -w 1 on the same rounds"}
 
 
 def run_single(args):
@@ -101,6 +137,7 @@ def run_single(args):
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args.hosts)
     res = {
         "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
         "value": pops / dt,
@@ -120,13 +157,15 @@ def run_single(args):
                    "n_hosts": args.hosts, "rounds_timed": rounds, "events_timed": pops,
                    "parallelism": "hosts sharded 1 way"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_process", "avg_launch_us": avg_launch_s * 1e6,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "traffic_gbs": traffic / avg_launch_s / 1e9 if traffic and avg_launch_s else None,
+                     "kernel": DOMINANT, "avg_launch_us": avg_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "kernel_ms": {k: v[0] for k, v in kt.items()}},
     }
     if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_rounds, args.cpu_rounds)
+        res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)
     return res
 
 

@@ -316,6 +316,12 @@ typedef struct sg_sched_result {
     uint64_t rounds, pops, sends, drop_reliability, drop_endtime, bumped;
     double seconds;          /* wall time of the round loop (worker.c:165-176 semantics) */
     sg_simtime last_window_start, last_window_end;
+    /* steady-state split: the only input field.  When mark_round > 0 the rounds
+     * after the first mark_round are also reported on their own (a bench's
+     * warmup excluded); otherwise the three outputs below are zero. */
+    uint64_t mark_round;
+    double marked_seconds;
+    uint64_t marked_pops, marked_rounds;
 } sg_sched_result;
 
 /* The gpu policy as a vtable (data = a new sg_policy on `device`); release it

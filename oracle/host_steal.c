@@ -176,10 +176,16 @@ static sg_hevent* pop_from(pol* p, td* t, dq* assigned, sg_simtime barrier) {
         if (q->n && q->a[0]->time < barrier) {
             q->last = q->a[0]->time;
             e = hq_pop(q);
-            /* migrate iff the host was stolen (host_steal.c:172-196, 303) */
-            pthread_rwlock_wrlock(&p->lock);
-            p->owner[h] = t->tnumber;
+            /* migrate iff the host was stolen (host_steal.c:172-196, 303): the
+             * owner is read under the reader lock, written only on a change */
+            pthread_rwlock_rdlock(&p->lock);
+            const uint32_t old = p->owner[h];
             pthread_rwlock_unlock(&p->lock);
+            if (old != t->tnumber) {
+                pthread_rwlock_wrlock(&p->lock);
+                p->owner[h] = t->tnumber;
+                pthread_rwlock_unlock(&p->lock);
+            }
         } else {
             dq_push(&t->proc, h);
             t->running = -1;

@@ -230,7 +230,9 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
         ops->add_host(ops->data, order[k], (uint64_t)d->w[n_workers > 1 ? k % n_workers : 0].th);
     free(order);
 
-    struct timespec t0, t1;
+    struct timespec t0, t1, tm;
+    const uint64_t mark_round = res ? res->mark_round : 0;
+    uint64_t mark_pops = 0;
     pthread_barrier_wait(&d->start_b); /* scheduler_start */
     clock_gettime(CLOCK_MONOTONIC, &t0);
     sg_window_state ws;
@@ -250,6 +252,10 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
         pthread_barrier_wait(&d->exec_b);
         pthread_barrier_wait(&d->collect_b);
         rounds++;
+        if (mark_round && rounds == mark_round) { /* workers idle between barriers */
+            clock_gettime(CLOCK_MONOTONIC, &tm);
+            for (uint32_t i = 0; i < n_workers; i++) mark_pops += d->w[i].pops;
+        }
         uint64_t jmin = UINT64_MAX;
         for (uint32_t i = 0; i < n_workers; i++)
             if (d->w[i].jmin < jmin) jmin = d->w[i].jmin;
@@ -276,6 +282,12 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
         res->seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
         res->last_window_start = start;
         res->last_window_end = end;
+        res->mark_round = mark_round;
+        if (mark_round && rounds > mark_round) {
+            res->marked_seconds = (double)(t1.tv_sec - tm.tv_sec) + 1e-9 * (double)(t1.tv_nsec - tm.tv_nsec);
+            res->marked_pops = res->pops - mark_pops;
+            res->marked_rounds = rounds - mark_round;
+        }
     }
     if (digest) memcpy(digest, d->digest, (size_t)d->N * 8);
     if (pops) memcpy(pops, d->pops, (size_t)d->N * 8);

@@ -36,10 +36,12 @@ class SchedResult(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("rounds", "pops", "sends", "drop_reliability",
                                           "drop_endtime", "bumped")] + \
                [("seconds", C.c_double), ("last_window_start", C.c_uint64),
-                ("last_window_end", C.c_uint64)]
+                ("last_window_end", C.c_uint64), ("mark_round", C.c_uint64),
+                ("marked_seconds", C.c_double), ("marked_pops", C.c_uint64),
+                ("marked_rounds", C.c_uint64)]
 
     def as_dict(self):
-        return {n: (float if n == "seconds" else int)(getattr(self, n)) for n, _ in self._fields_}
+        return {n: (float if t is C.c_double else int)(getattr(self, n)) for n, t in self._fields_}
 
 
 def _bind():
@@ -63,7 +65,8 @@ def gpu_ops(n_workers: int, n_hosts: int, device: int = 0) -> PolicyOps:
 
 
 def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 62,
-              scheduler_seed: int | None = None, free_ops: bool = True) -> dict:
+              scheduler_seed: int | None = None, free_ops: bool = True,
+              mark_round: int = 0) -> dict:
     """Run PHOLD under `ops` with n_workers CPU workers; returns per-host state
     (digest, pops, rng, ev) and the driver's counters/timing."""
     lib = _bind()
@@ -92,6 +95,7 @@ def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 
     dig, pops, ev = (np.zeros(n, np.uint64) for _ in range(3))
     rng = np.zeros(n, np.uint32)
     res = SchedResult()
+    res.mark_round = mark_round
     rc = lib.sg_sched_run_phold(C.byref(p), C.byref(t), n_workers, scheduler_seed, C.byref(ops),
                                 max_rounds, C.byref(res), dig.ctypes.data, pops.ctypes.data,
                                 rng.ctypes.data, ev.ctypes.data)

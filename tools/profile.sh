@@ -22,4 +22,5 @@ pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_A
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
+pass l2 TCC_HIT_sum TCC_MISS_sum
 find $OUT -name "*.csv" | head -20
