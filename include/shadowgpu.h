@@ -221,7 +221,7 @@ void* sg_engine_stream(sg_engine* e);
 /* Multi-shard round, driven by the caller around its collectives:
  *   step_process(e, send, send_counts) — pops + PHOLD body; events for other
  *       shards go to send[peer * exchange_cap * 3 ...] as int64 triples
- *       {time, seq, (dst << 32) | src}; send_counts[peer] gets their count
+ *       {time, src << 40 | srcHostEventID, dst}; send_counts[peer] gets their count
  *       (device pointers, e.g. torch tensors);
  *   step_insert(e, recv, n_recv) — local new events + n_recv received triples;
  *   step_reduce(e, out3) — out3 = {local min next time, local min jump ms,
