@@ -62,6 +62,10 @@ def parse():
                     default=min(16, len(os.sched_getaffinity(0))),
                     help="CPU baseline worker threads (the GPU box's share is 16 cores)")
     ap.add_argument("--batch", type=int, default=32, help="rounds enqueued per host sync")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="N > 1: nccl (RCCL, the measured path) or gloo (rehearsal only)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="N > 1 rehearsal: every rank on GPU 0 (needs --dist-backend gloo)")
     return ap.parse_args()
 
 

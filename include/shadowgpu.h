@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 1
+#define SG_ABI_VERSION 2
 
 typedef uint64_t sg_simtime;                /* SimulationTime, core/support/definitions.h:18 */
 #define SG_SIMTIME_INVALID UINT64_MAX       /* definitions.h:28 */
@@ -180,6 +180,8 @@ typedef struct sg_round_stats {
     uint64_t jmin_ms;         /* truncated min discovered latency, UINT64_MAX if none */
     uint64_t pending;         /* events queued in HBM after the last round */
     uint64_t trace_len;       /* pop records written */
+    uint64_t exchange_steps;  /* multi-shard: exchange steps run (rounds + drain steps) */
+    uint64_t phase;           /* multi-shard: 1 while outbox leftovers are being drained */
 } sg_round_stats;
 
 typedef struct sg_trace_rec {   /* one executed pop */
@@ -218,19 +220,28 @@ int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t
 int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);
 void* sg_engine_stream(sg_engine* e);
 
-/* Multi-shard round, driven by the caller around its collectives:
- *   step_process(e, send, send_counts) — pops + PHOLD body; events for other
- *       shards go to send[peer * exchange_cap * 3 ...] as int64 triples
- *       {time, src << 40 | srcHostEventID, dst}; send_counts[peer] gets their count
- *       (device pointers, e.g. torch tensors);
- *   step_insert(e, recv, n_recv) — local new events + n_recv received triples;
- *   step_reduce(e, out3) — out3 = {local min next time, local min jump ms,
- *       ~overflow} (device, reduce with MIN across ranks);
- *   step_window(e, in3) — next window from the reduced triple. */
-int sg_engine_step_process(sg_engine* e, int64_t* send, int64_t* send_counts);
-int sg_engine_step_insert(sg_engine* e, const int64_t* recv, uint64_t n_recv);
-int sg_engine_step_reduce(sg_engine* e, uint64_t* out3);
-int sg_engine_step_window(sg_engine* e, const uint64_t* in3);
+/* Multi-shard step, driven by the caller around ONE all-to-all per step (no
+ * host synchronisation, no all-reduce):
+ *   step_send(e, send) — on a process step: pops + PHOLD body + local MIN;
+ *       events for other shards go to a per-peer outbox.  On every step: up to
+ *       exchange_cap outbox events per peer are written into send, which is
+ *       [G][rows][3] int64 (rows = sg_engine_exchange_rows): per peer block two
+ *       header rows {n, sender has more, local MIN next time, local min jump ms,
+ *       overflow flags, round} then n triples {time, src << 40 | srcHostEventID,
+ *       dst};
+ *   (caller) all_to_all of send → recv, equal [rows][3] blocks per peer;
+ *   step_recv(e, recv) — local new events + received triples into the queues;
+ *       the next window from the G received headers (the MIN all-reduce of
+ *       scheduler.c:386-408 / master.c:450-480, carried by the all-to-all).
+ *       When any sender still has outbox leftovers the next step is a drain
+ *       step (same window, no processing). */
+int sg_engine_exchange_rows(sg_engine* e, uint64_t* rows);
+/* Change exchange_cap between steps (every shard must use the same value). */
+int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap);
+/* Largest per-peer outbox of a process step since the last reset. */
+int sg_engine_exchange_peak(sg_engine* e, uint64_t* peak, int reset);
+int sg_engine_step_send(sg_engine* e, int64_t* send);
+int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
 
 /* Kernel timing of the last sg_engine_run/enqueue (HIP events on the engine
  * stream): total ms per kernel class {process, insert, window}, and launches. */

@@ -52,7 +52,7 @@ class RoundStats(C.Structure):
                 ("rounds", "pops", "boots", "sends", "null_dst", "drop_reliability",
                  "drop_endtime", "bumped", "same_round", "overflow", "window_start",
                  "window_end", "done", "min_jump", "next_min_jump", "jmin_ms", "pending",
-                 "trace_len")]
+                 "trace_len", "exchange_steps", "phase")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -74,8 +74,8 @@ EXPORTS = [
     "sg_topology_lognormal", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
     "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace", "sg_engine_windows",
-    "sg_engine_stream", "sg_engine_step_process", "sg_engine_step_insert",
-    "sg_engine_step_reduce", "sg_engine_step_window", "sg_engine_kernel_times",
+    "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
+    "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv", "sg_engine_kernel_times",
     "sg_engine_set_timing", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
@@ -124,10 +124,11 @@ def lib():
     L.sg_engine_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_stream.argtypes = [C.c_void_p]
     L.sg_engine_stream.restype = C.c_void_p
-    L.sg_engine_step_process.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
-    L.sg_engine_step_insert.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    L.sg_engine_step_reduce.argtypes = [C.c_void_p, C.c_void_p]
-    L.sg_engine_step_window.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_engine_exchange_rows.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.sg_engine_set_exchange_cap.argtypes = [C.c_void_p, C.c_uint64]
+    L.sg_engine_exchange_peak.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
+    L.sg_engine_step_send.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_engine_step_recv.argtypes = [C.c_void_p, C.c_void_p]
     L.sg_engine_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sg_engine_set_timing.argtypes = [C.c_void_p, C.c_int]
     _lib = L

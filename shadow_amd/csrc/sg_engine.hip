@@ -11,7 +11,9 @@
 //              (event.c:38), endTime drop (scheduler.c:343), barrier bump
 //              (host_single.c:180-184). New events are staged per workgroup.
 //   k_pack     (multi-shard) moves staged events owned by other shards into the
-//              per-peer outbox for the RCCL all-to-all.
+//              per-peer outbox; k_fill copies up to exchange_cap of them per peer
+//              into the fixed-size blocks of the RCCL all-to-all, behind a header
+//              that also carries this shard's MIN terms (so no all-reduce).
 //   k_insert   delivers staged / received events into destination queues and
 //              keeps each host's earliest queued time.
 //   k_reduce   MIN next event time (host_single.c:273-305, scheduler.c:393-398),
@@ -48,6 +50,9 @@ constexpr int MAXG = 64;  // max shards
 constexpr uint64_t SIMTIME_MAX = UINT64_MAX - 1;
 constexpr int SRC_SHIFT = 40;
 constexpr uint64_t SEQ_MASK = (1ULL << SRC_SHIFT) - 1;
+// exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
+constexpr int HDR = 2;
+enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND };
 
 enum Ctr {
     C_POPS = 0, C_BOOTS, C_SENDS, C_NULL, C_DROPREL, C_DROPEND, C_BUMPED, C_SAME,
@@ -83,11 +88,17 @@ struct RoundState {
     uint64_t trace_len;
     uint64_t ctr[NCTR];
     uint64_t last_min;
+    // multi-shard step protocol
+    uint64_t phase;      // 0: process step, 1: drain step (outbox leftovers only)
+    uint64_t loc_min;    // this shard's MIN next time of the round being exchanged
+    uint64_t loc_jmin;   // this shard's cumulative min discovered latency (ms)
+    uint64_t steps;      // exchange steps executed
+    uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
 };
 
 struct Dev {
     uint32_t N, V, L, lo, CAP, load, dst_rule, window_rule, G, g, nblocks, bcap;
-    uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap;
+    uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
     const PairRec* pairs;     // [V*V]
@@ -100,6 +111,10 @@ struct Dev {
     uint32_t* blockcnt;       // [nblocks] staged events
     uint32_t* peercnt;        // [nblocks][G]
     uint32_t* peeroff;        // [nblocks][G]
+    int64_t* outq;            // [nblocks * bcap][3] per-peer outbox, peer p at peer_base[p]
+    uint64_t* peer_base;      // [G]
+    uint64_t* outn;           // [G] events in peer p's outbox this round
+    uint64_t* sent;           // [G] of which already sent
     Slot* st;                 // staging, bcap per block
     uint32_t* st_dst;
     sg_trace_rec* trace;
@@ -263,6 +278,16 @@ __global__ void k_boot(Dev d) {
         rs->trace_len = 0;
         for (int i = 0; i < NCTR; ++i) rs->ctr[i] = 0;
         rs->last_min = 0;
+        rs->phase = 0;
+        rs->loc_min = SIMTIME_MAX;
+        rs->loc_jmin = UINT64_MAX;
+        rs->steps = 0;
+        rs->peak_peer = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < d.G && d.outn) {
+        d.outn[threadIdx.x] = 0;
+        d.sent[threadIdx.x] = 0;
+        d.peer_base[threadIdx.x] = 0;
     }
 }
 
@@ -364,7 +389,7 @@ __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     __shared__ uint32_t s_peer[MAXG];
     __shared__ uint64_t s_red[BLOCK / 64][NCTR + NMIN];
     const RoundState* rs = d.rs;
-    if (rs->done) return;
+    if (rs->done | rs->phase) return;
     const uint64_t E = rs->E;
     const uint32_t lh = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t L = d.L;
@@ -514,25 +539,63 @@ __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     if (d.G > 1 && threadIdx.x < d.G) d.peercnt[(size_t)blockIdx.x * d.G + threadIdx.x] = s_peer[threadIdx.x];
 }
 
-// Multi-shard: exclusive prefix of per-block peer counts (one workgroup).
-__global__ void k_peer_scan(Dev d, int64_t* send_counts) {
-    if (d.rs->done) return;
-    const uint32_t p = threadIdx.x;
-    if (p < d.G) {
-        uint64_t run = 0;
-        for (uint32_t b = 0; b < d.nblocks; ++b) {
-            const size_t k = (size_t)b * d.G + p;
+// Inclusive scan across one workgroup of 1024 (16 waves).
+__device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t* s_w) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    if (lane == 63) s_w[wid] = v;
+    __syncthreads();
+    uint64_t add = 0;
+    for (int w = 0; w < wid; ++w) add += s_w[w];
+    __syncthreads();
+    return v + add;
+}
+
+// Multi-shard, process steps: per-(block, peer) offsets of the staged events
+// and each peer's outbox region.  One workgroup of 1024.
+__global__ __launch_bounds__(1024) void k_peer_scan(Dev d) {
+    RoundState* rs = d.rs;
+    if (rs->done | rs->phase) return;
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_tot[MAXG];
+    const uint32_t NB = d.nblocks, G = d.G;
+    const uint32_t chunk = (NB + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * chunk;
+    const uint32_t b1 = b0 + chunk < NB ? b0 + chunk : NB;
+    for (uint32_t p = 0; p < G; ++p) {
+        uint64_t sum = 0;
+        for (uint32_t b = b0; b < b1; ++b) sum += d.peercnt[(size_t)b * G + p];
+        const uint64_t incl = block_incl_scan(sum, s_w);
+        uint64_t run = incl - sum;
+        for (uint32_t b = b0; b < b1; ++b) {
+            const size_t k = (size_t)b * G + p;
             d.peeroff[k] = (uint32_t)run;
             run += d.peercnt[k];
         }
-        send_counts[p] = p == d.g ? 0 : (int64_t)(run < d.xcap ? run : d.xcap);
-        if (p != d.g && run > d.xcap) atomicOr((unsigned long long*)&d.rs->overflow, 2ULL);
+        if (threadIdx.x == 1023) s_tot[p] = incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint64_t base = 0, peak = rs->peak_peer;
+        for (uint32_t p = 0; p < G; ++p) {
+            const uint64_t n = p == d.g ? 0 : s_tot[p];
+            d.peer_base[p] = base;
+            d.outn[p] = n;
+            d.sent[p] = 0;
+            base += n;
+            peak = n > peak ? n : peak;
+        }
+        rs->peak_peer = peak;
     }
 }
 
-// Multi-shard: staged events for other shards → outbox triples {time, key, dst}.
-__global__ __launch_bounds__(BLOCK) void k_pack(Dev d, int64_t* send) {
-    if (d.rs->done) return;
+// Multi-shard, process steps: staged events owned by other shards → outbox
+// triples {time, key, dst}, grouped by owner.
+__global__ __launch_bounds__(BLOCK) void k_pack(Dev d) {
+    if (d.rs->done | d.rs->phase) return;
     __shared__ uint32_t s_slot[MAXG];
     if (threadIdx.x < MAXG) s_slot[threadIdx.x] = 0;
     __syncthreads();
@@ -543,13 +606,38 @@ __global__ __launch_bounds__(BLOCK) void k_pack(Dev d, int64_t* send) {
         const uint32_t dst = d.st_dst[so];
         const uint32_t p = owner_of(d, dst);
         if (p == d.g) continue;
-        const uint64_t slot = (uint64_t)d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
-        if (slot >= d.xcap) continue;  // flagged by k_peer_scan
+        const uint64_t slot = d.peer_base[p] + d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
         const Slot s = d.st[so];
-        int64_t* o = send + ((size_t)p * d.xcap + slot) * 3;
+        int64_t* o = d.outq + slot * 3;
         o[0] = (int64_t)s.t;
         o[1] = (int64_t)s.k;
         o[2] = (int64_t)dst;
+    }
+}
+
+// Every step: up to xcap outbox events per peer into the peer's exchange
+// block, behind the header {n, sender has more, MIN next, min jump, overflow,
+// round}.  Grid (chunks, G).
+__global__ __launch_bounds__(BLOCK) void k_fill(Dev d, int64_t* send) {
+    const RoundState* rs = d.rs;
+    if (rs->done) return;
+    const uint32_t p = blockIdx.y;
+    const uint64_t left = d.outn[p] - d.sent[p];
+    const uint64_t n = left < d.xcap ? left : d.xcap;
+    int64_t* blk = send + (size_t)p * d.xrows * 3;
+    const int64_t* src = d.outq + (d.peer_base[p] + d.sent[p]) * 3;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n * 3;
+         i += (uint64_t)gridDim.x * BLOCK)
+        blk[HDR * 3 + i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint64_t more = 0;
+        for (uint32_t q = 0; q < d.G; ++q) more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
+        blk[H_N] = (int64_t)n;
+        blk[H_MORE] = (int64_t)more;
+        blk[H_MIN] = (int64_t)rs->loc_min;
+        blk[H_JMIN] = (int64_t)rs->loc_jmin;
+        blk[H_OVF] = (int64_t)rs->overflow;
+        blk[H_ROUND] = (int64_t)rs->rounds;
     }
 }
 
@@ -569,7 +657,7 @@ __device__ __forceinline__ void deliver(const Dev& d, const Slot s, uint32_t dst
 
 // Staged events of this shard's own hosts → destination queues.
 __global__ __launch_bounds__(BLOCK) void k_insert(Dev d) {
-    if (d.rs->done) return;
+    if (d.rs->done | d.rs->phase) return;
     const uint32_t b = blockIdx.x;
     const uint32_t n = d.blockcnt[b];
     for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
@@ -580,11 +668,19 @@ __global__ __launch_bounds__(BLOCK) void k_insert(Dev d) {
     }
 }
 
-// Received triples → destination queues.
-__global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* recv, uint64_t n) {
+// Received exchange blocks → destination queues.  Grid (chunks, G).
+__global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* recv) {
     if (d.rs->done) return;
+    const uint32_t p = blockIdx.y;
+    if (p == d.g) return;
+    const int64_t* blk = recv + (size_t)p * d.xrows * 3;
+    const uint64_t n = (uint64_t)blk[H_N];
+    if (n > d.xcap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long*)&d.rs->overflow, 8ULL);
+        return;
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const int64_t* r = recv + i * 3;
+        const int64_t* r = blk + (HDR + i) * 3;
         const uint32_t dst = (uint32_t)r[2];
         if (dst - d.lo >= d.L) {
             atomicOr((unsigned long long*)&d.rs->overflow, 8ULL);
@@ -624,7 +720,7 @@ __device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint
 // Local MIN next time (remaining ∪ staged) and discovery min; with apply != 0
 // (single shard) also the next window.  One workgroup of 1024.
 __global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3, int apply) {
-    if (d.rs->done) return;
+    if (d.rs->done | d.rs->phase) return;
     __shared__ uint64_t s_v[16][NMIN];
     uint64_t v[NMIN];
 #pragma unroll
@@ -655,16 +751,46 @@ __global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3, int appl
         const uint64_t j = rs->jmin < r[M_JMIN] ? rs->jmin : r[M_JMIN];
         rs->jmin = j;
         const uint64_t m = r[M_EMIN] < r[M_RMIN] ? r[M_EMIN] : r[M_RMIN];
-        out3[0] = m;
-        out3[1] = j;
-        out3[2] = ~rs->overflow;
+        rs->loc_min = m;
+        rs->loc_jmin = j;
+        if (out3) {
+            out3[0] = m;
+            out3[1] = j;
+            out3[2] = ~rs->overflow;
+        }
         if (apply) apply_window(d, m, j, ~rs->overflow);
     }
 }
 
-__global__ void k_window(Dev d, const uint64_t* in3) {
-    if (d.rs->done) return;
-    apply_window(d, in3[0], in3[1], in3[2]);
+// Multi-shard step end: the window from the G received headers (every shard
+// sees the same headers, so every shard takes the same decision).  A sender
+// with outbox leftovers makes the next step a drain step: same window, no
+// processing, more exchange.
+__global__ void k_window(Dev d, const int64_t* recv) {
+    RoundState* rs = d.rs;
+    if (rs->done) return;
+    uint64_t m = UINT64_MAX, j = UINT64_MAX, ovf = 0, more = 0;
+    for (uint32_t p = 0; p < d.G; ++p) {
+        const int64_t* blk = recv + (size_t)p * d.xrows * 3;
+        more |= (uint64_t)blk[H_MORE];
+        const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
+        m = bm < m ? bm : m;
+        j = bj < j ? bj : j;
+        ovf |= (uint64_t)blk[H_OVF];
+        if ((uint64_t)blk[H_ROUND] != rs->rounds) ovf |= 16;  // shards out of step
+    }
+    for (uint32_t q = 0; q < d.G; ++q) {
+        const uint64_t left = d.outn[q] - d.sent[q];
+        d.sent[q] += left < d.xcap ? left : d.xcap;
+    }
+    rs->steps += 1;
+    if (more) {
+        rs->phase = 1;
+        rs->overflow |= ovf;
+        return;
+    }
+    rs->phase = 0;
+    apply_window(d, m, j, ~ovf);
 }
 
 // Cumulative counters (stats on demand) and pending events.
@@ -834,7 +960,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.fixed_jump = p.fixed_jump;
     d.runahead_min = p.runahead_min;
     d.trace_cap = p.trace_capacity;
-    d.xcap = p.exchange_cap ? p.exchange_cap : 1;
+    d.xcap = p.exchange_cap ? p.exchange_cap : 4096;
+    d.xrows = HDR + d.xcap;
     d.nblocks = (d.L + BLOCK - 1) / BLOCK;
     const uint32_t per_host = d.CAP > d.load ? d.CAP : d.load;
     d.bcap = BLOCK * per_host;
@@ -869,6 +996,12 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(d.blockcnt, NB);
     ALLOC(d.peercnt, NB * G);
     ALLOC(d.peeroff, NB * G);
+    if (G > 1) {
+        ALLOC(d.outq, ST * 3);
+        ALLOC(d.peer_base, G);
+        ALLOC(d.outn, G);
+        ALLOC(d.sent, G);
+    }
     ALLOC(d.st, ST);
     ALLOC(d.st_dst, ST);
     ALLOC(d.rs, 1);
@@ -1065,6 +1198,8 @@ int sg_engine_stats(sg_engine* e, sg_round_stats* out) {
     out->jmin_ms = r.jmin;
     out->pending = pend;
     out->trace_len = r.trace_len;
+    out->exchange_steps = r.steps;
+    out->phase = r.phase;
     return SG_OK;
 }
 
@@ -1122,53 +1257,82 @@ int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint
     return SG_OK;
 }
 
-int sg_engine_step_process(sg_engine* e, int64_t* send, int64_t* send_counts) {
+static int need_sharded(sg_engine* e, const char* fn) {
     if (!e || !e->booted) {
-        sg_set_error("sg_engine_step_process: engine not booted");
+        sg_set_error("%s: engine not booted", fn);
         return SG_ERR_STATE;
     }
-    int rc;
+    if (e->d.G < 2) {
+        sg_set_error("%s: single-shard engine, use sg_engine_run / enqueue_round", fn);
+        return SG_ERR_STATE;
+    }
+    return SG_OK;
+}
+
+static uint32_t fill_chunks(const Dev& d) {
+    uint64_t c = (d.xcap * 3 + BLOCK * 4 - 1) / (BLOCK * 4);
+    return (uint32_t)(c < 1 ? 1 : c > 256 ? 256 : c);
+}
+
+int sg_engine_exchange_rows(sg_engine* e, uint64_t* rows) {
+    if (!e || !rows) return SG_ERR_INVAL;
+    *rows = e->d.xrows;
+    return SG_OK;
+}
+
+int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap) {
+    if (!e || exchange_cap == 0) {
+        sg_set_error("sg_engine_set_exchange_cap: exchange_cap must be > 0");
+        return SG_ERR_INVAL;
+    }
+    e->d.xcap = exchange_cap;
+    e->d.xrows = HDR + exchange_cap;
+    return SG_OK;
+}
+
+int sg_engine_exchange_peak(sg_engine* e, uint64_t* peak, int reset) {
+    if (!e) return SG_ERR_INVAL;
+    int rc = read_rs(e);
+    if (rc) return rc;
+    if (peak) *peak = e->h_rs->peak_peer;
+    if (reset) HIPCHK(hipMemsetAsync(&e->d.rs->peak_peer, 0, 8, e->stream));
+    return SG_OK;
+}
+
+int sg_engine_step_send(sg_engine* e, int64_t* send) {
+    int rc = need_sharded(e, "sg_engine_step_send");
+    if (rc) return rc;
+    if (!send) {
+        sg_set_error("sg_engine_step_send: NULL send buffer");
+        return SG_ERR_INVAL;
+    }
     if ((rc = enqueue_process(e))) return rc;
     const Dev& d = e->d;
-    if (d.G > 1) {
-        if (!send || !send_counts) {
-            sg_set_error("sg_engine_step_process: sharded engine needs send buffers");
-            return SG_ERR_INVAL;
-        }
-        hipLaunchKernelGGL(k_peer_scan, dim3(1), dim3(MAXG), 0, e->stream, d, send_counts);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_pack, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d, send);
-        HIPCHK(hipGetLastError());
-    }
-    return SG_OK;
+    return timed_launch(e, 2, [&] {
+        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, d, (uint64_t*)nullptr, 0);
+        hipLaunchKernelGGL(k_peer_scan, dim3(1), dim3(1024), 0, e->stream, d);
+        hipLaunchKernelGGL(k_pack, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+        hipLaunchKernelGGL(k_fill, dim3(fill_chunks(d), d.G), dim3(BLOCK), 0, e->stream, d, send);
+    });
 }
 
-int sg_engine_step_insert(sg_engine* e, const int64_t* recv, uint64_t n_recv) {
-    if (!e || !e->booted) return SG_ERR_STATE;
-    int rc;
+int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
+    int rc = need_sharded(e, "sg_engine_step_recv");
+    if (rc) return rc;
+    if (!recv) {
+        sg_set_error("sg_engine_step_recv: NULL receive buffer");
+        return SG_ERR_INVAL;
+    }
     if ((rc = enqueue_local_insert(e))) return rc;
-    if (n_recv) {
-        const Dev& d = e->d;
-        uint32_t grid = (uint32_t)((n_recv + BLOCK - 1) / BLOCK);
-        if (grid > 2048) grid = 2048;
-        hipLaunchKernelGGL(k_insert_recv, dim3(grid), dim3(BLOCK), 0, e->stream, d, recv, n_recv);
-        HIPCHK(hipGetLastError());
-    }
-    return SG_OK;
-}
-
-int sg_engine_step_reduce(sg_engine* e, uint64_t* out3) {
-    if (!e || !out3) return SG_ERR_INVAL;
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, e->d, out3, 0);
-    HIPCHK(hipGetLastError());
-    return SG_OK;
-}
-
-int sg_engine_step_window(sg_engine* e, const uint64_t* in3) {
-    if (!e || !in3) return SG_ERR_INVAL;
-    hipLaunchKernelGGL(k_window, dim3(1), dim3(1), 0, e->stream, e->d, in3);
-    HIPCHK(hipGetLastError());
-    return SG_OK;
+    const Dev& d = e->d;
+    if ((rc = timed_launch(e, 1, [&] {
+             hipLaunchKernelGGL(k_insert_recv, dim3(fill_chunks(d), d.G), dim3(BLOCK), 0, e->stream, d,
+                                recv);
+         })))
+        return rc;
+    return timed_launch(e, 2, [&] {
+        hipLaunchKernelGGL(k_window, dim3(1), dim3(1), 0, e->stream, d, recv);
+    });
 }
 
 int sg_engine_set_timing(sg_engine* e, int enabled) {

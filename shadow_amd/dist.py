@@ -1,20 +1,26 @@
-"""One process per GPU: PHOLD hosts block-sharded over ranks, one exchange per
-conservative round.
+"""One process per GPU: PHOLD hosts block-sharded over ranks, ONE collective
+per step and no host synchronisation inside the round loop.
 
-Per round:
-  1. process   each shard pops its hosts' events before the barrier; new events
-               for another shard's hosts are packed per owner rank;
-  2. counts    all-to-all of the per-peer counts (G x int64);
-  3. events    all-to-all-v of the packed {time, id, dst<<32|src} triples —
-               RCCL over xGMI on GPUs (torch.distributed "nccl"), gloo on CPU;
-  4. insert    received events go into the destination queues;
-  5. window    all-reduce MIN of {next event time, min discovered jump, ~overflow}
-               — the window barrier (scheduler.c:386-408, master.c:450-480).
+A step:
+  1. step_send   a process step pops each shard's hosts' events before the
+                 barrier; new events for another shard's hosts go to a per-peer
+                 outbox.  Every step copies up to exchange_cap outbox events
+                 per peer into a fixed-size block behind a header that carries
+                 the shard's MIN next time, its min discovered latency and its
+                 overflow flags;
+  2. all-to-all  one all_to_all_single of equal [rows, 3] int64 blocks —
+                 RCCL over xGMI on GPUs (torch.distributed "nccl"), gloo on CPU;
+  3. step_recv   local + received events into the destination queues, then the
+                 window from the G headers: the MIN "all-reduce" of the window
+                 barrier (scheduler.c:386-408, master.c:450-480) rides on the
+                 all-to-all.  If a sender still has outbox leftovers every shard
+                 turns the next step into a drain step (same window, exchange
+                 only); the decision is taken on the device, identically on
+                 every shard, so the host never waits on a count.
 
 The per-shard compute is a backend: ``EngineShard`` (the HIP engine; product
 path) or, in CPU tests only, an oracle-backed shard with the same interface.
-Unsigned 64-bit values travel as int64 with the sign bit flipped so that a
-signed MIN reduction orders them as unsigned.
+Unsigned 64-bit values travel as int64 bit patterns.
 """
 from __future__ import annotations
 
@@ -22,50 +28,48 @@ import contextlib
 import os
 import time
 
-import numpy as np
 import torch
 import torch.distributed as dist
-
-SIGN = 1 << 63
-
-
-def u64_to_i64(x: int) -> int:
-    return (x ^ SIGN) - (1 << 64) if (x ^ SIGN) >= (1 << 63) else (x ^ SIGN)
-
-
-def i64_to_u64(x: int) -> int:
-    return (x & ((1 << 64) - 1)) ^ SIGN
-
 
 def owner_bounds(n_hosts: int, world: int):
     return [(g * n_hosts) // world for g in range(world + 1)]
 
 
+def default_exchange_cap(n_local: int, world: int) -> int:
+    """Per-peer rows per step before tuning: a shard's hosts emit well under one
+    event per host per round in steady state, about 1/world of them per peer."""
+    c = max(4096, -(-n_local // (2 * world)))
+    return -(-c // 256) * 256
+
+
 class EngineShard:
     """Product backend: the HIP round engine on this rank's GPU."""
 
-    def __init__(self, cfg, rank, world, device, exchange_cap=None, queue_cap=0):
+    def __init__(self, cfg, rank, world, device, exchange_cap=None, queue_cap=0, stream=None,
+                 trace_capacity=0):
         from .engine import Engine
         self.dev = torch.device("cuda", device)
         torch.cuda.set_device(self.dev)
-        # a dedicated stream: engine kernels, torch ops and the collectives of a
-        # round are all ordered on it (torch's default stream has handle 0,
+        # a dedicated stream: engine kernels, torch ops and the collective of a
+        # step are all ordered on it (torch's default stream has handle 0,
         # which the C-ABI reads as "make your own stream")
-        self.stream = torch.cuda.Stream(device=self.dev)
-        stream = self.stream.cuda_stream
-        n_local = owner_bounds(cfg["n_hosts"], world)[rank + 1] - owner_bounds(cfg["n_hosts"], world)[rank]
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=self.dev)
+        b = owner_bounds(cfg["n_hosts"], world)
+        n_local = b[rank + 1] - b[rank]
         if exchange_cap is None:
-            # the boot round stages load events per host: size for it
-            exchange_cap = max(4096, n_local * cfg["load"])
-        self.cap = exchange_cap
+            exchange_cap = default_exchange_cap(n_local, world)
         self.world = world
-        self.eng_args = (rank, world)
+        self.rank = rank
         self.eng = Engine(cfg, device=device, shard_index=rank, shard_count=world,
-                          queue_cap=queue_cap, exchange_cap=exchange_cap, stream=stream)
-        self.send = torch.empty((world, exchange_cap, 3), dtype=torch.int64, device=self.dev)
-        self.send_counts = torch.zeros(world, dtype=torch.int64, device=self.dev)
-        self.red = torch.zeros(3, dtype=torch.int64, device=self.dev)
-        self.recv = torch.empty((0, 3), dtype=torch.int64, device=self.dev)
+                          queue_cap=queue_cap, exchange_cap=exchange_cap,
+                          trace_capacity=trace_capacity, stream=self.stream.cuda_stream)
+        self._alloc()
+
+    def _alloc(self):
+        rows = self.eng.exchange_rows()
+        self.rows = rows
+        self.send = torch.zeros((self.world, rows, 3), dtype=torch.int64, device=self.dev)
+        self.recv = torch.zeros_like(self.send)
 
     def stream_ctx(self):
         return torch.cuda.stream(self.stream)
@@ -73,20 +77,21 @@ class EngineShard:
     def boot(self):
         self.eng.boot()
 
-    def process(self):
-        self.eng.step_process(self.send.data_ptr(), self.send_counts.data_ptr())
-        return self.send, self.send_counts
+    def pre(self) -> torch.Tensor:
+        self.eng.step_send(self.send.data_ptr())
+        return self.send
 
-    def insert(self, recv, n):
-        self.recv = recv  # keep alive until the kernel consumed it
-        self.eng.step_insert(recv.data_ptr() if n else 0, n)
+    def post(self):
+        self.eng.step_recv(self.recv.data_ptr())
 
-    def reduce(self):
-        self.eng.step_reduce(self.red.data_ptr())
-        return self.red
+    def set_exchange_cap(self, cap: int):
+        """Between steps; every rank must pass the same value."""
+        self.sync()
+        self.eng.set_exchange_cap(cap)
+        self._alloc()
 
-    def window(self, red):
-        self.eng.step_window(red.data_ptr())
+    def exchange_peak(self, reset: bool = False) -> int:
+        return self.eng.exchange_peak(reset)
 
     def done(self) -> bool:
         return bool(self.eng.stats()["done"])
@@ -98,45 +103,45 @@ class EngineShard:
         self.stream.synchronize()
 
 
-def _flip(t: torch.Tensor) -> torch.Tensor:
-    # unsigned order -> signed order (and back): xor the sign bit
-    return torch.bitwise_xor(t, torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device))
+def _all_to_all(recv: torch.Tensor, send: torch.Tensor):
+    if send.is_cuda and dist.get_backend() == "gloo":
+        # rehearsal only (several ranks on one GPU, where RCCL refuses to run):
+        # gloo exchanges host tensors
+        r = torch.empty(send.shape, dtype=send.dtype)
+        dist.all_to_all_single(r, send.cpu())
+        recv.copy_(r)
+    else:
+        dist.all_to_all_single(recv, send)
 
 
-def exchange(send: torch.Tensor, send_counts: torch.Tensor, world: int):
-    """All-to-all-v of packed triples.  Returns (recv [n, 3], n)."""
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts)
-    sc = send_counts.tolist()  # host sync on the counts (v1 protocol)
-    rc = recv_counts.tolist()
-    parts = [send[p, :sc[p]] for p in range(world)]
-    flat = torch.cat(parts, 0).reshape(-1) if sum(sc) else send.new_zeros(0)
-    recv = send.new_empty(sum(rc) * 3)
-    dist.all_to_all_single(recv, flat, [c * 3 for c in rc], [c * 3 for c in sc])
-    return recv.reshape(-1, 3), sum(rc)
+def run_step(shard, world: int):
+    send = shard.pre()
+    _all_to_all(shard.recv, send)
+    shard.post()
 
 
-def run_round(shard, world: int):
-    send, counts = shard.process()
-    recv, n = exchange(send, counts, world)
-    shard.insert(recv, n)
-    red = shard.reduce()
-    red = _flip(red)
-    dist.all_reduce(red, op=dist.ReduceOp.MIN)
-    red = _flip(red)
-    shard.window(red)
-
-
-def run(shard, world: int, max_rounds: int = 1 << 62, check_every: int = 16) -> int:
+def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16) -> int:
+    """Run steps until the simulation is done (checked every check_every steps)
+    or max_steps; returns the steps run."""
     ctx = shard.stream_ctx() if hasattr(shard, "stream_ctx") else contextlib.nullcontext()
-    r = 0
+    n = 0
     with ctx:
-        while r < max_rounds:
-            run_round(shard, world)
-            r += 1
-            if r % check_every == 0 and shard.done():
+        while n < max_steps:
+            run_step(shard, world)
+            n += 1
+            if n % check_every == 0 and shard.done():
                 break
-    return r
+    return n
+
+
+def run_until_round(shard, world: int, rounds: int, check_every: int = 8) -> int:
+    """Run steps until the shard has completed `rounds` windows (or is done)."""
+    n = 0
+    while True:
+        st = shard.stats()
+        if st["done"] or st["rounds"] >= rounds:
+            return n
+        n += run(shard, world, check_every, check_every=1 << 30)
 
 
 # ------------------------------------------------------------------ bench ----
@@ -146,19 +151,33 @@ def _env_rank():
 
 
 def bench(args):
-    """bench.py --gpus N under torch.distributed.run: strong scaling of the 1M-host
-    PHOLD over N GPUs.  Returns the JSON dict on rank 0, None elsewhere."""
+    """bench.py --gpus N under torch.distributed.run: the 1M-host PHOLD over N
+    GPUs (strong scaling: the host count stays 1M).  Returns the JSON dict on
+    rank 0, None elsewhere."""
     from . import phold
     rank, world, local = _env_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with "
                          "torch.distributed.run --nproc-per-node N")
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = 0 if args.same_device else local
+    torch.cuda.set_device(dev)
+    if args.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:  # rehearsal of the multi-rank path on one GPU
+        dist.init_process_group(args.dist_backend)
     cfg = phold.c4_config(n_hosts=args.hosts)
-    shard = EngineShard(cfg, rank, world, local)
+    shard = EngineShard(cfg, rank, world, dev)
     shard.boot()
-    run(shard, world, args.warmup, check_every=1 << 30)
+    # warmup: the boot round (its outbox drains over several steps), then size
+    # the exchange blocks from the steady-state per-peer peak, the same on every rank
+    run_until_round(shard, world, 2)
+    shard.exchange_peak(reset=True)
+    run_until_round(shard, world, 2 + max(args.warmup, 8))
+    peak = torch.tensor([shard.exchange_peak()], dtype=torch.int64, device=shard.dev)
+    dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+    cap = -(-(int(peak.item()) * 5 // 4 + 256) // 256) * 256
+    shard.set_exchange_cap(cap)
+    run(shard, world, 8, check_every=1 << 30)
     shard.sync()
     s0 = shard.stats()
     dist.barrier()
@@ -171,17 +190,17 @@ def bench(args):
     dt = time.perf_counter() - t0
     dist.barrier()
     s1 = shard.stats()
-    shard.sync()
     t = torch.tensor([dt], dtype=torch.float64, device=shard.dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    pops = torch.tensor([s1["pops"] - s0["pops"], s1["rounds"] - s0["rounds"], s1["overflow"]],
-                        dtype=torch.int64, device=shard.dev)
-    dist.all_reduce(pops, op=dist.ReduceOp.SUM)
+    tot = torch.tensor([s1["pops"] - s0["pops"], s1["rounds"] - s0["rounds"],
+                        s1["exchange_steps"] - s0["exchange_steps"], s1["overflow"]],
+                       dtype=torch.int64, device=shard.dev)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     tmax = float(t.item())
-    total, rounds_sum, ovf = (int(x) for x in pops.tolist())
+    total, rounds_sum, steps_sum, ovf = (int(x) for x in tot.tolist())
     dist.destroy_process_group()
     if ovf:
-        raise SystemExit(f"exchange/queue overflow during bench ({ovf:#x})")
+        raise SystemExit(f"queue/outbox overflow during bench ({ovf:#x})")
     if rank != 0:
         return None
     return {
@@ -201,5 +220,9 @@ def bench(args):
                                "latency (median 30 ms, sigma 0.9, min 1 ms), runahead 1 ms, "
                                "weights rule, seed 1",
                    "n_hosts": args.hosts, "events_timed": total,
-                   "parallelism": f"hosts block-sharded {world} ways, RCCL all-to-all per round"},
+                   "rounds_timed": rounds_sum // world, "drain_steps": (steps_sum - rounds_sum) // world,
+                   "exchange_cap": cap,
+                   "parallelism": f"hosts block-sharded {world} ways, one "
+                                  f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                                  "all-to-all per step"},
     }

@@ -121,17 +121,24 @@ class Engine:
         return {"process": (ms[0], n[0]), "insert": (ms[1], n[1]), "window": (ms[2], n[2])}
 
     # ---------------------------------------------------------- multi shard
-    def step_process(self, send_ptr: int, send_counts_ptr: int):
-        L.check(L.lib().sg_engine_step_process(self.h, send_ptr, send_counts_ptr))
+    def exchange_rows(self) -> int:
+        r = C.c_uint64()
+        L.check(L.lib().sg_engine_exchange_rows(self.h, C.byref(r)))
+        return r.value
 
-    def step_insert(self, recv_ptr: int, n_recv: int):
-        L.check(L.lib().sg_engine_step_insert(self.h, recv_ptr or None, n_recv))
+    def set_exchange_cap(self, cap: int):
+        L.check(L.lib().sg_engine_set_exchange_cap(self.h, cap))
 
-    def step_reduce(self, out3_ptr: int):
-        L.check(L.lib().sg_engine_step_reduce(self.h, out3_ptr))
+    def exchange_peak(self, reset: bool = False) -> int:
+        r = C.c_uint64()
+        L.check(L.lib().sg_engine_exchange_peak(self.h, C.byref(r), int(reset)))
+        return r.value
 
-    def step_window(self, in3_ptr: int):
-        L.check(L.lib().sg_engine_step_window(self.h, in3_ptr))
+    def step_send(self, send_ptr: int):
+        L.check(L.lib().sg_engine_step_send(self.h, send_ptr))
+
+    def step_recv(self, recv_ptr: int):
+        L.check(L.lib().sg_engine_step_recv(self.h, recv_ptr))
 
 
 def probe_hash(trace: np.ndarray) -> tuple[int, int]:

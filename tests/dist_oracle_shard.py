@@ -1,61 +1,112 @@
-"""TEST INFRASTRUCTURE: an oracle-backed shard with EngineShard's interface, so
-the distributed round protocol (shadow_amd.dist) can be exercised on CPU with
-gloo.  Never used by the product path."""
+"""TEST INFRASTRUCTURE: an oracle-backed shard with EngineShard's step
+interface (pre / post around one all-to-all), so the distributed step protocol
+of shadow_amd.dist — fixed-size exchange blocks with headers, drain steps when
+an outbox exceeds exchange_cap, the window from the received headers — can be
+exercised on CPU with gloo.  Mirrors sg_engine.hip's k_fill / k_insert_recv /
+k_window.  Never used by the product path."""
 import numpy as np
 import torch
 
 from oracle import oracle as O
 from shadow_amd.dist import owner_bounds
 
+HDR = 2
+M64 = (1 << 64) - 1
+
+
+def _i64(x: int) -> int:
+    x &= M64
+    return x - (1 << 64) if x >= (1 << 63) else x
+
 
 class OracleShard:
-    def __init__(self, cfg, rank, world):
+    def __init__(self, cfg, rank, world, exchange_cap=64):
         b = owner_bounds(cfg["n_hosts"], world)
         self.bounds = b
         self.world = world
         self.rank = rank
         self.sim = O.Sim(cfg, first_host=b[rank], n_local=b[rank + 1] - b[rank])
+        self.xcap = exchange_cap
+        self.rows = HDR + exchange_cap
+        self.recv = torch.zeros((world, self.rows, 3), dtype=torch.int64)
+        self.phase = 0
+        self.outq = [np.zeros((0, 3), np.int64) for _ in range(world)]
+        self.sent = [0] * world
+        self.loc_min = (1 << 64) - 2
+        self.loc_jmin = M64
+        self.steps = 0
 
     def boot(self):
         self.sim.boot()
 
-    def process(self):
-        self.sim.round_process()
-        out = self.sim.outbox()
-        owner = np.searchsorted(np.array(self.bounds[1:]), out["dst"], side="right")
-        counts = np.bincount(owner, minlength=self.world).astype(np.int64)
-        cap = max(1, int(counts.max()) if len(counts) else 1)
-        send = torch.zeros((self.world, cap, 3), dtype=torch.int64)
-        for p in range(self.world):
-            ev = out[owner == p]
-            if len(ev):
-                tri = np.stack([ev["time"].astype(np.int64), ev["seq"].astype(np.int64),
-                                ((ev["dst"].astype(np.uint64) << np.uint64(32)) |
-                                 ev["src"].astype(np.uint64)).astype(np.int64)], 1)
-                send[p, :len(ev)] = torch.from_numpy(tri)
-        return send, torch.from_numpy(counts)
-
-    def insert(self, recv, n):
-        if n == 0:
-            return
-        r = recv.numpy().astype(np.uint64)
-        ev = np.zeros(n, O.EVENT_DTYPE)
-        ev["time"] = r[:, 0]
-        ev["seq"] = r[:, 1]
-        ev["dst"] = (r[:, 2] >> np.uint64(32)).astype(np.uint32)
-        ev["src"] = (r[:, 2] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-        self.sim.ingest(ev)
-
-    def reduce(self):
-        v = [self.sim.local_min(), self.sim.local_jmin(), (1 << 64) - 1]
-        return torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in v], dtype=torch.int64)
-
-    def window(self, red):
-        vals = [int(x) & ((1 << 64) - 1) for x in red.tolist()]
-        self.sim.window_apply(vals[0], vals[1])
-
-    def done(self):
+    def _done(self):
         return bool(self.sim.stats()["done"])
 
+    def pre(self) -> torch.Tensor:
+        send = torch.zeros((self.world, self.rows, 3), dtype=torch.int64)
+        if self._done():
+            return send
+        if self.phase == 0:
+            self.sim.round_process()
+            out = self.sim.outbox()
+            owner = np.searchsorted(np.array(self.bounds[1:]), out["dst"], side="right")
+            for p in range(self.world):
+                ev = out[owner == p] if p != self.rank else out[:0]
+                self.outq[p] = np.stack([ev["time"].astype(np.int64),
+                                         ((ev["src"].astype(np.uint64) << np.uint64(40)) |
+                                          ev["seq"].astype(np.uint64)).astype(np.int64),
+                                         ev["dst"].astype(np.int64)], 1) if len(ev) else \
+                    np.zeros((0, 3), np.int64)
+            self.sent = [0] * self.world
+            m = self.sim.local_min()
+            if len(out):
+                m = min(m, int(out["time"].min()))
+            self.loc_min = m
+            self.loc_jmin = self.sim.local_jmin()
+        more = any(len(self.outq[q]) - self.sent[q] > self.xcap for q in range(self.world))
+        rounds = self.sim.stats()["rounds"]
+        for p in range(self.world):
+            n = min(self.xcap, len(self.outq[p]) - self.sent[p])
+            send[p, 0] = torch.tensor([n, int(more), _i64(self.loc_min)])
+            send[p, 1] = torch.tensor([_i64(self.loc_jmin), 0, rounds])
+            if n:
+                send[p, HDR:HDR + n] = torch.from_numpy(self.outq[p][self.sent[p]:self.sent[p] + n])
+        return send
+
+    def post(self):
+        if self._done():
+            return
+        r = self.recv.numpy()
+        m = j = M64
+        more = False
+        for p in range(self.world):
+            more |= bool(r[p, 0, 1])
+            m = min(m, int(r[p, 0, 2]) & M64)
+            j = min(j, int(r[p, 1, 0]) & M64)
+            assert int(r[p, 1, 2]) == self.sim.stats()["rounds"], "shards out of step"
+            n = int(r[p, 0, 0])
+            if p == self.rank or n == 0:
+                continue
+            tri = r[p, HDR:HDR + n].astype(np.uint64)
+            ev = np.zeros(n, O.EVENT_DTYPE)
+            ev["time"] = tri[:, 0]
+            ev["seq"] = tri[:, 1] & np.uint64((1 << 40) - 1)
+            ev["src"] = (tri[:, 1] >> np.uint64(40)).astype(np.uint32)
+            ev["dst"] = tri[:, 2].astype(np.uint32)
+            self.sim.ingest(ev)
+        for q in range(self.world):
+            self.sent[q] += min(self.xcap, len(self.outq[q]) - self.sent[q])
+        self.steps += 1
+        if more:
+            self.phase = 1
+            return
+        self.phase = 0
+        self.sim.window_apply(m, j)
+
+    def done(self):
+        return self._done()
+
     def stats(self):
-        return self.sim.stats()
+        st = self.sim.stats()
+        st["exchange_steps"] = self.steps
+        return st

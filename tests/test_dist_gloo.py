@@ -1,7 +1,8 @@
-"""CPU, world size 2 and 3 over gloo: the distributed round protocol of
-shadow_amd.dist (per-round all-to-all of new events + MIN all-reduce window)
-reproduces the unsharded simulation exactly (per-host digests, pops, RNG
-states, event counters, global counters)."""
+"""CPU, world size 2 and 3 over gloo: the distributed step protocol of
+shadow_amd.dist (one all-to-all of fixed-size blocks per step, the window from
+the block headers, drain steps when an outbox exceeds the block) reproduces
+the unsharded simulation exactly (per-host digests, pops, RNG states, event
+counters, global counters)."""
 import os
 import socket
 
@@ -22,13 +23,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cfg, q):
+def _worker(rank, world, port, cfg, xcap, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from tests.dist_oracle_shard import OracleShard
     from shadow_amd import dist as D
-    sh = OracleShard(cfg, rank, world)
+    sh = OracleShard(cfg, rank, world, exchange_cap=xcap)
     sh.boot()
     rounds = D.run(sh, world, check_every=4)
     st = sh.sim.host_state()
@@ -37,11 +38,11 @@ def _worker(rank, world, port, cfg, q):
     dist.destroy_process_group()
 
 
-def _run(cfg, world):
+def _run(cfg, world, xcap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, cfg, xcap, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -51,13 +52,14 @@ def _run(cfg, world):
     return sorted(res, key=lambda x: x[0])
 
 
-@pytest.mark.parametrize("world,kind", [(2, "tiny"), (3, "lossy"), (2, "probe10")])
-def test_sharded_protocol_matches_unsharded(world, kind):
+@pytest.mark.parametrize("world,kind,xcap", [(2, "tiny", 64), (3, "lossy", 16), (2, "probe10", 4096),
+                                             (2, "tiny", 3)])
+def test_sharded_protocol_matches_unsharded(world, kind, xcap):
     from oracle import oracle as O
     cfg = {"tiny": lambda: phold.tiny_config(n_hosts=200, V=6, load=4, end_time_s=0.4),
            "lossy": lambda: phold.tiny_config(n_hosts=151, V=5, load=3, loss=0.3, end_time_s=0.3),
            "probe10": lambda: phold.probe_config(n_hosts=120, jump_ms=10, end_time_s=0.3)}[kind]()
-    res = _run(cfg, world)
+    res = _run(cfg, world, xcap)
     ref = O.Sim(cfg)
     ref.boot()
     ref.run()
@@ -70,6 +72,9 @@ def test_sharded_protocol_matches_unsharded(world, kind):
     want = ref.stats()
     for k, v in tot.items():
         assert v == want[k], (k, v, want[k])
-    for r in res:  # every rank ran the same windows and ended in the same state
+    for r in res:  # every rank ran the same windows and steps, and ended in the same state
         assert r[2]["rounds"] == want["rounds"]
         assert r[2]["window_start"] == want["window_start"]
+        assert r[2]["exchange_steps"] == res[0][2]["exchange_steps"]
+    if xcap <= 16:  # small blocks: the boot round's outbox must have drained over extra steps
+        assert res[0][2]["exchange_steps"] > want["rounds"]
