@@ -2,7 +2,7 @@
 BASELINE.json metric's workload: synthetic PHOLD, 1M hosts x 16 events,
 log-normal latency over 1024 vertices, runahead 1 ms (configs[3]).
 
-A step is one conservative round (process → insert → window) over the whole
+A step is one conservative round (gather → process → insert → plan) over the whole
 host population.  W warmup rounds (the boot round included) run untimed; K
 rounds are timed between a barrier + device synchronisation on both sides.
 value = committed events (executed pops) in the K rounds, all ranks, / max
@@ -11,7 +11,7 @@ and new events cross shards each round through RCCL all-to-all; the total
 host count stays 1M (strong scaling, as the metric names it).
 
 Also reported:
-  roofline     dominant kernel (k_process): algorithmic bytes (64 B per
+  roofline     dominant kernel (k_proc): algorithmic bytes (64 B per
                committed event + 24 B per active host-round)
                per launch / its average launch time (HIP events on the engine
                stream), against 8 TB/s HBM.
@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
 PMC_JSON = os.path.join(ROOT, "profiles", "r01", "bench_default", "pmc.json")
-DOMINANT = "k_process<true>"
+DOMINANT = "k_proc"
 
 
 def pmc_traffic(n_hosts):

@@ -11,11 +11,13 @@
  *   1. Host-side restatements of the reference arithmetic that feeds the device
  *      tables (glibc rand_r streams, the seed chain, host attachment, direct-path
  *      delay/reliability resolution, PHOLD destination weights, window logic).
- *   2. The device engine: per-host event queues resident in HBM, one conservative
- *      round = process (pop every event before the barrier in event_compare order,
- *      run the PHOLD body, resolve delivery times and drops) → insert (deliver the
- *      new events into the destination queues, barrier bump applied) → window
- *      (MIN next-event time + min-latency runahead → next [start, end)).
+ *   2. The device engine: an HBM-resident calendar of time buckets; one
+ *      conservative round = gather (the window's due events, counting-sorted by
+ *      host partition) → process (per host, pop every event before the barrier
+ *      in event_compare order, run the PHOLD body, resolve delivery times and
+ *      drops, barrier bump) → insert (new events into their time buckets) →
+ *      plan (MIN next-event time + min-latency runahead → next [start, end),
+ *      the next window's due chunks).
  */
 #ifndef SHADOWGPU_H
 #define SHADOWGPU_H
@@ -27,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 2
+#define SG_ABI_VERSION 3
 
 typedef uint64_t sg_simtime;                /* SimulationTime, core/support/definitions.h:18 */
 #define SG_SIMTIME_INVALID UINT64_MAX       /* definitions.h:28 */
@@ -141,7 +143,9 @@ typedef struct sg_phold_params {
     uint32_t load;           /* messages each host sends when it boots (test_phold.c:234-239) */
     uint32_t dst_rule;       /* enum sg_dst_rule */
     uint32_t window_rule;    /* enum sg_window_rule */
-    uint32_t queue_cap;      /* event slots per host in HBM (0 = default 64) */
+    uint32_t queue_cap;      /* HBM event capacity per local host: the calendar's
+                                chunk pool holds n_local * queue_cap events
+                                (0 = default 64); running out is SG_ERR_OVERFLOW */
     uint32_t shard_index;    /* this rank */
     uint32_t shard_count;    /* ranks; hosts are block-partitioned */
     sg_simtime end_time;     /* scheduler endTime (scheduler.c:343) */
@@ -205,7 +209,7 @@ int sg_engine_boot(sg_engine* e);
 /* Single shard: runs up to max_rounds windows without host round-trips, in
  * batches of `batch` rounds per host synchronisation; stops when done. */
 int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch);
-/* Enqueue one round (process + insert + window) without synchronising. */
+/* Enqueue one round (gather + process + insert + plan) without synchronising. */
 int sg_engine_enqueue_round(sg_engine* e);
 int sg_engine_sync(sg_engine* e);
 int sg_engine_stats(sg_engine* e, sg_round_stats* out);   /* synchronises */
@@ -219,6 +223,19 @@ int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t
 /* Executed windows {start, end} per round (recorded when trace_capacity > 0). */
 int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);
 void* sg_engine_stream(sg_engine* e);
+
+/* Calendar geometry chosen at create. */
+typedef struct sg_engine_geom {
+    uint64_t bucket_width;    /* W ns: the narrowest window the rules allow */
+    uint32_t ring_buckets;    /* R: covers the widest window + the longest delay */
+    uint32_t chunk_events;    /* events per pool chunk */
+    uint32_t chunks;          /* pool chunks */
+    uint32_t partition_hosts; /* HP: hosts per k_proc workgroup */
+    uint32_t partitions;      /* P */
+    uint32_t partition_cap;   /* due events one partition can take per round */
+    uint32_t stage_cap;       /* new events one partition can stage per round */
+} sg_engine_geom;
+int sg_engine_geometry(sg_engine* e, sg_engine_geom* out);
 
 /* Multi-shard step, driven by the caller around ONE all-to-all per step (no
  * host synchronisation, no all-reduce):
@@ -243,9 +260,16 @@ int sg_engine_exchange_peak(sg_engine* e, uint64_t* peak, int reset);
 int sg_engine_step_send(sg_engine* e, int64_t* send);
 int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
 
-/* Kernel timing of the last sg_engine_run/enqueue (HIP events on the engine
- * stream): total ms per kernel class {process, insert, window}, and launches. */
-int sg_engine_kernel_times(sg_engine* e, double* ms3, uint64_t* launches);
+/* Kernel timing since sg_engine_set_timing(e, 1) (HIP events on the engine
+ * stream): total ms and launches per kernel class, arrays of SG_KCLASSES. */
+enum sg_kernel_class {
+    SG_K_PROCESS = 0,  /* k_proc: per-host pops + PHOLD body + send resolution */
+    SG_K_INSERT = 1,   /* k_ins: new / received events into time buckets */
+    SG_K_PLAN = 2,     /* k_plan (+ k_locmin, k_pack, k_fill when sharded) */
+    SG_K_GATHER = 3,   /* k_gather: due chunks → host partitions */
+    SG_KCLASSES = 4
+};
+int sg_engine_kernel_times(sg_engine* e, double* ms, uint64_t* launches);
 int sg_engine_set_timing(sg_engine* e, int enabled);
 
 /* ------------------------------------------------------------------------ */

@@ -58,6 +58,18 @@ class RoundStats(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
+class EngineGeom(C.Structure):
+    _fields_ = [("bucket_width", C.c_uint64)] + [(n, C.c_uint32) for n in
+                ("ring_buckets", "chunk_events", "chunks", "partition_hosts", "partitions",
+                 "partition_cap", "stage_cap")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+KERNEL_CLASSES = ("process", "insert", "plan", "gather")  # enum sg_kernel_class
+
+
 class WindowState(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("min_jump", "next_min_jump", "min_jump_config", "end_time")]
 
@@ -76,7 +88,7 @@ EXPORTS = [
     "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
     "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv", "sg_engine_kernel_times",
-    "sg_engine_set_timing", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
+    "sg_engine_set_timing", "sg_engine_geometry", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
 ]
@@ -131,6 +143,7 @@ def lib():
     L.sg_engine_step_recv.argtypes = [C.c_void_p, C.c_void_p]
     L.sg_engine_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sg_engine_set_timing.argtypes = [C.c_void_p, C.c_int]
+    L.sg_engine_geometry.argtypes = [C.c_void_p, C.POINTER(EngineGeom)]
     _lib = L
     return L
 

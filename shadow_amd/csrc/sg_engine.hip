@@ -1,39 +1,52 @@
 // sg_engine.hip — MI355X (gfx950) device engine of libshadowgpu.
 //
-// One conservative round of Shadow's host-family scheduler on HBM-resident
-// per-host queues (contract: include/shadowgpu.h; design: DESIGN.md):
+// One conservative round of Shadow's host-family scheduler (contract:
+// include/shadowgpu.h; design: DESIGN.md) on an HBM-resident calendar:
 //
-//   k_process  one lane per host. Pops every queued event with time < barrier in
-//              event_compare order (core/work/event.c:110-153) — self events it
-//              creates inside the window included (host_single.c:237-267) — and
-//              runs the PHOLD body: destination draw (test_phold.c:160-178),
-//              reliability draw + ceil delay (worker.c:243-304), srcHostEventID
-//              (event.c:38), endTime drop (scheduler.c:343), barrier bump
-//              (host_single.c:180-184). New events are staged per workgroup.
-//   k_pack     (multi-shard) moves staged events owned by other shards into the
-//              per-peer outbox; k_fill copies up to exchange_cap of them per peer
-//              into the fixed-size blocks of the RCCL all-to-all, behind a header
-//              that also carries this shard's MIN terms (so no all-reduce).
-//   k_insert   delivers staged / received events into destination queues and
-//              keeps each host's earliest queued time.
-//   k_reduce   MIN next event time (host_single.c:273-305, scheduler.c:393-398),
-//              the minimum discovered latency (topology.c:1374-1385) and, for a
-//              single shard, the next window (master.c:450-480).
+//   events      live in time buckets of width W (a ring of R buckets), each a
+//               list of 1024-event chunks.  A round reads only the buckets its
+//               window [S, E) covers, never a host's whole queue.
+//   k_gather    streams the due buckets' chunks and counting-sorts the events
+//               with t < E by host partition (HP consecutive hosts; LDS
+//               histogram, one reservation per workgroup and partition).  The
+//               window's last bucket may straddle E: its due events are
+//               tombstoned in place, the rest stay (their MIN is the carry min).
+//   k_proc      one workgroup per partition: LDS counting sort of the
+//               partition's due events by host, compaction of the active hosts,
+//               then one lane per active host pops its events in event_compare
+//               order (core/work/event.c:110-153), same-round self events
+//               included (host_single.c:237-267), and runs the PHOLD body:
+//               destination draw (test_phold.c:160-178), reliability draw +
+//               ceil delay (worker.c:243-304), srcHostEventID (event.c:38),
+//               endTime drop (scheduler.c:343), barrier bump
+//               (host_single.c:180-184).  New events are staged per partition.
+//   k_count     staged (and, multi-shard, received) events → bucket counts:
+//               LDS histogram by bucket, one atomic reservation per
+//               (workgroup, bucket); the reserved bases are kept for k_scatter.
+//   k_plan      one workgroup: frees the consumed chunks, gives every bucket
+//               the chunks its new count needs (free ring), MIN next time
+//               (host_single.c:273-305, scheduler.c:393-398: the per-workgroup
+//               minima plus the first non-empty bucket beyond the window),
+//               discovery minimum (topology.c:1374-1385), next window
+//               (master.c:450-480), and lists the next window's due chunks.
+//   k_scatter   the counted events into their reserved chunk slots.
+// Chunk tables are written only by k_boot / k_plan and read by later kernels,
+// so no workgroup ever waits on another inside a launch.
+//   multi-shard k_locmin / k_pack / k_fill build the fixed-size exchange blocks
+//               (the header carries the shard's MIN terms); k_plan reads the G
+//               headers back instead of the local minima.
 //
-// HBM layout:
-//   queue slot   16 B {time, key}, key = src << 40 | srcHostEventID: with the
-//                destination implied by the queue, event_compare is the
-//                lexicographic order of (time, key)
-//   queues       host-major, slot j of local host h at [h * CAP + j]: a round
-//                reads only the queues of hosts with an event before the barrier
-//   per pair     16 B {ceil delay ns, keep threshold, truncated ms}: one random
-//                access per send
-//   per host     8 B {weight threshold, vertex} (read-only, all N hosts) and
-//                32 B {rand_r state, event counter, pops, digest} (local hosts)
-// Compiled with -ffp-contract=off: the only FP is the FP64 floor destination
-// rule, which must round exactly as the reference does.
+// HBM layout: 16-B records everywhere.
+//   bucket record     {dst_local << 40 | (t - b*W),  src << 40 | srcHostEventID}
+//   partition record  {host_in_partition << 52 | (t - S), key}
+//   staged record     {dst_local << 40 | (t - S), key}
+// With the destination fixed, event_compare is the lexicographic order of
+// (time, src << 40 | srcHostEventID).  Compiled with -ffp-contract=off: the
+// only FP is the FP64 floor destination rule, which must round as the
+// reference does.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,24 +58,50 @@ extern "C" void sg_set_error(const char* fmt, ...);
 
 namespace {
 
-constexpr int BLOCK = 256;
 constexpr int MAXG = 64;  // max shards
 constexpr uint64_t SIMTIME_MAX = UINT64_MAX - 1;
 constexpr int SRC_SHIFT = 40;
 constexpr uint64_t SEQ_MASK = (1ULL << SRC_SHIFT) - 1;
+constexpr uint64_t M40 = (1ULL << 40) - 1;
+constexpr uint64_t M52 = (1ULL << 52) - 1;
+constexpr uint64_t TOMB = ~0ULL;
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+constexpr int CH_SHIFT = 10;
+constexpr uint32_t CH = 1u << CH_SHIFT;  // events per chunk (16 KB)
+constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
+constexpr uint32_t HPMAX = 4096;         // hosts per partition
+constexpr uint32_t PMAX = 4096;          // partitions
+constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
+constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
+constexpr uint32_t SRCMAX = PMAX + MAXG;              // k_count / k_scatter sources
+constexpr uint32_t SRC_PER = (SRCMAX + K3_T - 1) / K3_T;
+constexpr uint32_t RETAINED = 1u << 31;
 // exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
 constexpr int HDR = 2;
 enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND };
+// overflow flags
+enum Ovf : uint64_t {
+    OV_PROC = 1, OV_PART = 2, OV_POOL = 4, OV_XCHG = 8, OV_STEP = 16, OV_HORIZON = 32,
+    OV_BUG = 128  // internal inconsistency caught by a bounds guard
+};
 
 enum Ctr {
     C_POPS = 0, C_BOOTS, C_SENDS, C_NULL, C_DROPREL, C_DROPEND, C_BUMPED, C_SAME,
     C_ACTIVE, C_EMIT, NCTR
 };
-enum Mins { M_JMIN = 0, M_EMIN, M_RMIN, NMIN };
 
+struct Rec {
+    uint64_t a;
+    uint64_t k;  // src << 40 | srcHostEventID
+};
 struct Slot {
-    uint64_t t;   // event time
-    uint64_t k;   // src << 40 | srcHostEventID
+    uint64_t t;
+    uint64_t k;
+};
+struct DueEnt {
+    uint32_t id;      // chunk
+    uint32_t nflags;  // events in the chunk | RETAINED
+    uint64_t base;    // bucket start time b*W
 };
 struct HostInfo {
     int32_t wt;       // PHOLD weight threshold (test_phold.c:160-178)
@@ -88,6 +127,15 @@ struct RoundState {
     uint64_t trace_len;
     uint64_t ctr[NCTR];
     uint64_t last_min;
+    // calendar
+    uint64_t bS, bL;         // due bucket range of the current window (absolute indices)
+    uint64_t rmin;           // min time in buckets beyond bL (exact, at plan time)
+    uint64_t ndue;           // due chunk entries
+    uint64_t ndueb;          // listed non-retained buckets (reset at the next plan)
+    uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
+    uint64_t fl_head, fl_tail;
+    uint64_t ins_local;      // k_count took the staged local events (process step)
+    uint64_t ins_S;          // their window start (staged times are relative to it)
     // multi-shard step protocol
     uint64_t phase;      // 0: process step, 1: drain step (outbox leftovers only)
     uint64_t loc_min;    // this shard's MIN next time of the round being exchanged
@@ -97,31 +145,51 @@ struct RoundState {
 };
 
 struct Dev {
-    uint32_t N, V, L, lo, CAP, load, dst_rule, window_rule, G, g, nblocks, bcap;
+    uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
+    uint32_t R, NCH, HP, hp_shift, P, CAPP, ECAP, G1, G3;
+    uint64_t W;
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
     const PairRec* pairs;     // [V*V]
-    Slot* bag;                // [L][CAP]
-    uint32_t* bag_cnt;        // [L]
-    uint64_t* hmin;           // [L]
     HostState* hs;            // [L]
-    uint64_t* pmin;           // [NMIN][nblocks], this round
-    uint64_t* pcum;           // [NCTR][nblocks], cumulative
-    uint32_t* blockcnt;       // [nblocks] staged events
-    uint32_t* peercnt;        // [nblocks][G]
-    uint32_t* peeroff;        // [nblocks][G]
-    int64_t* outq;            // [nblocks * bcap][3] per-peer outbox, peer p at peer_base[p]
+    // calendar
+    Rec* pool;                // [NCH][CH]
+    uint32_t* btab;           // [R][NCH] chunk ids of each bucket
+    uint32_t* bcnt;           // [R] records appended (tombstones included)
+    uint32_t* btomb;          // [R] tombstones
+    uint64_t* bmin;           // [R] min live time
+    uint32_t* fring;          // [NCH] free chunk ring
+    uint32_t* nal;            // [R] chunks allocated to each bucket
+    uint32_t* wbase;          // [G3][R] k_count's reserved base per (workgroup, bucket)
+    DueEnt* due;              // [NCH]
+    uint32_t* dueb;           // [R] ring slots of the listed non-retained buckets
+    // partitions
+    uint32_t* pcnt;           // [P] due events of the partition this round
+    Rec* part;                // [P][CAPP]
+    Rec* part2;               // [P][CAPP] sorted by host
+    Rec* extras;              // [P][K2_T][XCAP]
+    uint32_t* rcnt;           // [P] staged local events
+    Rec* loc;                 // [P][ECAP]
+    // per-workgroup partials
+    uint64_t* c1min;          // [G1] carry min
+    uint64_t* p2min;          // [2][P] emitted min, discovery min
+    uint64_t* pcum;           // [NCTR][P] cumulative counters
+    // multi-shard
+    uint32_t* remn;           // [P] staged events for other shards
+    Slot* rem;                // [P][ECAP]
+    uint32_t* rem_dst;        // [P][ECAP]
+    uint32_t* peercnt;        // [P][G]
+    uint32_t* peeroff;        // [P][G]
+    int64_t* outq;            // [P*ECAP][3] per-peer outbox, peer p at peer_base[p]
     uint64_t* peer_base;      // [G]
-    uint64_t* outn;           // [G] events in peer p's outbox this round
-    uint64_t* sent;           // [G] of which already sent
-    Slot* st;                 // staging, bcap per block
-    uint32_t* st_dst;
+    uint64_t* outn;           // [G]
+    uint64_t* sent;           // [G]
+    // debug
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
     RoundState* rs;
-    uint64_t* red3;           // single-shard reduce output
 };
 
 __device__ __forceinline__ int32_t dev_rand_r(uint32_t& state) {
@@ -232,10 +300,52 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
     return v;
 }
 
+// Workgroup-wide reductions through a [16] LDS scratch (blocks of <= 1024);
+// every thread of the block must call them.
+__device__ __forceinline__ uint64_t block_min(uint64_t v, uint64_t* s16) {
+    v = wave_min(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if (lane == 0) s16[wid] = v;
+    __syncthreads();
+    uint64_t r = s16[0];
+    for (int w = 1; w < nw; ++w) r = s16[w] < r ? s16[w] : r;
+    return r;
+}
+__device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if (lane == 0) s16[wid] = v;
+    __syncthreads();
+    uint64_t r = 0;
+    for (int w = 0; w < nw; ++w) r += s16[w];
+    return r;
+}
+// Exclusive scan across the workgroup; *total gets the sum.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s16, uint64_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(x, o, 64);
+        if (lane >= o) x += u;
+    }
+    __syncthreads();
+    if (lane == 63) s16[wid] = x;
+    __syncthreads();
+    uint64_t add = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        if (w < wid) add += s16[w];
+        tot += s16[w];
+    }
+    *total = tot;
+    return x - v + add;
+}
+
 // event_compare with equal dst (event.c:122-148) on (time, src<<40|seq).
 // Bitwise, not short-circuit, and the running minimum is updated through one
-// select mask: ROCm 7.2 mis-compiled the branchy form inside the selection
-// loop (the winning slot index was not updated on a time tie).
+// select mask: ROCm 7.2 mis-compiled the branchy form inside a selection
+// loop (the winning index was not updated on a time tie).
 __device__ __forceinline__ bool key_less(uint64_t t, uint64_t k, uint64_t bt, uint64_t bk) {
     return (t < bt) | ((t == bt) & (k < bk));
 }
@@ -250,22 +360,40 @@ __device__ __forceinline__ void best_take(Best& b, uint64_t t, uint64_t k, uint3
     b.slot = take ? slot : b.slot;
 }
 
+__device__ __forceinline__ void flag(const Dev& d, uint64_t f) {
+    atomicOr((unsigned long long*)&d.rs->overflow, (unsigned long long)f);
+}
+
+// ----------------------------------------------------------------- boot ----
+// worker_bootHosts: one self event per host at t=0 carrying id 0 (event.c:38),
+// all in bucket 0 (chunks 0.. in order); the free ring holds the rest.
 __global__ void k_boot(Dev d) {
-    const uint32_t lh = blockIdx.x * BLOCK + threadIdx.x;
-    if (lh < d.L) {
-        const uint32_t h = d.lo + lh;
-        // worker_bootHosts: self event at t=0 carrying id 0 (event.c:38)
-        d.bag[(size_t)lh * d.CAP] = Slot{0, (uint64_t)h << SRC_SHIFT};
-        d.bag_cnt[lh] = 1;
-        d.hmin[lh] = 0;
-        HostState s = d.hs[lh];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nb0 = (d.L + CH - 1) >> CH_SHIFT;
+    if (i < d.L) {
+        const uint32_t h = d.lo + i;
+        d.pool[i] = Rec{(uint64_t)i << 40, (uint64_t)h << SRC_SHIFT};
+        HostState s = d.hs[i];
         s.evc = 1;
         s.pops = 0;
         s.digest = 0;
-        d.hs[lh] = s;
+        d.hs[i] = s;
     }
-    if (threadIdx.x < NCTR) d.pcum[(size_t)threadIdx.x * d.nblocks + blockIdx.x] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (i < d.NCH) d.fring[i] = i;
+    if (i < nb0) d.btab[i] = i;  // bucket 0 is ring slot 0
+    if (i < d.R) {
+        d.nal[i] = i == 0 ? nb0 : 0;
+        d.bcnt[i] = i == 0 ? d.L : 0;
+        d.btomb[i] = 0;
+        d.bmin[i] = i == 0 ? 0 : UINT64_MAX;
+    }
+    if (i < d.P) {
+        d.pcnt[i] = 0;
+        d.rcnt[i] = 0;
+        if (d.remn) d.remn[i] = 0;
+        for (int c = 0; c < NCTR; ++c) d.pcum[(size_t)c * d.P + i] = 0;
+    }
+    if (i == 0) {
         RoundState* rs = d.rs;
         rs->S = 0;  // slave.c:431
         rs->E = 1;
@@ -276,23 +404,114 @@ __global__ void k_boot(Dev d) {
         rs->jmin = UINT64_MAX;
         rs->overflow = 0;
         rs->trace_len = 0;
-        for (int i = 0; i < NCTR; ++i) rs->ctr[i] = 0;
+        for (int c = 0; c < NCTR; ++c) rs->ctr[c] = 0;
         rs->last_min = 0;
+        rs->bS = rs->bL = 0;
+        rs->rmin = SIMTIME_MAX;
+        rs->ndue = 0;
+        rs->ndueb = 0;
+        rs->ret_b = UINT64_MAX;
+        rs->fl_head = nb0;
+        rs->fl_tail = d.NCH;
+        rs->ins_local = 0;
+        rs->ins_S = 0;
         rs->phase = 0;
         rs->loc_min = SIMTIME_MAX;
         rs->loc_jmin = UINT64_MAX;
         rs->steps = 0;
         rs->peak_peer = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x < d.G && d.outn) {
-        d.outn[threadIdx.x] = 0;
-        d.sent[threadIdx.x] = 0;
-        d.peer_base[threadIdx.x] = 0;
+    if (i < d.G && d.outn) {
+        d.outn[i] = 0;
+        d.sent[i] = 0;
+        d.peer_base[i] = 0;
     }
 }
 
+// --------------------------------------------------------------- gather ----
+// Due chunks → partition regions: two passes over the workgroup's chunks
+// (LDS histogram + one reservation per partition, then the scatter).
+__global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
+    const RoundState* rs = d.rs;
+    if (rs->done | rs->phase) return;
+    __shared__ uint32_t s_cnt[PMAX];
+    __shared__ uint32_t s_cur[PMAX];
+    __shared__ uint64_t s16[16];
+    const uint64_t S = rs->S, E = rs->E;
+    const uint64_t nd = rs->ndue;
+    const uint64_t c0 = nd * blockIdx.x / gridDim.x, c1 = nd * (blockIdx.x + 1) / gridDim.x;
+    const uint32_t P = d.P, sh = d.hp_shift, hmask = d.HP - 1;
+    for (uint32_t p = threadIdx.x; p < P; p += K1_T) s_cnt[p] = 0;
+    __syncthreads();
+    uint64_t cmin = UINT64_MAX;
+    for (uint64_t c = c0; c < c1; ++c) {
+        const DueEnt de = d.due[c];
+        const bool ok = de.id < d.NCH;
+        if (!ok && de.id != EMPTY && threadIdx.x == 0) flag(d, OV_BUG);
+        const uint32_t n = ok ? de.nflags & 0xFFFFu : 0;
+        const Rec* ch = d.pool + ((size_t)(ok ? de.id : 0) << CH_SHIFT);
+        for (uint32_t i = threadIdx.x; i < n; i += K1_T) {
+            const uint64_t a = ch[i].a;
+            if (a == TOMB) continue;
+            const uint64_t t = de.base + (a & M40);
+            if ((uint32_t)(a >> 40) >= d.L) {
+                flag(d, OV_BUG);
+                continue;
+            }
+            if (t < E) atomicAdd(&s_cnt[(uint32_t)(a >> 40) >> sh], 1u);
+            else cmin = t < cmin ? t : cmin;
+        }
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
+        const uint32_t c = s_cnt[p];
+        if (c) {
+            const uint32_t base = atomicAdd(&d.pcnt[p], c);
+            if (base + c > d.CAPP) flag(d, OV_PART);
+            s_cnt[p] = base;
+        }
+        s_cur[p] = 0;
+    }
+    __syncthreads();
+    uint64_t ntomb = 0;
+    for (uint64_t c = c0; c < c1; ++c) {
+        const DueEnt de = d.due[c];
+        const bool ok = de.id < d.NCH;
+        const uint32_t n = ok ? de.nflags & 0xFFFFu : 0;
+        const bool ret = (de.nflags & RETAINED) != 0;
+        Rec* ch = d.pool + ((size_t)(ok ? de.id : 0) << CH_SHIFT);
+        for (uint32_t i = threadIdx.x; i < n; i += K1_T) {
+            const Rec r = ch[i];
+            if (r.a == TOMB) continue;
+            const uint64_t t = de.base + (r.a & M40);
+            if (t >= E) continue;
+            const uint32_t dl = (uint32_t)(r.a >> 40);
+            if (dl >= d.L) continue;
+            const uint32_t p = dl >> sh;
+            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            if (slot < d.CAPP)
+                d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl & hmask) << 52) | (t - S), r.k};
+            if (ret) {
+                ch[i].a = TOMB;
+                ++ntomb;
+            }
+        }
+    }
+    const uint64_t m = block_min(cmin, s16);
+    const uint64_t nt = block_sum(ntomb, s16);
+    if (threadIdx.x == 0) {
+        d.c1min[blockIdx.x] = m;
+        if (rs->ret_b != UINT64_MAX) {
+            const uint32_t rb = (uint32_t)(rs->ret_b % d.R);
+            if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
+            if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)m);
+        }
+    }
+}
+
+// ----------------------------------------------------------------- proc ----
 struct Acc {
-    uint64_t ctr[NCTR];
+    uint32_t ctr[NCTR];
     uint64_t jmin;   // min truncated latency of attempted sends
     uint64_t emin;   // min time of staged (emitted) events
     bool overflow;
@@ -303,14 +522,19 @@ struct HostCtx {
     HostState s;
 };
 
+struct ProcShared {
+    uint32_t nloc, nrem;
+    uint32_t peer[MAXG];
+};
+
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
-// Self events that fall inside the window go back to the host's own queue
-// through `append` (they are popped later this round); everything else is
-// staged in the workgroup's region for k_insert / k_pack.
+// Self events that fall inside the window go to the lane's same-round list
+// through `append`; everything else is staged for k_count (this shard) or for
+// the outbox (other shards).
 template <class Append>
-__device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx& c, Acc& a, uint64_t bt,
-                                              uint64_t bk, uint32_t* s_emit, uint32_t* s_peer,
-                                              Append append) {
+__device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t E, uint32_t part,
+                                              HostCtx& c, Acc& a, uint64_t bt, uint64_t bk,
+                                              ProcShared& sh, Append append) {
     const uint32_t bsrc = (uint32_t)(bk >> SRC_SHIFT);
     const uint64_t bseq = bk & SEQ_MASK;
     c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
@@ -358,44 +582,97 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t E, HostCtx&
         const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | sq;
         if (dst == c.h && tn < E) {
             ++a.ctr[C_SAME];
-            if (!append(tn, key)) a.overflow = true;
+            if (!append(tn - S, key)) a.overflow = true;
             continue;
         }
         if (dst != c.h && tn < E) {  // host_single.c:180-184
             tn = E;
             ++a.ctr[C_BUMPED];
         }
-        const uint32_t slot = atomicAdd(s_emit, 1u);
-        if (slot >= d.bcap) {
-            a.overflow = true;
-            continue;
+        const uint32_t dl = dst - d.lo;
+        if (dl < d.L) {
+            const uint32_t slot = atomicAdd(&sh.nloc, 1u);
+            if (slot < d.ECAP) d.loc[(size_t)part * d.ECAP + slot] = Rec{((uint64_t)dl << 40) | (tn - S), key};
+            else a.overflow = true;
+        } else {
+            const uint32_t slot = atomicAdd(&sh.nrem, 1u);
+            if (slot < d.ECAP) {
+                const size_t so = (size_t)part * d.ECAP + slot;
+                d.rem[so] = Slot{tn, key};
+                d.rem_dst[so] = dst;
+                atomicAdd(&sh.peer[owner_of(d, dst)], 1u);
+            } else {
+                a.overflow = true;
+            }
         }
-        const size_t so = (size_t)blockIdx.x * d.bcap + slot;
-        d.st[so] = Slot{tn, key};
-        d.st_dst[so] = dst;
-        if (d.G > 1) atomicAdd(&s_peer[owner_of(d, dst)], 1u);
         a.emin = tn < a.emin ? tn : a.emin;
         ++a.ctr[C_EMIT];
     }
 }
 
-// One lane per host.  MASKED (queue_cap <= 64): the queue is read once with
-// independent 16-B loads, the minimum event before the barrier and the last
-// slot are kept from that scan, further due slots are tracked in a 64-bit
-// mask.  Otherwise every pop rescans the queue.
-template <bool MASKED>
-__global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
-    __shared__ uint32_t s_emit;
-    __shared__ uint32_t s_peer[MAXG];
-    __shared__ uint64_t s_red[BLOCK / 64][NCTR + NMIN];
+// One workgroup per partition of HP hosts.
+__global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const RoundState* rs = d.rs;
     if (rs->done | rs->phase) return;
-    const uint64_t E = rs->E;
-    const uint32_t lh = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t L = d.L;
-    if (threadIdx.x == 0) s_emit = 0;
-    if (threadIdx.x < MAXG) s_peer[threadIdx.x] = 0;
+    __shared__ uint32_t s_n[HPMAX];    // events per host
+    __shared__ uint32_t s_c[HPMAX];    // start offset, then end (scatter cursor)
+    __shared__ uint16_t s_act[HPMAX];  // active hosts, ascending
+    __shared__ ProcShared sh;
+    __shared__ uint64_t s16[16];
+    __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
+    const uint64_t S = rs->S, E = rs->E;
+    const uint32_t p = blockIdx.x, HP = d.HP;
+    const uint32_t tid = threadIdx.x;
+    uint32_t n = d.pcnt[p];
+    n = n < d.CAPP ? n : d.CAPP;
+    for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
+    if (tid == 0) {
+        sh.nloc = 0;
+        sh.nrem = 0;
+    }
+    if (tid < MAXG) sh.peer[tid] = 0;
     __syncthreads();
+    const Rec* part = d.part + (size_t)p * d.CAPP;
+    Rec* part2 = d.part2 + (size_t)p * d.CAPP;
+    for (uint32_t i = tid; i < n; i += K2_T) {
+        const uint32_t hl = (uint32_t)(part[i].a >> 52);
+        if (hl < HP) atomicAdd(&s_n[hl], 1u);
+        else flag(d, OV_BUG);
+    }
+    __syncthreads();
+    // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
+    const uint32_t per = (HP + K2_T - 1) / K2_T;
+    const uint32_t h0 = tid * per;
+    uint64_t mine = 0;
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t h = h0 + j;
+        if (h < HP) {
+            const uint32_t c = s_n[h];
+            mine += ((uint64_t)c << 32) | (c ? 1u : 0u);
+        }
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(mine, s16, &tot);
+    for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t h = h0 + j;
+        if (h < HP) {
+            const uint32_t c = s_n[h];
+            s_c[h] = (uint32_t)(run >> 32);
+            if (c) s_act[(uint32_t)run] = (uint16_t)h;
+            run += ((uint64_t)c << 32) | (c ? 1u : 0u);
+        }
+    }
+    const uint32_t nact = (uint32_t)tot;
+    __syncthreads();
+    if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
+    for (uint32_t i = tid; i < n; i += K2_T) {
+        const Rec r = part[i];
+        const uint32_t hl = (uint32_t)(r.a >> 52);
+        if (hl >= HP) continue;
+        const uint32_t pos = atomicAdd(&s_c[hl], 1u);
+        if (pos < n) part2[pos] = r;
+    }
+    __syncthreads();  // part2 is read back by other lanes of this workgroup
 
     Acc a;
 #pragma unroll
@@ -403,293 +680,220 @@ __global__ __launch_bounds__(BLOCK) void k_process(Dev d) {
     a.jmin = UINT64_MAX;
     a.emin = SIMTIME_MAX;
     a.overflow = false;
-    uint64_t newmin = SIMTIME_MAX;
-
-    if (lh < L) {
-        const uint64_t hm = d.hmin[lh];
-        newmin = hm;
-        if (hm < E) {
-            HostCtx c;
-            c.h = d.lo + lh;
-            c.s = d.hs[lh];
-            c.vh = d.hinfo[c.h].vertex;
-            uint32_t cnt = d.bag_cnt[lh];
-            // k_insert counts deliveries past capacity (flagged as overflow and
-            // reported at the next sync); never read beyond the queue
-            cnt = cnt < d.CAP ? cnt : d.CAP;
-            a.ctr[C_ACTIVE] = 1;
-            Slot* bag = d.bag + (size_t)lh * d.CAP;  // this host's queue, contiguous
-            if (MASKED) {
-                uint64_t due = 0, rest_min = SIMTIME_MAX;
-                Best b{UINT64_MAX, 0, 0};
-                Slot lastslot{0, 0};
-                for (uint32_t base = 0; base < cnt; base += 8) {
-                    Slot s[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) s[i] = bag[base + i];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint32_t j = base + i;
-                        const bool live = j < cnt;
-                        const bool isdue = live & (s[i].t < E);
-                        due |= (uint64_t)isdue << j;
-                        const uint64_t rt = (live & !isdue) ? s[i].t : SIMTIME_MAX;
-                        rest_min = rt < rest_min ? rt : rest_min;
-                        best_take(b, isdue ? s[i].t : UINT64_MAX, s[i].k, j);
-                        const bool is_last = j + 1 == cnt;
-                        lastslot.t = is_last ? s[i].t : lastslot.t;
-                        lastslot.k = is_last ? s[i].k : lastslot.k;
-                    }
-                }
-                // slots after the barrier only move (never leave) while popping
-                newmin = rest_min;
-                bool fresh = true;  // b / lastslot still describe the scanned queue
-                auto append = [&](uint64_t tn, uint64_t key) -> bool {
-                    if (cnt >= d.CAP) return false;
-                    bag[cnt] = Slot{tn, key};
-                    due |= 1ULL << cnt;
-                    ++cnt;
-                    return true;
-                };
-                while (due) {
-                    if (!fresh) {
-                        b = Best{UINT64_MAX, 0, 0};
-                        uint64_t m = due;
-                        while (m) {
-                            const uint32_t j = (uint32_t)__builtin_ctzll(m);
-                            m &= m - 1;
-                            const Slot s = bag[j];
-                            best_take(b, s.t, s.k, j);
-                        }
-                    }
-                    const uint32_t best = b.slot;
-                    const uint64_t bt = b.t, bk = b.k;
-                    // remove `best`: the last slot fills the hole
-                    const uint32_t last = cnt - 1;
-                    due &= ~(1ULL << best);
-                    if (best != last) {
-                        const Slot ls = fresh ? lastslot : bag[last];
-                        bag[best] = ls;
-                        const uint64_t lastbit = (due >> last) & 1ULL;
-                        due &= ~(1ULL << last);
-                        due |= lastbit << best;
-                    }
-                    cnt = last;
-                    fresh = false;
-                    execute_event(d, E, c, a, bt, bk, &s_emit, s_peer, append);
-                }
-            } else {
-                auto append = [&](uint64_t tn, uint64_t key) -> bool {
-                    if (cnt >= d.CAP) return false;
-                    bag[cnt] = Slot{tn, key};
-                    ++cnt;
-                    return true;
-                };
-                for (;;) {
-                    Best b{UINT64_MAX, 0, UINT32_MAX};
-                    uint64_t rest_min = SIMTIME_MAX;
-                    for (uint32_t j = 0; j < cnt; ++j) {
-                        const Slot s = bag[j];
-                        if (s.t < E) {
-                            best_take(b, s.t, s.k, j);
-                        } else if (s.t < rest_min) {
-                            rest_min = s.t;
-                        }
-                    }
-                    if (b.slot == UINT32_MAX) {
-                        newmin = rest_min;
-                        break;
-                    }
-                    --cnt;
-                    if (b.slot != cnt) bag[b.slot] = bag[cnt];
-                    execute_event(d, E, c, a, b.t, b.k, &s_emit, s_peer, append);
-                }
-            }
-            d.bag_cnt[lh] = cnt;
-            d.hs[lh] = c.s;
-            d.hmin[lh] = newmin;
+    Rec* xs = d.extras + ((size_t)p * K2_T + tid) * XCAP;
+    const uint32_t hbase = d.lo + p * HP;
+    for (uint32_t j = tid; j < nact; j += K2_T) {
+        const uint32_t hl = s_act[j];
+        const uint32_t cnt = s_n[hl];
+        Rec* seg = part2 + (s_c[hl] - cnt);
+        HostCtx c;
+        c.h = hbase + hl;
+        const uint32_t lh = c.h - d.lo;
+        if (lh >= d.L) {
+            a.overflow = true;
+            continue;
         }
+        c.s = d.hs[lh];
+        c.vh = d.hinfo[c.h].vertex;
+        ++a.ctr[C_ACTIVE];
+        uint32_t ns = cnt, nx = 0;
+        auto append = [&](uint64_t trel, uint64_t key) -> bool {
+            if (nx >= XCAP) return false;
+            xs[nx++] = Rec{trel, key};
+            return true;
+        };
+        for (;;) {
+            Best b{UINT64_MAX, 0, UINT32_MAX};
+            for (uint32_t i = 0; i < ns; ++i) {
+                const Rec r = seg[i];
+                best_take(b, r.a & M52, r.k, i);
+            }
+            for (uint32_t i = 0; i < nx; ++i) {
+                const Rec r = xs[i];
+                best_take(b, r.a, r.k, 0x80000000u | i);
+            }
+            if (b.slot == UINT32_MAX) break;
+            if (b.slot & 0x80000000u) {
+                const uint32_t i = b.slot & 0x7FFFFFFFu;
+                --nx;
+                if (i != nx) xs[i] = xs[nx];
+            } else {
+                --ns;
+                if (b.slot != ns) seg[b.slot] = seg[ns];
+            }
+            execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
+        }
+        d.hs[lh] = c.s;
     }
 
-    // workgroup partials: cumulative counters and this round's three minima
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t v[NCTR + NMIN];
+    // workgroup partials: cumulative counters, this round's two minima
+    const int lane = tid & 63, wid = tid >> 6;
+    uint64_t v[NCTR + 2];
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum(a.ctr[i]);
-    v[NCTR + M_JMIN] = wave_min(a.jmin);
-    v[NCTR + M_EMIN] = wave_min(a.emin);
-    v[NCTR + M_RMIN] = wave_min(newmin);
+    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum((uint64_t)a.ctr[i]);
+    v[NCTR] = wave_min(a.emin);
+    v[NCTR + 1] = wave_min(a.jmin);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < NCTR + NMIN; ++i) s_red[wid][i] = v[i];
+        for (int i = 0; i < NCTR + 2; ++i) s_red[wid][i] = v[i];
     }
-    if (a.overflow) atomicOr((unsigned long long*)&d.rs->overflow, 1ULL);
+    if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
-    if (threadIdx.x < NCTR + NMIN) {
-        const int i = threadIdx.x;
+    if (tid < NCTR + 2) {
+        const int i = tid;
         uint64_t r = s_red[0][i];
-        for (int w = 1; w < BLOCK / 64; ++w) {
+        for (int w = 1; w < K2_T / 64; ++w) {
             const uint64_t x = s_red[w][i];
             r = i < NCTR ? r + x : (x < r ? x : r);
         }
-        if (i < NCTR) d.pcum[(size_t)i * d.nblocks + blockIdx.x] += r;
-        else d.pmin[(size_t)(i - NCTR) * d.nblocks + blockIdx.x] = r;
+        if (i < NCTR) d.pcum[(size_t)i * d.P + p] += r;
+        else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
     }
-    if (threadIdx.x == 0) d.blockcnt[blockIdx.x] = s_emit < d.bcap ? s_emit : d.bcap;
-    if (d.G > 1 && threadIdx.x < d.G) d.peercnt[(size_t)blockIdx.x * d.G + threadIdx.x] = s_peer[threadIdx.x];
+    if (tid == 0) {
+        if (sh.nloc > d.ECAP || sh.nrem > d.ECAP) flag(d, OV_PROC);
+        d.rcnt[p] = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
+        if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
+    }
+    if (d.G > 1 && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
 }
 
-// Inclusive scan across one workgroup of 1024 (16 waves).
-__device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t* s_w) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
+// --------------------------------------------------------------- insert ----
+// Staged events (process steps) and received exchange blocks (multi-shard)
+// → buckets.  The sources' events are split evenly over the grid; k_count and
+// k_scatter compute the same split.
+
+// Event `idx` of the concatenated sources: t (absolute), key, dst_local.
+__device__ __forceinline__ bool src_event(const Dev& d, const int64_t* recv, const uint32_t* s_off,
+                                          uint32_t nsrc, uint64_t S, uint32_t idx, uint64_t& t,
+                                          uint64_t& k, uint32_t& dl) {
+    uint32_t lo = 0, hi = nsrc - 1;  // last source with s_off <= idx
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= idx) lo = mid; else hi = mid - 1;
     }
-    if (lane == 63) s_w[wid] = v;
-    __syncthreads();
-    uint64_t add = 0;
-    for (int w = 0; w < wid; ++w) add += s_w[w];
-    __syncthreads();
-    return v + add;
+    const uint32_t off = idx - s_off[lo];
+    if (lo < d.P) {
+        const Rec r = d.loc[(size_t)lo * d.ECAP + off];
+        t = S + (r.a & M40);
+        k = r.k;
+        dl = (uint32_t)(r.a >> 40);
+        return dl < d.L;
+    }
+    const int64_t* row = recv + ((size_t)(lo - d.P) * d.xrows + HDR + off) * 3;
+    t = (uint64_t)row[0];
+    k = (uint64_t)row[1];
+    dl = (uint32_t)row[2] - d.lo;
+    return dl < d.L;
 }
 
-// Multi-shard, process steps: per-(block, peer) offsets of the staged events
-// and each peer's outbox region.  One workgroup of 1024.
-__global__ __launch_bounds__(1024) void k_peer_scan(Dev d) {
+// Exclusive offsets of the sources' event counts into s_off; returns the total.
+__device__ uint64_t src_offsets(const Dev& d, const int64_t* recv, bool local, uint32_t nsrc,
+                                uint32_t* s_off, uint64_t* s16, bool check) {
+    uint32_t cs[SRC_PER];
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SRC_PER; ++j) {
+        const uint32_t s = threadIdx.x * SRC_PER + j;
+        uint32_t c = 0;
+        if (s < d.P) {
+            c = local ? d.rcnt[s] : 0;
+        } else if (s < nsrc && s - d.P != d.g) {
+            const uint64_t n = (uint64_t)recv[(size_t)(s - d.P) * d.xrows * 3 + H_N];
+            if (n <= d.xcap) c = (uint32_t)n;
+            else if (check) flag(d, OV_XCHG);
+        }
+        cs[j] = c;
+        mine += c;
+    }
+    uint64_t total;
+    uint64_t run = block_excl_scan(mine, s16, &total);
+#pragma unroll
+    for (uint32_t j = 0; j < SRC_PER; ++j) {
+        const uint32_t s = threadIdx.x * SRC_PER + j;
+        if (s < nsrc) s_off[s] = (uint32_t)run;
+        run += cs[j];
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     RoundState* rs = d.rs;
-    if (rs->done | rs->phase) return;
-    __shared__ uint64_t s_w[16];
-    __shared__ uint64_t s_tot[MAXG];
-    const uint32_t NB = d.nblocks, G = d.G;
-    const uint32_t chunk = (NB + 1023) / 1024;
-    const uint32_t b0 = threadIdx.x * chunk;
-    const uint32_t b1 = b0 + chunk < NB ? b0 + chunk : NB;
-    for (uint32_t p = 0; p < G; ++p) {
-        uint64_t sum = 0;
-        for (uint32_t b = b0; b < b1; ++b) sum += d.peercnt[(size_t)b * G + p];
-        const uint64_t incl = block_incl_scan(sum, s_w);
-        uint64_t run = incl - sum;
-        for (uint32_t b = b0; b < b1; ++b) {
-            const size_t k = (size_t)b * G + p;
-            d.peeroff[k] = (uint32_t)run;
-            run += d.peercnt[k];
-        }
-        if (threadIdx.x == 1023) s_tot[p] = incl;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        uint64_t base = 0, peak = rs->peak_peer;
-        for (uint32_t p = 0; p < G; ++p) {
-            const uint64_t n = p == d.g ? 0 : s_tot[p];
-            d.peer_base[p] = base;
-            d.outn[p] = n;
-            d.sent[p] = 0;
-            base += n;
-            peak = n > peak ? n : peak;
-        }
-        rs->peak_peer = peak;
-    }
-}
-
-// Multi-shard, process steps: staged events owned by other shards → outbox
-// triples {time, key, dst}, grouped by owner.
-__global__ __launch_bounds__(BLOCK) void k_pack(Dev d) {
-    if (d.rs->done | d.rs->phase) return;
-    __shared__ uint32_t s_slot[MAXG];
-    if (threadIdx.x < MAXG) s_slot[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = d.blockcnt[b];
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-        const size_t so = (size_t)b * d.bcap + i;
-        const uint32_t dst = d.st_dst[so];
-        const uint32_t p = owner_of(d, dst);
-        if (p == d.g) continue;
-        const uint64_t slot = d.peer_base[p] + d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
-        const Slot s = d.st[so];
-        int64_t* o = d.outq + slot * 3;
-        o[0] = (int64_t)s.t;
-        o[1] = (int64_t)s.k;
-        o[2] = (int64_t)dst;
-    }
-}
-
-// Every step: up to xcap outbox events per peer into the peer's exchange
-// block, behind the header {n, sender has more, MIN next, min jump, overflow,
-// round}.  Grid (chunks, G).
-__global__ __launch_bounds__(BLOCK) void k_fill(Dev d, int64_t* send) {
-    const RoundState* rs = d.rs;
     if (rs->done) return;
-    const uint32_t p = blockIdx.y;
-    const uint64_t left = d.outn[p] - d.sent[p];
-    const uint64_t n = left < d.xcap ? left : d.xcap;
-    int64_t* blk = send + (size_t)p * d.xrows * 3;
-    const int64_t* src = d.outq + (d.peer_base[p] + d.sent[p]) * 3;
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n * 3;
-         i += (uint64_t)gridDim.x * BLOCK)
-        blk[HDR * 3 + i] = src[i];
+    __shared__ uint32_t s_off[SRCMAX];
+    __shared__ uint32_t s_bc[RMAX];  // per bucket: events of this workgroup
+    __shared__ uint32_t s_bm[RMAX];  // per bucket: min time offset within the bucket
+    __shared__ uint64_t s16[16];
+    const bool local = rs->phase == 0;
+    const uint64_t S = rs->S, W = d.W, bS = rs->bS;
+    const uint32_t R = d.R;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        uint64_t more = 0;
-        for (uint32_t q = 0; q < d.G; ++q) more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
-        blk[H_N] = (int64_t)n;
-        blk[H_MORE] = (int64_t)more;
-        blk[H_MIN] = (int64_t)rs->loc_min;
-        blk[H_JMIN] = (int64_t)rs->loc_jmin;
-        blk[H_OVF] = (int64_t)rs->overflow;
-        blk[H_ROUND] = (int64_t)rs->rounds;
+        rs->ins_local = local;
+        rs->ins_S = S;
     }
-}
-
-__device__ __forceinline__ void deliver(const Dev& d, const Slot s, uint32_t dst) {
-    const uint32_t dl = dst - d.lo;
-    const uint32_t slot = atomicAdd(&d.bag_cnt[dl], 1u);
-    if (slot >= d.CAP) {
-        atomicOr((unsigned long long*)&d.rs->overflow, 4ULL);
-        return;
+    const uint32_t nsrc = d.P + (recv ? d.G : 0);
+    for (uint32_t b = threadIdx.x; b < R; b += K3_T) {
+        s_bc[b] = 0;
+        s_bm[b] = UINT32_MAX;
     }
-    d.bag[(size_t)dl * d.CAP + slot] = s;
-    // the earliest-time word only decreases here: skip the atomic when it is
-    // already at or below this event
-    if (s.t < __hip_atomic_load(&d.hmin[dl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMin((unsigned long long*)&d.hmin[dl], (unsigned long long)s.t);
-}
-
-// Staged events of this shard's own hosts → destination queues.
-__global__ __launch_bounds__(BLOCK) void k_insert(Dev d) {
-    if (d.rs->done | d.rs->phase) return;
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = d.blockcnt[b];
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-        const size_t so = (size_t)b * d.bcap + i;
-        const uint32_t dst = d.st_dst[so];
-        if (dst - d.lo >= d.L) continue;  // another shard's host
-        deliver(d, d.st[so], dst);
-    }
-}
-
-// Received exchange blocks → destination queues.  Grid (chunks, G).
-__global__ __launch_bounds__(BLOCK) void k_insert_recv(Dev d, const int64_t* recv) {
-    if (d.rs->done) return;
-    const uint32_t p = blockIdx.y;
-    if (p == d.g) return;
-    const int64_t* blk = recv + (size_t)p * d.xrows * 3;
-    const uint64_t n = (uint64_t)blk[H_N];
-    if (n > d.xcap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned long long*)&d.rs->overflow, 8ULL);
-        return;
-    }
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const int64_t* r = blk + (HDR + i) * 3;
-        const uint32_t dst = (uint32_t)r[2];
-        if (dst - d.lo >= d.L) {
-            atomicOr((unsigned long long*)&d.rs->overflow, 8ULL);
+    const uint64_t total = src_offsets(d, recv, local, nsrc, s_off, s16, true);
+    const uint64_t lo = total * blockIdx.x / gridDim.x, hi = total * (blockIdx.x + 1) / gridDim.x;
+    for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
+        uint64_t t, k;
+        uint32_t dl;
+        if (!src_event(d, recv, s_off, nsrc, S, (uint32_t)idx, t, k, dl)) {
+            flag(d, OV_XCHG);
             continue;
         }
-        deliver(d, Slot{(uint64_t)r[0], (uint64_t)r[1]}, dst);
+        const uint64_t b = t / W;
+        if (b < bS || b - bS >= R) {
+            flag(d, OV_HORIZON);
+            continue;
+        }
+        const uint32_t rb = (uint32_t)(b % R);
+        atomicAdd(&s_bc[rb], 1u);
+        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
+    }
+    __syncthreads();
+    uint32_t* wb = d.wbase + (size_t)blockIdx.x * R;
+    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) {
+        const uint32_t c = s_bc[rb];
+        if (!c) continue;
+        const uint64_t b = bS + ((rb + R - (uint32_t)(bS % R)) % R);  // absolute bucket of slot rb
+        wb[rb] = atomicAdd(&d.bcnt[rb], c);
+        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
     }
 }
 
+__global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
+    const RoundState* rs = d.rs;
+    if (rs->done) return;
+    __shared__ uint32_t s_off[SRCMAX];
+    __shared__ uint32_t s_cur[RMAX];
+    __shared__ uint64_t s16[16];
+    const bool local = rs->ins_local != 0;
+    const uint64_t S = rs->ins_S, W = d.W;
+    const uint32_t R = d.R, NCH = d.NCH;
+    const uint32_t nsrc = d.P + (recv ? d.G : 0);
+    const uint32_t* wb = d.wbase + (size_t)blockIdx.x * R;
+    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+    const uint64_t total = src_offsets(d, recv, local, nsrc, s_off, s16, false);
+    const uint64_t lo = total * blockIdx.x / gridDim.x, hi = total * (blockIdx.x + 1) / gridDim.x;
+    for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
+        uint64_t t, k;
+        uint32_t dl;
+        if (!src_event(d, recv, s_off, nsrc, S, (uint32_t)idx, t, k, dl)) continue;
+        const uint64_t b = t / W;
+        const uint32_t rb = (uint32_t)(b % R);
+        const uint32_t pos = atomicAdd(&s_cur[rb], 1u);
+        if ((pos >> CH_SHIFT) >= d.nal[rb]) continue;  // beyond the pool (flagged by k_plan)
+        const uint32_t id = d.btab[(size_t)rb * NCH + (pos >> CH_SHIFT)];
+        if (id >= NCH) continue;
+        d.pool[((size_t)id << CH_SHIFT) + (pos & (CH - 1))] = Rec{((uint64_t)dl << 40) | (t - b * W), k};
+    }
+}
+
+// ----------------------------------------------------------------- plan ----
 // master_slaveFinishedCurrentRound (master.c:450-480) on a reduced triple.
 __device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t not_overflow) {
     RoundState* rs = d.rs;
@@ -717,103 +921,345 @@ __device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint
     rs->done = start < end ? 0 : 1;
 }
 
-// Local MIN next time (remaining ∪ staged) and discovery min; with apply != 0
-// (single shard) also the next window.  One workgroup of 1024.
-__global__ __launch_bounds__(1024) void k_reduce(Dev d, uint64_t* out3, int apply) {
-    if (d.rs->done | d.rs->phase) return;
-    __shared__ uint64_t s_v[16][NMIN];
-    uint64_t v[NMIN];
-#pragma unroll
-    for (int i = 0; i < NMIN; ++i) v[i] = UINT64_MAX;
-    const size_t NB = d.nblocks;
-    for (uint32_t b = threadIdx.x; b < NB; b += 1024) {
-#pragma unroll
-        for (int i = 0; i < NMIN; ++i) {
-            const uint64_t x = d.pmin[(size_t)i * NB + b];
-            v[i] = x < v[i] ? x : v[i];
-        }
+__device__ __forceinline__ void reset_bucket(const Dev& d, uint32_t rb) {
+    d.nal[rb] = 0;
+    d.bcnt[rb] = 0;
+    d.btomb[rb] = 0;
+    d.bmin[rb] = UINT64_MAX;
+}
+
+// The local MIN terms of a round: carry min (k_gather), emitted min and
+// discovery min (k_proc), and the buckets beyond the window (rmin).
+__device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
+    uint64_t mm = UINT64_MAX, jj = UINT64_MAX;
+    for (uint32_t i = threadIdx.x; i < d.G1; i += blockDim.x) mm = d.c1min[i] < mm ? d.c1min[i] : mm;
+    for (uint32_t i = threadIdx.x; i < d.P; i += blockDim.x) {
+        const uint64_t x = d.p2min[i], y = d.p2min[d.P + i];
+        mm = x < mm ? x : mm;
+        jj = y < jj ? y : jj;
     }
+    m = block_min(mm, s16);
+    j = block_min(jj, s16);
+    const RoundState* rs = d.rs;
+    m = rs->rmin < m ? rs->rmin : m;
+    m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+    j = rs->jmin < j ? rs->jmin : j;
+}
+
+// Give every bucket the chunks its count needs (after k_count), from the free
+// ring; chunk ids go to the bucket's table for k_scatter and the next listing.
+__device__ void plan_alloc(const Dev& d, uint64_t* s16, uint64_t& s_head, uint64_t s_tail) {
+    const uint32_t R = d.R, NCH = d.NCH;
+    constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
+    uint32_t need[PER];
+    uint64_t mine = 0;
 #pragma unroll
-    for (int i = 0; i < NMIN; ++i) v[i] = wave_min(v[i]);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t rb = threadIdx.x * PER + j;
+        need[j] = 0;
+        if (rb < R) {
+            const uint64_t want = ((uint64_t)d.bcnt[rb] + CH - 1) >> CH_SHIFT;
+            const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
+            const uint32_t have = d.nal[rb];
+            need[j] = w > have ? w - have : 0;
+        }
+        mine += need[j];
+    }
+    uint64_t total;
+    uint64_t off = block_excl_scan(mine, s16, &total);
+    const uint64_t head = s_head;
+    const uint64_t avail = s_tail - head;
+    if (total > avail && threadIdx.x == 0) flag(d, OV_POOL);
 #pragma unroll
-        for (int i = 0; i < NMIN; ++i) s_v[wid][i] = v[i];
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t rb = threadIdx.x * PER + j;
+        if (rb >= R || !need[j]) continue;
+        uint32_t have = d.nal[rb];
+        uint32_t* tab = d.btab + (size_t)rb * NCH;
+        uint32_t k = 0;
+        for (; k < need[j] && off + k < avail; ++k) tab[have + k] = d.fring[(head + off + k) % NCH];
+        d.nal[rb] = have + k;
+        off += need[j];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t r[NMIN];
-        for (int i = 0; i < NMIN; ++i) {
-            r[i] = s_v[0][i];
-            for (int w = 1; w < 16; ++w) r[i] = s_v[w][i] < r[i] ? s_v[w][i] : r[i];
+    if (threadIdx.x == 0) s_head = head + (total < avail ? total : avail);
+    __syncthreads();
+}
+
+// mode 0: single shard, end of round.  mode 1: multi-shard, window from the
+// received headers (or the end of a drain step).  mode 2: boot (list the
+// first window).  Values one thread computes for the others go through LDS.
+__global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int mode) {
+    RoundState* rs = d.rs;
+    if (rs->done) return;
+    __shared__ uint64_t s16[16];
+    __shared__ uint32_t s_nfree;
+    __shared__ uint64_t s_head, s_tail, s_S, s_E, s_done, s_more, s_spent, s_m, s_j, s_ovf;
+    const uint32_t R = d.R, NCH = d.NCH;
+    const uint64_t W = d.W;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        s_head = rs->fl_head;
+        s_tail = rs->fl_tail;
+        s_S = rs->S;
+        s_E = rs->E;
+        s_done = 0;
+        s_more = 0;
+        s_spent = UINT64_MAX;
+        s_nfree = 0;
+        if (mode == 1) {
+            uint64_t more = 0, m = UINT64_MAX, j = UINT64_MAX, ovf = 0;
+            for (uint32_t p = 0; p < d.G; ++p) {
+                const int64_t* blk = recv + (size_t)p * d.xrows * 3;
+                more |= (uint64_t)blk[H_MORE];
+                const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
+                m = bm < m ? bm : m;
+                j = bj < j ? bj : j;
+                ovf |= (uint64_t)blk[H_OVF];
+                if ((uint64_t)blk[H_ROUND] != rs->rounds) ovf |= OV_STEP;  // shards out of step
+            }
+            for (uint32_t q = 0; q < d.G; ++q) {
+                const uint64_t left = d.outn[q] - d.sent[q];
+                d.sent[q] += left < d.xcap ? left : d.xcap;
+            }
+            rs->steps += 1;
+            s_more = more;
+            s_m = m;
+            s_j = j;
+            s_ovf = ovf;
         }
-        RoundState* rs = d.rs;
-        const uint64_t j = rs->jmin < r[M_JMIN] ? rs->jmin : r[M_JMIN];
-        rs->jmin = j;
-        const uint64_t m = r[M_EMIN] < r[M_RMIN] ? r[M_EMIN] : r[M_RMIN];
-        rs->loc_min = m;
-        rs->loc_jmin = j;
-        if (out3) {
-            out3[0] = m;
-            out3[1] = j;
-            out3[2] = ~rs->overflow;
+    }
+    __syncthreads();
+    const bool round_done = mode == 0 || (mode == 1 && !s_more);
+    uint64_t m = 0, j = 0, ovf = 0;
+    if (mode == 0) {
+        reduce_local(d, s16, m, j);
+        ovf = rs->overflow;
+    } else if (mode == 1) {
+        m = s_m;
+        j = s_j;
+        ovf = s_ovf;
+    }
+    if (round_done) {
+        // free the chunks of the window just executed (not the retained
+        // bucket's) and reset its fully consumed buckets
+        const uint64_t nd = rs->ndue, tail = s_tail, ndb = rs->ndueb;
+        for (uint64_t i = tid; i < nd; i += PL_T) {
+            const DueEnt de = d.due[i];
+            if ((de.nflags & RETAINED) || de.id >= NCH) continue;
+            d.fring[(tail + atomicAdd(&s_nfree, 1u)) % NCH] = de.id;
         }
-        if (apply) apply_window(d, m, j, ~rs->overflow);
+        for (uint64_t i = 0; i < ndb; ++i) {
+            const uint32_t rb = d.dueb[i];
+            const uint32_t nc = d.nal[rb];
+            for (uint32_t ci = tid; ci < nc; ci += PL_T) d.btab[(size_t)rb * NCH + ci] = EMPTY;
+        }
+        __syncthreads();
+        for (uint64_t i = tid; i < ndb; i += PL_T) reset_bucket(d, d.dueb[i]);
+        __syncthreads();
+        if (tid == 0) {
+            s_tail = tail + s_nfree;
+            s_nfree = 0;
+        }
+        __syncthreads();
+    }
+    if (mode != 2) plan_alloc(d, s16, s_head, s_tail);
+    if (mode == 1 && s_more) {  // drain step: same window, more exchange
+        if (tid == 0) {
+            rs->phase = 1;
+            rs->overflow |= ovf;
+            rs->fl_head = s_head;
+            rs->fl_tail = s_tail;
+        }
+        return;
+    }
+    if (round_done) {
+        if (tid == 0) {
+            rs->phase = 0;
+            rs->jmin = j;
+            apply_window(d, m, j, ~ovf);
+            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
+            s_S = rs->S;
+            s_E = rs->E;
+            s_done = rs->done;
+            if (s_done) {
+                rs->fl_head = s_head;
+                rs->fl_tail = s_tail;
+            }
+        }
+        __syncthreads();
+        if (s_done) return;
+    }
+    // list the due chunks of the new window [S, E)
+    const uint64_t S = s_S, E = s_E;
+    const uint64_t bS = S / W, bL = (E - 1) / W;
+    const uint64_t pr = rs->ret_b;
+    if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
+        const uint32_t rb = (uint32_t)(pr % R);
+        const uint32_t nc = d.nal[rb];
+        const uint64_t tail = s_tail;
+        for (uint32_t ci = tid; ci < nc; ci += PL_T) {
+            uint32_t* e = &d.btab[(size_t)rb * NCH + ci];
+            d.fring[(tail + ci) % NCH] = *e;
+            *e = EMPTY;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            s_tail = tail + nc;
+            s_spent = rb;
+            reset_bucket(d, rb);
+        }
+        __syncthreads();
+    }
+    // Fully due buckets keep their tables until the next plan (k_scatter of
+    // this round still writes the events k_count counted into them).
+    uint64_t nd = 0, ndb = 0;
+    const bool straddle = E < (bL + 1) * W;
+    for (uint64_t b = bS; b <= bL; ++b) {
+        const uint32_t rb = (uint32_t)(b % R);
+        const uint32_t c = d.bcnt[rb], nc = d.nal[rb];
+        const bool ret = straddle && b == bL;
+        const uint32_t* tab = d.btab + (size_t)rb * NCH;
+        for (uint32_t ci = tid; ci < nc; ci += PL_T) {
+            const uint32_t left = c - (ci << CH_SHIFT);
+            const uint32_t n = left < CH ? left : CH;
+            d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
+        }
+        nd += nc;
+        if (tid == 0) {
+            if (ret) d.bmin[rb] = UINT64_MAX;  // k_gather's carry min and k_count restore it
+            else if (c) d.dueb[ndb] = rb;
+        }
+        if (!ret && c) ++ndb;
+    }
+    // exact min beyond the window: the first non-empty bucket in (bL, bS + R)
+    // (the window's own slots lie outside that range; the spent slot is empty)
+    uint64_t first = UINT64_MAX;
+    const uint32_t span = (uint32_t)(bL - bS);
+    for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
+        const uint64_t b = bL + o;
+        const uint32_t rb = (uint32_t)(b % R);
+        if (rb == s_spent) continue;
+        if (d.bcnt[rb] > d.btomb[rb]) first = b < first ? b : first;
+    }
+    first = block_min(first, s16);
+    if (tid == 0) {
+        rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : d.bmin[first % R];
+        rs->bS = bS;
+        rs->bL = bL;
+        rs->ndue = nd;
+        rs->ndueb = ndb;
+        rs->ret_b = straddle ? bL : UINT64_MAX;
+        rs->fl_head = s_head;
+        rs->fl_tail = s_tail;
     }
 }
 
-// Multi-shard step end: the window from the G received headers (every shard
-// sees the same headers, so every shard takes the same decision).  A sender
-// with outbox leftovers makes the next step a drain step: same window, no
-// processing, more exchange.
-__global__ void k_window(Dev d, const int64_t* recv) {
+// --------------------------------------------------------- multi-shard ----
+// After k_proc on a process step: this shard's MIN terms (for the header) and
+// the per-(partition, peer) outbox offsets.
+__global__ __launch_bounds__(PL_T) void k_locmin(Dev d) {
     RoundState* rs = d.rs;
+    if (rs->done | rs->phase) return;
+    __shared__ uint64_t s16[16];
+    __shared__ uint64_t s_tot[MAXG];
+    uint64_t m, j;
+    reduce_local(d, s16, m, j);
+    const uint32_t P = d.P, G = d.G;
+    const uint32_t chunk = (P + PL_T - 1) / PL_T;
+    const uint32_t b0 = threadIdx.x * chunk;
+    const uint32_t b1 = b0 + chunk < P ? b0 + chunk : P;
+    for (uint32_t p = 0; p < G; ++p) {
+        uint64_t sum = 0;
+        for (uint32_t b = b0; b < b1; ++b) sum += d.peercnt[(size_t)b * G + p];
+        uint64_t tot;
+        uint64_t run = block_excl_scan(sum, s16, &tot);
+        for (uint32_t b = b0; b < b1; ++b) {
+            const size_t k = (size_t)b * G + p;
+            d.peeroff[k] = (uint32_t)run;
+            run += d.peercnt[k];
+        }
+        if (threadIdx.x == 0) s_tot[p] = tot;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        rs->loc_min = m;
+        rs->loc_jmin = j;
+        uint64_t base = 0, peak = rs->peak_peer;
+        for (uint32_t p = 0; p < G; ++p) {
+            const uint64_t n = p == d.g ? 0 : s_tot[p];
+            d.peer_base[p] = base;
+            d.outn[p] = n;
+            d.sent[p] = 0;
+            base += n;
+            peak = n > peak ? n : peak;
+        }
+        rs->peak_peer = peak;
+    }
+}
+
+// Multi-shard, process steps: staged events owned by other shards → outbox
+// triples {time, key, dst}, grouped by owner.  One workgroup per partition.
+__global__ __launch_bounds__(256) void k_pack(Dev d) {
+    if (d.rs->done | d.rs->phase) return;
+    __shared__ uint32_t s_slot[MAXG];
+    if (threadIdx.x < MAXG) s_slot[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    const uint32_t n = d.remn[b];
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const size_t so = (size_t)b * d.ECAP + i;
+        const uint32_t dst = d.rem_dst[so];
+        const uint32_t p = owner_of(d, dst);
+        const uint64_t slot = d.peer_base[p] + d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
+        const Slot s = d.rem[so];
+        int64_t* o = d.outq + slot * 3;
+        o[0] = (int64_t)s.t;
+        o[1] = (int64_t)s.k;
+        o[2] = (int64_t)dst;
+    }
+}
+
+// Every step: up to xcap outbox events per peer into the peer's exchange
+// block, behind the header {n, sender has more, MIN next, min jump, overflow,
+// round}.  Grid (chunks, G).
+__global__ __launch_bounds__(256) void k_fill(Dev d, int64_t* send) {
+    const RoundState* rs = d.rs;
     if (rs->done) return;
-    uint64_t m = UINT64_MAX, j = UINT64_MAX, ovf = 0, more = 0;
-    for (uint32_t p = 0; p < d.G; ++p) {
-        const int64_t* blk = recv + (size_t)p * d.xrows * 3;
-        more |= (uint64_t)blk[H_MORE];
-        const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
-        m = bm < m ? bm : m;
-        j = bj < j ? bj : j;
-        ovf |= (uint64_t)blk[H_OVF];
-        if ((uint64_t)blk[H_ROUND] != rs->rounds) ovf |= 16;  // shards out of step
+    const uint32_t p = blockIdx.y;
+    const uint64_t left = d.outn[p] - d.sent[p];
+    const uint64_t n = left < d.xcap ? left : d.xcap;
+    int64_t* blk = send + (size_t)p * d.xrows * 3;
+    const int64_t* src = d.outq + (d.peer_base[p] + d.sent[p]) * 3;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n * 3; i += (uint64_t)gridDim.x * 256)
+        blk[HDR * 3 + i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint64_t more = 0;
+        for (uint32_t q = 0; q < d.G; ++q) more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
+        blk[H_N] = (int64_t)n;
+        blk[H_MORE] = (int64_t)more;
+        blk[H_MIN] = (int64_t)rs->loc_min;
+        blk[H_JMIN] = (int64_t)rs->loc_jmin;
+        blk[H_OVF] = (int64_t)rs->overflow;
+        blk[H_ROUND] = (int64_t)rs->rounds;
     }
-    for (uint32_t q = 0; q < d.G; ++q) {
-        const uint64_t left = d.outn[q] - d.sent[q];
-        d.sent[q] += left < d.xcap ? left : d.xcap;
-    }
-    rs->steps += 1;
-    if (more) {
-        rs->phase = 1;
-        rs->overflow |= ovf;
-        return;
-    }
-    rs->phase = 0;
-    apply_window(d, m, j, ~ovf);
 }
 
 // Cumulative counters (stats on demand) and pending events.
 __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pending) {
-    __shared__ uint64_t s_c[16][NCTR + 1];
-    uint64_t c[NCTR + 1];
-    for (int i = 0; i <= NCTR; ++i) c[i] = 0;
-    for (uint32_t b = threadIdx.x; b < d.nblocks; b += 1024)
-        for (int i = 0; i < NCTR; ++i) c[i] += d.pcum[(size_t)i * d.nblocks + b];
-    for (uint32_t h = threadIdx.x; h < d.L; h += 1024) {
-        const uint32_t n = d.bag_cnt[h];
-        c[NCTR] += n < d.CAP ? n : d.CAP;
+    __shared__ uint64_t s16[16];
+    uint64_t c[NCTR];
+    for (int i = 0; i < NCTR; ++i) c[i] = 0;
+    for (uint32_t b = threadIdx.x; b < d.P; b += 1024)
+        for (int i = 0; i < NCTR; ++i) c[i] += d.pcum[(size_t)i * d.P + b];
+    uint64_t pend = 0;
+    for (uint32_t rb = threadIdx.x; rb < d.R; rb += 1024) pend += d.bcnt[rb] - d.btomb[rb];
+    for (int i = 0; i < NCTR; ++i) {
+        const uint64_t t = block_sum(c[i], s16);
+        if (threadIdx.x == 0) d.rs->ctr[i] = t;
     }
-    for (int i = 0; i <= NCTR; ++i) c[i] = wave_sum(c[i]);
-    if ((threadIdx.x & 63) == 0)
-        for (int i = 0; i <= NCTR; ++i) s_c[threadIdx.x >> 6][i] = c[i];
-    __syncthreads();
-    if (threadIdx.x <= NCTR) {
-        uint64_t t = 0;
-        for (int w = 0; w < 16; ++w) t += s_c[w][threadIdx.x];
-        if (threadIdx.x < NCTR) d.rs->ctr[threadIdx.x] = t;
-        else *pending = t;
-    }
+    pend = block_sum(pend, s16);
+    if (threadIdx.x == 0) *pending = pend;
 }
 
 }  // namespace
@@ -830,12 +1276,14 @@ struct sg_engine {
     bool booted;
     std::vector<void*> allocs;
     RoundState* h_rs;  // pinned
+    unsigned long long* d_pend;
     bool timing;
+    bool debug_sync;  // SG_DEBUG_SYNC=1: synchronise after every launch, name the faulting class
     struct Pair { hipEvent_t a, b; int cls; };
     std::vector<Pair> pending_ev;
     std::vector<hipEvent_t> free_ev;
-    double ms[3];
-    uint64_t launches[3];
+    double ms[SG_KCLASSES];
+    uint64_t launches[SG_KCLASSES];
 };
 
 #define HIPCHK(x)                                                                      \
@@ -883,6 +1331,15 @@ static int timed_launch(sg_engine* e, int cls, F&& launch) {
     }
     launch();
     HIPCHK(hipGetLastError());
+    if (e->debug_sync) {
+        const hipError_t err = hipStreamSynchronize(e->stream);
+        if (err != hipSuccess) {
+            static const char* names[SG_KCLASSES] = {"process", "insert", "plan", "gather"};
+            sg_set_error("kernel class %s (launch %llu) failed: %s", names[cls],
+                         (unsigned long long)e->launches[cls], hipGetErrorString(err));
+            return SG_ERR_HIP;
+        }
+    }
     if (e->timing && a && b) {
         HIPCHK(hipEventRecord(b, e->stream));
         e->pending_ev.push_back({a, b, cls});
@@ -899,6 +1356,19 @@ static void harvest_timing(sg_engine* e) {
         e->free_ev.push_back(pr.b);
     }
     e->pending_ev.clear();
+}
+
+static uint32_t next_pow2(uint64_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* s = getenv(name);
+    if (!s || !*s) return dflt;
+    const long v = strtol(s, nullptr, 10);
+    return v > 0 ? (uint32_t)v : dflt;
 }
 
 extern "C" {
@@ -932,15 +1402,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     HIPCHK(hipSetDevice(device));
 
-    sg_engine* e = new sg_engine();
-    e->p = p;
-    e->device = device;
-    e->timing = false;
-    for (int i = 0; i < 3; ++i) {
-        e->ms[i] = 0;
-        e->launches[i] = 0;
-    }
-    Dev& d = e->d;
+    Dev d;
     memset(&d, 0, sizeof d);
     d.N = p.n_hosts;
     d.V = p.n_vertices;
@@ -949,9 +1411,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     for (uint32_t i = 0; i <= G; ++i) d.bounds[i] = (uint32_t)(((uint64_t)i * p.n_hosts) / G);
     d.lo = d.bounds[d.g];
     d.L = d.bounds[d.g + 1] - d.lo;
-    d.CAP = p.queue_cap ? p.queue_cap : 64;
-    if (d.CAP < p.load) d.CAP = p.load;  // a boot event may queue `load` self events
-    d.CAP = (d.CAP + 7u) & ~7u;           // the masked scan reads slots in groups of 8
+    if (d.L == 0) {
+        sg_set_error("sg_engine_create: shard has no hosts");
+        return SG_ERR_INVAL;
+    }
     d.load = p.load;
     d.dst_rule = p.dst_rule;
     d.window_rule = p.window_rule;
@@ -962,18 +1425,76 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.trace_cap = p.trace_capacity;
     d.xcap = p.exchange_cap ? p.exchange_cap : 4096;
     d.xrows = HDR + d.xcap;
-    d.nblocks = (d.L + BLOCK - 1) / BLOCK;
-    const uint32_t per_host = d.CAP > d.load ? d.CAP : d.load;
-    d.bcap = BLOCK * per_host;
-    if (d.L == 0) {
-        delete e;
-        sg_set_error("sg_engine_create: shard has no hosts");
+
+    // Calendar geometry: bucket width W = the narrowest window the rules allow
+    // after the first, ring R covering the widest window plus the longest delay.
+    const size_t VV = (size_t)d.V * d.V;
+    uint64_t max_delay = 0, max_jump_ms = 0;
+    for (size_t i = 0; i < VV; ++i) {
+        max_delay = std::max<uint64_t>(max_delay, t->delay_ns[i]);
+        max_jump_ms = std::max<uint64_t>(max_jump_ms, t->jump_ms[i]);
+    }
+    uint64_t W, max_jump;
+    if (p.window_rule == SG_WINDOW_FIXED) {
+        W = std::max<uint64_t>(p.fixed_jump, 1);
+        max_jump = p.fixed_jump;
+    } else {
+        W = std::max<uint64_t>(p.runahead_min, SG_ONE_MS);
+        max_jump = std::max<uint64_t>(std::max<uint64_t>(10 * SG_ONE_MS, p.runahead_min),
+                                      max_jump_ms * SG_ONE_MS);
+    }
+    const uint64_t span = max_jump + max_delay + 2;
+    if (span >= (1ULL << 39)) {
+        sg_set_error("sg_engine_create: window + delay span %llu ns exceeds 2^39 ns",
+                     (unsigned long long)span);
         return SG_ERR_INVAL;
     }
+    if (span / W + 3 > RMAX) W = (span + RMAX - 4) / (RMAX - 3);
+    if (W >= (1ULL << 32)) {
+        sg_set_error("sg_engine_create: bucket width %llu ns too large", (unsigned long long)W);
+        return SG_ERR_INVAL;
+    }
+    d.W = W;
+    d.R = (uint32_t)(span / W + 3);
+    d.G3 = env_u32("SG_INS_GRID", 128);
+    const uint64_t qc = p.queue_cap ? p.queue_cap : 64;
+    const uint64_t base_ch = ((uint64_t)d.L * qc + CH - 1) / CH;
+    // every live bucket may hold one partly filled chunk
+    const uint64_t nch = base_ch + d.R + 64;
+    if (nch >= (1ULL << 31) || (uint64_t)d.R * nch > (3ULL << 30)) {
+        sg_set_error("sg_engine_create: calendar too large (R=%u chunks=%llu); lower queue_cap",
+                     d.R, (unsigned long long)nch);
+        return SG_ERR_INVAL;
+    }
+    d.NCH = (uint32_t)nch;
+    d.G1 = env_u32("SG_GATHER_GRID", 128);
+    // host partitions: HP hosts per k_proc workgroup (power of two)
+    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, next_pow2((d.L + 255) / 256)));
+    d.hp_shift = 0;
+    while ((1u << d.hp_shift) < d.HP) ++d.hp_shift;
+    d.P = (d.L + d.HP - 1) / d.HP;
+    if (d.P > PMAX) {
+        sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
+        return SG_ERR_INVAL;
+    }
+    const uint32_t per_host = std::max<uint32_t>(32, 2 * d.load);
+    d.CAPP = d.HP * per_host;
+    d.ECAP = d.HP * per_host + 1024;
+
+    sg_engine* e = new sg_engine();
+    e->p = p;
+    e->device = device;
+    e->timing = false;
+    e->debug_sync = env_u32("SG_DEBUG_SYNC", 0) != 0;
+    for (int i = 0; i < SG_KCLASSES; ++i) {
+        e->ms[i] = 0;
+        e->launches[i] = 0;
+    }
+    e->d = d;
+    Dev& D = e->d;
 
     int rc = SG_OK;
-    const size_t N = d.N, VV = (size_t)d.V * d.V, L = d.L, S = (size_t)d.CAP * L;
-    const size_t NB = d.nblocks, ST = (size_t)NB * d.bcap;
+    const size_t N = D.N, L = D.L, P = D.P;
 #define ALLOC(ptr, n)                                  \
     do {                                               \
         if ((rc = dalloc(e, &(ptr), (n))) != SG_OK) {  \
@@ -985,30 +1506,44 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     PairRec* pairs;
     ALLOC(hinfo, N);
     ALLOC(pairs, VV);
-    d.hinfo = hinfo;
-    d.pairs = pairs;
-    ALLOC(d.bag, S);
-    ALLOC(d.bag_cnt, L);
-    ALLOC(d.hmin, L);
-    ALLOC(d.hs, L);
-    ALLOC(d.pmin, NB * NMIN);
-    ALLOC(d.pcum, NB * NCTR);
-    ALLOC(d.blockcnt, NB);
-    ALLOC(d.peercnt, NB * G);
-    ALLOC(d.peeroff, NB * G);
+    D.hinfo = hinfo;
+    D.pairs = pairs;
+    ALLOC(D.hs, L);
+    ALLOC(D.pool, (size_t)D.NCH * CH);
+    ALLOC(D.btab, (size_t)D.R * D.NCH);
+    ALLOC(D.bcnt, D.R);
+    ALLOC(D.btomb, D.R);
+    ALLOC(D.bmin, D.R);
+    ALLOC(D.fring, D.NCH);
+    ALLOC(D.nal, D.R);
+    ALLOC(D.wbase, (size_t)D.G3 * D.R);
+    ALLOC(D.due, D.NCH);
+    ALLOC(D.dueb, D.R);
+    ALLOC(D.pcnt, P);
+    ALLOC(D.part, P * D.CAPP);
+    ALLOC(D.part2, P * D.CAPP);
+    ALLOC(D.extras, P * K2_T * XCAP);
+    ALLOC(D.rcnt, P);
+    ALLOC(D.loc, P * D.ECAP);
+    ALLOC(D.c1min, D.G1);
+    ALLOC(D.p2min, 2 * P);
+    ALLOC(D.pcum, NCTR * P);
     if (G > 1) {
-        ALLOC(d.outq, ST * 3);
-        ALLOC(d.peer_base, G);
-        ALLOC(d.outn, G);
-        ALLOC(d.sent, G);
+        ALLOC(D.remn, P);
+        ALLOC(D.rem, P * D.ECAP);
+        ALLOC(D.rem_dst, P * D.ECAP);
+        ALLOC(D.peercnt, P * G);
+        ALLOC(D.peeroff, P * G);
+        ALLOC(D.outq, P * D.ECAP * 3);
+        ALLOC(D.peer_base, G);
+        ALLOC(D.outn, G);
+        ALLOC(D.sent, G);
     }
-    ALLOC(d.st, ST);
-    ALLOC(d.st_dst, ST);
-    ALLOC(d.rs, 1);
-    ALLOC(d.red3, 4);
-    if (d.trace_cap) ALLOC(d.trace, d.trace_cap);
-    d.wlog_cap = d.trace_cap ? 1u << 20 : 0;
-    if (d.wlog_cap) ALLOC(d.wlog, 2 * d.wlog_cap);
+    ALLOC(D.rs, 1);
+    ALLOC(e->d_pend, 1);
+    if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
+    D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
+    if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
 
     if (hip_stream) {
@@ -1033,22 +1568,22 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     for (size_t i = 0; i < N; ++i) {
         hi[i].vertex = t->host_vertex[i];
         hi[i].wt = t->weight_thresh ? t->weight_thresh[i] : 0;
-        if (hi[i].vertex >= d.V) {
+        if (hi[i].vertex >= D.V) {
             sg_engine_destroy(e);
-            sg_set_error("sg_engine_create: host %zu attached to vertex %u >= %u", i, hi[i].vertex, d.V);
+            sg_set_error("sg_engine_create: host %zu attached to vertex %u >= %u", i, hi[i].vertex, D.V);
             return SG_ERR_INVAL;
         }
     }
     std::vector<PairRec> pr(VV);
     for (size_t i = 0; i < VV; ++i) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
     std::vector<HostState> hs(L);
-    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[d.lo + i], 0, 0, 0, 0};
+    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(d.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemset(d.rs, 0, sizeof(RoundState));
-    err = err != hipSuccess ? err : hipMemset(d.pcum, 0, NB * NCTR * 8);
+    err = err != hipSuccess ? err : hipMemcpy(D.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemset(D.rs, 0, sizeof(RoundState));
+    err = err != hipSuccess ? err : hipMemset(D.pcum, 0, NCTR * P * 8);
     if (err != hipSuccess) {
         sg_set_error("table upload failed: %s", hipGetErrorString(err));
         sg_engine_destroy(e);
@@ -1083,6 +1618,20 @@ int sg_engine_host_range(sg_engine* e, uint32_t* first_host, uint32_t* n_local) 
     return SG_OK;
 }
 
+int sg_engine_geometry(sg_engine* e, sg_engine_geom* out) {
+    if (!e || !out) return SG_ERR_INVAL;
+    const Dev& d = e->d;
+    out->bucket_width = d.W;
+    out->ring_buckets = d.R;
+    out->chunk_events = CH;
+    out->chunks = d.NCH;
+    out->partition_hosts = d.HP;
+    out->partitions = d.P;
+    out->partition_cap = d.CAPP;
+    out->stage_cap = d.ECAP;
+    return SG_OK;
+}
+
 int sg_engine_boot(sg_engine* e) {
     if (!e) return SG_ERR_INVAL;
     if (e->booted) {
@@ -1090,8 +1639,12 @@ int sg_engine_boot(sg_engine* e) {
         return SG_ERR_STATE;
     }
     HIPCHK(hipSetDevice(e->device));
-    Dev d = e->d;
-    hipLaunchKernelGGL(k_boot, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+    const Dev& d = e->d;
+    HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)d.R * d.NCH * sizeof(uint32_t), e->stream));
+    const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P));
+    hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, (const int64_t*)nullptr, 2);
     HIPCHK(hipGetLastError());
     e->booted = true;
     return SG_OK;
@@ -1099,18 +1652,29 @@ int sg_engine_boot(sg_engine* e) {
 
 static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
-    return timed_launch(e, 0, [&] {
-        if (d.CAP <= 64)
-            hipLaunchKernelGGL(k_process<true>, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
-        else
-            hipLaunchKernelGGL(k_process<false>, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+    int rc = timed_launch(e, SG_K_GATHER, [&] {
+        hipLaunchKernelGGL(k_gather, dim3(d.G1), dim3(K1_T), 0, e->stream, d);
+    });
+    if (rc) return rc;
+    return timed_launch(e, SG_K_PROCESS, [&] {
+        hipLaunchKernelGGL(k_proc, dim3(d.P), dim3(K2_T), 0, e->stream, d);
     });
 }
 
-static int enqueue_local_insert(sg_engine* e) {
+// k_count → k_plan (mode) → k_scatter: the new (and received) events into the
+// calendar, the window and the next round's due list.
+static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
     const Dev& d = e->d;
-    return timed_launch(e, 1, [&] {
-        hipLaunchKernelGGL(k_insert, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
+    int rc = timed_launch(e, SG_K_INSERT, [&] {
+        hipLaunchKernelGGL(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, d, recv);
+    });
+    if (rc) return rc;
+    rc = timed_launch(e, SG_K_PLAN, [&] {
+        hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, recv, mode);
+    });
+    if (rc) return rc;
+    return timed_launch(e, SG_K_INSERT, [&] {
+        hipLaunchKernelGGL(k_scatter, dim3(d.G3), dim3(K3_T), 0, e->stream, d, recv);
     });
 }
 
@@ -1125,11 +1689,7 @@ int sg_engine_enqueue_round(sg_engine* e) {
     }
     int rc;
     if ((rc = enqueue_process(e))) return rc;
-    if ((rc = enqueue_local_insert(e))) return rc;
-    const Dev& d = e->d;
-    return timed_launch(e, 2, [&] {
-        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, d, d.red3, 1);
-    });
+    return enqueue_insert_plan(e, nullptr, 0);
 }
 
 int sg_engine_sync(sg_engine* e) {
@@ -1161,7 +1721,7 @@ int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch) {
         done_rounds += n;
         if ((rc = read_rs(e))) return rc;
         if (e->h_rs->overflow) {
-            sg_set_error("sg_engine_run: device queue overflow (flags 0x%llx); raise queue_cap",
+            sg_set_error("sg_engine_run: device capacity overflow (flags 0x%llx); raise queue_cap",
                          (unsigned long long)e->h_rs->overflow);
             return SG_ERR_OVERFLOW;
         }
@@ -1171,11 +1731,10 @@ int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch) {
 
 int sg_engine_stats(sg_engine* e, sg_round_stats* out) {
     if (!e || !out) return SG_ERR_INVAL;
-    unsigned long long* dp = (unsigned long long*)e->d.red3 + 3;
-    hipLaunchKernelGGL(k_stats, dim3(1), dim3(1024), 0, e->stream, e->d, dp);
+    hipLaunchKernelGGL(k_stats, dim3(1), dim3(1024), 0, e->stream, e->d, e->d_pend);
     HIPCHK(hipGetLastError());
     uint64_t pend = 0;
-    HIPCHK(hipMemcpyAsync(&pend, dp, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&pend, e->d_pend, 8, hipMemcpyDeviceToHost, e->stream));
     int rc = read_rs(e);
     if (rc) return rc;
     const RoundState& r = *e->h_rs;
@@ -1270,7 +1829,7 @@ static int need_sharded(sg_engine* e, const char* fn) {
 }
 
 static uint32_t fill_chunks(const Dev& d) {
-    uint64_t c = (d.xcap * 3 + BLOCK * 4 - 1) / (BLOCK * 4);
+    uint64_t c = (d.xcap * 3 + 256 * 4 - 1) / (256 * 4);
     return (uint32_t)(c < 1 ? 1 : c > 256 ? 256 : c);
 }
 
@@ -1308,11 +1867,10 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
     }
     if ((rc = enqueue_process(e))) return rc;
     const Dev& d = e->d;
-    return timed_launch(e, 2, [&] {
-        hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, e->stream, d, (uint64_t*)nullptr, 0);
-        hipLaunchKernelGGL(k_peer_scan, dim3(1), dim3(1024), 0, e->stream, d);
-        hipLaunchKernelGGL(k_pack, dim3(d.nblocks), dim3(BLOCK), 0, e->stream, d);
-        hipLaunchKernelGGL(k_fill, dim3(fill_chunks(d), d.G), dim3(BLOCK), 0, e->stream, d, send);
+    return timed_launch(e, SG_K_PLAN, [&] {
+        hipLaunchKernelGGL(k_locmin, dim3(1), dim3(PL_T), 0, e->stream, d);
+        hipLaunchKernelGGL(k_pack, dim3(d.P), dim3(256), 0, e->stream, d);
+        hipLaunchKernelGGL(k_fill, dim3(fill_chunks(d), d.G), dim3(256), 0, e->stream, d, send);
     });
 }
 
@@ -1323,34 +1881,25 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
         sg_set_error("sg_engine_step_recv: NULL receive buffer");
         return SG_ERR_INVAL;
     }
-    if ((rc = enqueue_local_insert(e))) return rc;
-    const Dev& d = e->d;
-    if ((rc = timed_launch(e, 1, [&] {
-             hipLaunchKernelGGL(k_insert_recv, dim3(fill_chunks(d), d.G), dim3(BLOCK), 0, e->stream, d,
-                                recv);
-         })))
-        return rc;
-    return timed_launch(e, 2, [&] {
-        hipLaunchKernelGGL(k_window, dim3(1), dim3(1), 0, e->stream, d, recv);
-    });
+    return enqueue_insert_plan(e, recv, 1);
 }
 
 int sg_engine_set_timing(sg_engine* e, int enabled) {
     if (!e) return SG_ERR_INVAL;
     e->timing = enabled != 0;
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < SG_KCLASSES; ++i) {
         e->ms[i] = 0;
         e->launches[i] = 0;
     }
     return SG_OK;
 }
 
-int sg_engine_kernel_times(sg_engine* e, double* ms3, uint64_t* launches) {
+int sg_engine_kernel_times(sg_engine* e, double* ms, uint64_t* launches) {
     if (!e) return SG_ERR_INVAL;
     int rc = sg_engine_sync(e);
     if (rc) return rc;
-    for (int i = 0; i < 3; ++i) {
-        if (ms3) ms3[i] = e->ms[i];
+    for (int i = 0; i < SG_KCLASSES; ++i) {
+        if (ms) ms[i] = e->ms[i];
         if (launches) launches[i] = e->launches[i];
     }
     return SG_OK;

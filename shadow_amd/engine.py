@@ -115,10 +115,17 @@ class Engine:
         L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
 
     def kernel_times(self):
-        ms = (C.c_double * 3)()
-        n = (C.c_uint64 * 3)()
+        """{class: (total ms, launches)} since set_timing(True), per sg_kernel_class."""
+        k = len(L.KERNEL_CLASSES)
+        ms = (C.c_double * k)()
+        n = (C.c_uint64 * k)()
         L.check(L.lib().sg_engine_kernel_times(self.h, ms, n))
-        return {"process": (ms[0], n[0]), "insert": (ms[1], n[1]), "window": (ms[2], n[2])}
+        return {c: (ms[i], n[i]) for i, c in enumerate(L.KERNEL_CLASSES)}
+
+    def geometry(self) -> dict:
+        g = L.EngineGeom()
+        L.check(L.lib().sg_engine_geometry(self.h, C.byref(g)))
+        return g.as_dict()
 
     # ---------------------------------------------------------- multi shard
     def exchange_rows(self) -> int:

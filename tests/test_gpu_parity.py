@@ -134,17 +134,19 @@ def test_full_size_c4_invariants():
     assert np.array_equal(g["digest"], o["digest"])
 
 
-@pytest.mark.parametrize("cap", [8, 128])
+@pytest.mark.parametrize("cap", [1, 128])
 def test_queue_capacity_paths(cap):
-    """queue_cap <= 64 runs the masked selection, > 64 the rescanning one; a cap
-    of 8 (below PHOLD's per-host peak) must fail loudly, never silently."""
-    cfg = phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.5)
-    if cap == 8:
+    """queue_cap sizes the calendar's chunk pool (n_local * queue_cap events plus
+    one chunk per ring bucket).  A pool far below the live event count must fail
+    loudly (SG_ERR_OVERFLOW), never silently; a large one stays bit-exact."""
+    if cap == 1:
+        cfg = phold.c2_config(n_hosts=20_000, end_time_s=0.3)
         eng = Engine(cfg, queue_cap=cap)
         eng.boot()
         with pytest.raises(L.SgError) as ei:
             eng.run()
         assert ei.value.code == L.SG_ERR_OVERFLOW
         return
+    cfg = phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.5)
     eng, orc = _run_both(cfg, trace=200_000, queue_cap=cap)
     _assert_same(eng, orc)

@@ -36,7 +36,7 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert L.lib().sg_abi_version() == 2
+    assert L.lib().sg_abi_version() == 3
 
 
 def test_engine_without_gpu_fails_loudly():
