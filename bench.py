@@ -62,6 +62,8 @@ def parse():
                     default=min(16, len(os.sched_getaffinity(0))),
                     help="CPU baseline worker threads (the GPU box's share is 16 cores)")
     ap.add_argument("--batch", type=int, default=32, help="rounds enqueued per host sync")
+    ap.add_argument("--kernel-rounds", type=int, default=50,
+                    help="rounds after the timed region that are re-run with per-kernel HIP events")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N > 1: nccl (RCCL, the measured path) or gloo (rehearsal only)")
     ap.add_argument("--same-device", action="store_true",
@@ -112,9 +114,8 @@ def run_single(args):
     eng.boot()
     eng.run(args.warmup, batch=args.batch)
     s0 = eng.stats()
-    a0, _ = eng.active_hosts()
-    eng.set_timing(True)
     eng.sync()
+    # timed region: K rounds, nothing but the rounds on the stream
     t0 = time.perf_counter()
     left = args.steps
     while left > 0:
@@ -126,18 +127,27 @@ def run_single(args):
             eng.sync()  # bounded queue depth; the same host round-trips sg_engine_run makes
     eng.sync()
     dt = time.perf_counter() - t0
-    kt = eng.kernel_times()
-    eng.set_timing(False)
     s1 = eng.stats()
-    a1, _ = eng.active_hosts()
     if s1["overflow"]:
         raise SystemExit(f"device queue overflow during bench: {s1['overflow']:#x}")
     pops = s1["pops"] - s0["pops"]
     rounds = s1["rounds"] - s0["rounds"]
     if rounds != args.steps:
         raise SystemExit(f"simulation ended early: {rounds} of {args.steps} rounds")
+    # kernel durations: the next rounds of the same run with HIP events around
+    # every launch on the engine stream (the events themselves add gaps between
+    # kernels, so they stay out of the headline region above)
+    a1, _ = eng.active_hosts()
+    kr = max(1, min(args.steps, args.kernel_rounds))
+    eng.set_timing(True)
+    eng.run(kr, batch=args.batch)
+    kt = eng.kernel_times()
+    eng.set_timing(False)
+    s2 = eng.stats()
+    a2, _ = eng.active_hosts()
+    kpops = s2["pops"] - s1["pops"]
     proc_ms, proc_n = kt["process"]
-    alg_bytes = ALG_BYTES_PER_EVENT * pops + ALG_BYTES_PER_ACTIVE_HOST * (a1 - a0)
+    alg_bytes = ALG_BYTES_PER_EVENT * kpops + ALG_BYTES_PER_ACTIVE_HOST * (a2 - a1)
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
@@ -166,7 +176,8 @@ def run_single(args):
                      "traffic_gbs": traffic / avg_launch_s / 1e9 if traffic and avg_launch_s else None,
                      "kernel": DOMINANT, "avg_launch_us": avg_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
-                     "kernel_ms": {k: v[0] for k, v in kt.items()}},
+                     "timing_rounds": kr,
+                     "kernel_us_per_round": {k: v[0] * 1e3 / kr for k, v in kt.items()}},
     }
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)

@@ -171,6 +171,7 @@ struct Dev {
     Rec* extras;              // [P][K2_T][XCAP]
     uint32_t* rcnt;           // [P] staged local events
     Rec* loc;                 // [P][ECAP]
+    Rec* sends;               // [P][ECAP] k_proc's per-send records (phases A-C)
     // per-workgroup partials
     uint64_t* c1min;          // [G1] carry min
     uint64_t* p2min;          // [2][P] emitted min, discovery min
@@ -186,6 +187,7 @@ struct Dev {
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
+    uint64_t* stamps;         // [P][8] s_memrealtime per k_proc phase (SG_STAMPS=1), else null
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
@@ -226,7 +228,10 @@ __device__ __forceinline__ uint64_t digest_mix(uint64_t pos, uint64_t t, uint32_
 }
 
 // Destination draw; returns N when no host is selected (test_phold.c:176-177)
-// and the chosen host's info record.
+// and the chosen host's info record.  Weights rule: the first i with
+// x <= wt[i] (non-decreasing thresholds); the uniform-position guess and its
+// two neighbours are loaded together, which settles near-uniform weights in
+// one round trip, and anything else is bisected.
 __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
     const uint32_t N = d.N;
     const HostInfo* w = d.hinfo;
@@ -238,41 +243,28 @@ __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo
         info = w[dd];
         return dd;
     }
-    // first i with x <= wt[i] (non-decreasing): guess from the uniform
-    // position, walk a few steps, bisect the rest.
     uint32_t g = (uint32_t)(((uint64_t)(uint32_t)x * N) >> 31);
     if (g >= N) g = N - 1;
-    HostInfo cur = w[g];
+    const HostInfo cur = w[g];
+    const HostInfo prev = w[g > 0 ? g - 1 : 0];
+    const HostInfo next = w[g + 1 < N ? g + 1 : N - 1];
+    uint32_t lo, hi;
     if (x <= cur.wt) {
-        for (int k = 0; k < 8; ++k) {
-            if (g == 0) break;
-            const HostInfo prev = w[g - 1];
-            if (x > prev.wt) break;
-            --g;
-            cur = prev;
-        }
-        if (g > 0 && x <= w[g - 1].wt) {
-            uint32_t lo = 0, hi = g - 1;  // answer in [lo, hi]
-            while (lo < hi) {
-                const uint32_t mid = lo + (hi - lo) / 2;
-                if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
-            }
-            g = lo;
-            cur = w[g];
-        }
-        info = cur;
-        return g;
-    }
-    if (x > w[N - 1].wt) return N;
-    for (int k = 0; k < 8; ++k) {
-        ++g;
-        cur = w[g];
-        if (x <= cur.wt) {
+        if (g == 0 || x > prev.wt) {
             info = cur;
             return g;
         }
+        lo = 0;
+        hi = g - 1;  // x <= wt[g-1]: the answer is in [0, g-1]
+    } else {
+        if (g + 1 < N && x <= next.wt) {
+            info = next;
+            return g + 1;
+        }
+        if (g + 1 >= N || x > w[N - 1].wt) return N;
+        lo = g + 2;
+        hi = N - 1;  // wt[g+1] < x <= wt[N-1]
     }
-    uint32_t lo = g + 1, hi = N - 1;
     while (lo < hi) {
         const uint32_t mid = lo + (hi - lo) / 2;
         if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
@@ -430,37 +422,81 @@ __global__ void k_boot(Dev d) {
 
 // --------------------------------------------------------------- gather ----
 // Due chunks → partition regions: two passes over the workgroup's chunks
-// (LDS histogram + one reservation per partition, then the scatter).
+// (LDS histogram + one reservation per partition, then the scatter).  The
+// workgroup's due entries are staged in LDS so that every event load of a
+// pass is independent of the others.
+constexpr uint32_t GDMAX = 32;   // due entries staged per batch
+constexpr int GUNR = 4;          // events in flight per thread
+
+template <bool SCATTER>
+__device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
+                                            uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
+                                            uint64_t& cmin, uint64_t& ntomb) {
+    const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
+    const uint32_t tot = nb * CH;
+    for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += K1_T * GUNR) {
+        Rec r[GUNR];
+        bool v[GUNR];
+#pragma unroll
+        for (int q = 0; q < GUNR; ++q) {
+            const uint32_t e = e0 + q * K1_T;
+            const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
+            v[q] = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
+            r[q] = v[q] ? d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))] : Rec{TOMB, 0};
+        }
+#pragma unroll
+        for (int q = 0; q < GUNR; ++q) {
+            if (!v[q] || r[q].a == TOMB) continue;
+            const uint32_t e = e0 + q * K1_T;
+            const DueEnt de = s_de[e >> CH_SHIFT];
+            const uint64_t t = de.base + (r[q].a & M40);
+            const uint32_t dl = (uint32_t)(r[q].a >> 40);
+            if (dl >= d.L) {
+                if (!SCATTER) flag(d, OV_BUG);
+                continue;
+            }
+            if (t >= E) {
+                if (!SCATTER) cmin = t < cmin ? t : cmin;
+                continue;
+            }
+            const uint32_t p = dl >> sh;
+            if (!SCATTER) {
+                atomicAdd(&s_cnt[p], 1u);
+                continue;
+            }
+            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            if (slot < d.CAPP)
+                d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl & hmask) << 52) | (t - S), r[q].k};
+            if (de.nflags & RETAINED) {
+                d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
+                ++ntomb;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
     const RoundState* rs = d.rs;
     if (rs->done | rs->phase) return;
     __shared__ uint32_t s_cnt[PMAX];
     __shared__ uint32_t s_cur[PMAX];
+    __shared__ DueEnt s_de[GDMAX];
     __shared__ uint64_t s16[16];
     const uint64_t S = rs->S, E = rs->E;
     const uint64_t nd = rs->ndue;
     const uint64_t c0 = nd * blockIdx.x / gridDim.x, c1 = nd * (blockIdx.x + 1) / gridDim.x;
-    const uint32_t P = d.P, sh = d.hp_shift, hmask = d.HP - 1;
-    for (uint32_t p = threadIdx.x; p < P; p += K1_T) s_cnt[p] = 0;
-    __syncthreads();
-    uint64_t cmin = UINT64_MAX;
-    for (uint64_t c = c0; c < c1; ++c) {
-        const DueEnt de = d.due[c];
-        const bool ok = de.id < d.NCH;
-        if (!ok && de.id != EMPTY && threadIdx.x == 0) flag(d, OV_BUG);
-        const uint32_t n = ok ? de.nflags & 0xFFFFu : 0;
-        const Rec* ch = d.pool + ((size_t)(ok ? de.id : 0) << CH_SHIFT);
-        for (uint32_t i = threadIdx.x; i < n; i += K1_T) {
-            const uint64_t a = ch[i].a;
-            if (a == TOMB) continue;
-            const uint64_t t = de.base + (a & M40);
-            if ((uint32_t)(a >> 40) >= d.L) {
-                flag(d, OV_BUG);
-                continue;
-            }
-            if (t < E) atomicAdd(&s_cnt[(uint32_t)(a >> 40) >> sh], 1u);
-            else cmin = t < cmin ? t : cmin;
-        }
+    const uint32_t P = d.P;
+    for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
+        s_cnt[p] = 0;
+        s_cur[p] = 0;
+    }
+    uint64_t cmin = UINT64_MAX, ntomb = 0;
+    for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
+        const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
+        __syncthreads();
+        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+        __syncthreads();
+        gather_pass<false>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
@@ -470,32 +506,13 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
             if (base + c > d.CAPP) flag(d, OV_PART);
             s_cnt[p] = base;
         }
-        s_cur[p] = 0;
     }
-    __syncthreads();
-    uint64_t ntomb = 0;
-    for (uint64_t c = c0; c < c1; ++c) {
-        const DueEnt de = d.due[c];
-        const bool ok = de.id < d.NCH;
-        const uint32_t n = ok ? de.nflags & 0xFFFFu : 0;
-        const bool ret = (de.nflags & RETAINED) != 0;
-        Rec* ch = d.pool + ((size_t)(ok ? de.id : 0) << CH_SHIFT);
-        for (uint32_t i = threadIdx.x; i < n; i += K1_T) {
-            const Rec r = ch[i];
-            if (r.a == TOMB) continue;
-            const uint64_t t = de.base + (r.a & M40);
-            if (t >= E) continue;
-            const uint32_t dl = (uint32_t)(r.a >> 40);
-            if (dl >= d.L) continue;
-            const uint32_t p = dl >> sh;
-            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
-            if (slot < d.CAPP)
-                d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl & hmask) << 52) | (t - S), r.k};
-            if (ret) {
-                ch[i].a = TOMB;
-                ++ntomb;
-            }
-        }
+    for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
+        const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
+        __syncthreads();
+        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+        __syncthreads();
+        gather_pass<true>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
     }
     const uint64_t m = block_min(cmin, s16);
     const uint64_t nt = block_sum(ntomb, s16);
@@ -526,6 +543,30 @@ struct ProcShared {
     uint32_t nloc, nrem;
     uint32_t peer[MAXG];
 };
+
+// Stage one new event (time already bumped) for k_count (this shard's hosts) or
+// for the outbox (other shards).
+__device__ __forceinline__ void stage_event(const Dev& d, uint64_t S, uint32_t part, ProcShared& sh,
+                                            Acc& a, uint32_t dst, uint64_t tn, uint64_t key) {
+    const uint32_t dl = dst - d.lo;
+    if (dl < d.L) {
+        const uint32_t slot = atomicAdd(&sh.nloc, 1u);
+        if (slot < d.ECAP) d.loc[(size_t)part * d.ECAP + slot] = Rec{((uint64_t)dl << 40) | (tn - S), key};
+        else a.overflow = true;
+    } else {
+        const uint32_t slot = atomicAdd(&sh.nrem, 1u);
+        if (slot < d.ECAP) {
+            const size_t so = (size_t)part * d.ECAP + slot;
+            d.rem[so] = Slot{tn, key};
+            d.rem_dst[so] = dst;
+            atomicAdd(&sh.peer[owner_of(d, dst)], 1u);
+        } else {
+            a.overflow = true;
+        }
+    }
+    a.emin = tn < a.emin ? tn : a.emin;
+    ++a.ctr[C_EMIT];
+}
 
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
 // Self events that fall inside the window go to the lane's same-round list
@@ -589,46 +630,50 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             tn = E;
             ++a.ctr[C_BUMPED];
         }
-        const uint32_t dl = dst - d.lo;
-        if (dl < d.L) {
-            const uint32_t slot = atomicAdd(&sh.nloc, 1u);
-            if (slot < d.ECAP) d.loc[(size_t)part * d.ECAP + slot] = Rec{((uint64_t)dl << 40) | (tn - S), key};
-            else a.overflow = true;
-        } else {
-            const uint32_t slot = atomicAdd(&sh.nrem, 1u);
-            if (slot < d.ECAP) {
-                const size_t so = (size_t)part * d.ECAP + slot;
-                d.rem[so] = Slot{tn, key};
-                d.rem_dst[so] = dst;
-                atomicAdd(&sh.peer[owner_of(d, dst)], 1u);
-            } else {
-                a.overflow = true;
-            }
-        }
-        a.emin = tn < a.emin ? tn : a.emin;
-        ++a.ctr[C_EMIT];
+        stage_event(d, S, part, sh, a, dst, tn, key);
     }
 }
 
 // One workgroup per partition of HP hosts.
+//   sort     the partition's due events by host (LDS counting sort) and list
+//            the active hosts;
+//   phase A  per active host: pop order (event_compare), trace digest, and the
+//            host's rand_r draws, which are pure arithmetic: one record
+//            {time, x, c} per send with a destination.  A host that could
+//            create an event for itself inside this window (its earliest event
+//            + its self-path delay < barrier) runs the whole sequential body
+//            here instead (same-round self events, host_single.c:237-267);
+//   phase B  one lane per send, balanced across the workgroup: destination,
+//            path record, reliability test, delivery time;
+//   phase C  per active host, in send order: srcHostEventID, endTime drop,
+//            barrier bump, staging.
+constexpr uint32_t HPT = HPMAX / K2_T;  // active hosts per lane, at most
+
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const RoundState* rs = d.rs;
     if (rs->done | rs->phase) return;
     __shared__ uint32_t s_n[HPMAX];    // events per host
     __shared__ uint32_t s_c[HPMAX];    // start offset, then end (scatter cursor)
     __shared__ uint16_t s_act[HPMAX];  // active hosts, ascending
+    __shared__ uint32_t s_vh[HPMAX];   // vertex of active host j
+    __shared__ uint32_t s_nsend;
+    __shared__ int32_t s_last;         // last weight threshold: x above it selects no host
     __shared__ ProcShared sh;
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
     const uint64_t S = rs->S, E = rs->E;
     const uint32_t p = blockIdx.x, HP = d.HP;
     const uint32_t tid = threadIdx.x;
+    uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * 8 : nullptr;
+    if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
     for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
     if (tid == 0) {
         sh.nloc = 0;
         sh.nrem = 0;
+        s_nsend = 0;
+        s_last = d.dst_rule == SG_DST_WEIGHTS ? d.hinfo[d.N - 1].wt : INT32_MAX;
     }
     if (tid < MAXG) sh.peer[tid] = 0;
     __syncthreads();
@@ -673,6 +718,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if (pos < n) part2[pos] = r;
     }
     __syncthreads();  // part2 is read back by other lanes of this workgroup
+    if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
     Acc a;
 #pragma unroll
@@ -681,8 +727,18 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     a.emin = SIMTIME_MAX;
     a.overflow = false;
     Rec* xs = d.extras + ((size_t)p * K2_T + tid) * XCAP;
+    Rec* snd = d.sends + (size_t)p * d.ECAP;
     const uint32_t hbase = d.lo + p * HP;
-    for (uint32_t j = tid; j < nact; j += K2_T) {
+    const int32_t last = s_last;
+    uint32_t sbase[HPT], scnt[HPT];  // this lane's hosts' send ranges (UINT32_MAX: sequential)
+
+    // ---- phase A
+#pragma unroll
+    for (uint32_t q = 0; q < HPT; ++q) {
+        sbase[q] = UINT32_MAX;
+        scnt[q] = 0;
+        const uint32_t j = tid + q * K2_T;
+        if (j >= nact) continue;
         const uint32_t hl = s_act[j];
         const uint32_t cnt = s_n[hl];
         Rec* seg = part2 + (s_c[hl] - cnt);
@@ -695,35 +751,167 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         c.s = d.hs[lh];
         c.vh = d.hinfo[c.h].vertex;
+        s_vh[j] = c.vh;
         ++a.ctr[C_ACTIVE];
-        uint32_t ns = cnt, nx = 0;
-        auto append = [&](uint64_t trel, uint64_t key) -> bool {
-            if (nx >= XCAP) return false;
-            xs[nx++] = Rec{trel, key};
-            return true;
-        };
-        for (;;) {
-            Best b{UINT64_MAX, 0, UINT32_MAX};
-            for (uint32_t i = 0; i < ns; ++i) {
-                const Rec r = seg[i];
-                best_take(b, r.a & M52, r.k, i);
+        // pop order: selection sort of the (small) segment by (time, key)
+        for (uint32_t i = 0; i + 1 < cnt; ++i) {
+            Best b{UINT64_MAX, 0, i};
+            for (uint32_t k = i; k < cnt; ++k) {
+                const Rec r = seg[k];
+                best_take(b, r.a & M52, r.k, k);
             }
-            for (uint32_t i = 0; i < nx; ++i) {
-                const Rec r = xs[i];
-                best_take(b, r.a, r.k, 0x80000000u | i);
+            if (b.slot != i) {
+                const Rec t = seg[i];
+                seg[i] = seg[b.slot];
+                seg[b.slot] = t;
             }
-            if (b.slot == UINT32_MAX) break;
-            if (b.slot & 0x80000000u) {
-                const uint32_t i = b.slot & 0x7FFFFFFFu;
-                --nx;
-                if (i != nx) xs[i] = xs[nx];
-            } else {
-                --ns;
-                if (b.slot != ns) seg[b.slot] = seg[ns];
-            }
-            execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
         }
-        d.hs[lh] = c.s;
+        const uint64_t self_delay = d.pairs[(size_t)c.vh * d.V + c.vh].delay;
+        if (S + (seg[0].a & M52) + self_delay < E) {
+            // sequential body: a self event may land inside this window
+            uint32_t nx = 0;
+            auto append = [&](uint64_t trel, uint64_t key) -> bool {
+                if (nx >= XCAP) return false;
+                xs[nx++] = Rec{trel, key};
+                return true;
+            };
+            uint32_t ns = cnt, i0 = 0;
+            for (;;) {
+                Best b{UINT64_MAX, 0, UINT32_MAX};
+                for (uint32_t i = i0; i < ns; ++i) {
+                    const Rec r = seg[i];
+                    best_take(b, r.a & M52, r.k, i);
+                }
+                for (uint32_t i = 0; i < nx; ++i) {
+                    const Rec r = xs[i];
+                    best_take(b, r.a, r.k, 0x80000000u | i);
+                }
+                if (b.slot == UINT32_MAX) break;
+                if (b.slot & 0x80000000u) {
+                    const uint32_t i = b.slot & 0x7FFFFFFFu;
+                    --nx;
+                    if (i != nx) xs[i] = xs[nx];
+                } else {
+                    --ns;
+                    if (b.slot != ns) seg[b.slot] = seg[ns];
+                }
+                execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
+            }
+            d.hs[lh] = c.s;
+            continue;
+        }
+        // count this host's sends (arithmetic only), reserve, then record them
+        uint32_t r = c.s.rng, ns = 0;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const uint64_t bk = seg[i].k;
+            const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
+            const uint32_t nsend = boot ? d.load : 1u;
+            for (uint32_t m = 0; m < nsend; ++m) {
+                const int32_t x = dev_rand_r(r);
+                if (x > last) continue;
+                (void)dev_rand_r(r);
+                ++ns;
+            }
+        }
+        const uint32_t base = atomicAdd(&s_nsend, ns);
+        if (base + ns > d.ECAP) {
+            a.overflow = true;
+            continue;
+        }
+        sbase[q] = base;
+        scnt[q] = ns;
+        uint32_t k = base;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const Rec ev = seg[i];
+            const uint64_t trel = ev.a & M52, bt = S + trel;
+            const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
+            const uint64_t bseq = ev.k & SEQ_MASK;
+            c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
+            if (d.trace) {
+                const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
+                if (ts < d.trace_cap) {
+                    sg_trace_rec tr;
+                    tr.time = bt;
+                    tr.seq = bseq;
+                    tr.host = c.h;
+                    tr.src = bsrc;
+                    tr.pos = c.s.pops;
+                    d.trace[ts] = tr;
+                } else {
+                    a.overflow = true;
+                }
+            }
+            ++c.s.pops;
+            ++a.ctr[C_POPS];
+            const bool boot = (bsrc == c.h) & (bseq == 0);
+            a.ctr[C_BOOTS] += boot;
+            const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+            for (uint32_t m = 0; m < nsend; ++m) {
+                const int32_t x = dev_rand_r(c.s.rng);
+                if (x > last) {  // no host selected (test_phold.c:176-177)
+                    ++a.ctr[C_NULL];
+                    continue;
+                }
+                const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
+                ++a.ctr[C_SENDS];
+                snd[k++] = Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
+            }
+        }
+        HostState* hp = d.hs + lh;
+        hp->rng = c.s.rng;
+        hp->pops = c.s.pops;
+        hp->digest = c.s.digest;
+    }
+    __syncthreads();
+    if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- phase B: one lane per send
+    const uint32_t nsend = s_nsend < d.ECAP ? s_nsend : d.ECAP;
+    for (uint32_t i = tid; i < nsend; i += K2_T) {
+        const Rec r = snd[i];
+        const uint32_t j = (uint32_t)(r.a >> 52);
+        const uint64_t bt = S + (r.a & M52);
+        const int32_t x = (int32_t)(uint32_t)r.k, ch = (int32_t)(uint32_t)(r.k >> 32);
+        HostInfo di;
+        const uint32_t dst = choose_dst(d, x, di);
+        const PairRec pr = d.pairs[(size_t)s_vh[j] * d.V + di.vertex];
+        a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
+        const bool keep = bt < d.bootstrap_end || ch <= pr.keep;  // worker.c:268-273
+        const uint64_t tn = bt + pr.delay;                        // worker.c:275-277
+        snd[i] = Rec{((uint64_t)keep << 63) | (tn - S), dst};
+    }
+    __syncthreads();
+    if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- phase C: per host, in send order
+#pragma unroll
+    for (uint32_t q = 0; q < HPT; ++q) {
+        if (sbase[q] == UINT32_MAX) continue;
+        const uint32_t j = tid + q * K2_T;
+        const uint32_t h = hbase + s_act[j];
+        HostState* hp = d.hs + (h - d.lo);
+        uint64_t evc = hp->evc;
+        for (uint32_t k = sbase[q]; k < sbase[q] + scnt[q]; ++k) {
+            const Rec r = snd[k];
+            if (!(r.a >> 63)) {
+                ++a.ctr[C_DROPREL];
+                continue;
+            }
+            const uint64_t sq = evc++;              // event.c:38
+            uint64_t tn = S + (r.a & M40);
+            if (tn >= d.end_time) {                 // scheduler.c:343-346
+                ++a.ctr[C_DROPEND];
+                continue;
+            }
+            const uint32_t dst = (uint32_t)r.k;
+            if (dst == h && tn < E) a.overflow = true;  // excluded by the phase A test
+            if (dst != h && tn < E) {               // host_single.c:180-184
+                tn = E;
+                ++a.ctr[C_BUMPED];
+            }
+            stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq);
+        }
+        hp->evc = evc;
     }
 
     // workgroup partials: cumulative counters, this round's two minima
@@ -750,11 +938,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
     }
     if (tid == 0) {
-        if (sh.nloc > d.ECAP || sh.nrem > d.ECAP) flag(d, OV_PROC);
+        if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
         d.rcnt[p] = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
     if (d.G > 1 && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
+    if (stamp && tid == 0) {
+        stamp[4] = __builtin_amdgcn_s_memrealtime();
+        stamp[5] = n;
+        stamp[6] = nact;
+        stamp[7] = s_nsend;
+    }
 }
 
 // --------------------------------------------------------------- insert ----
@@ -946,45 +1140,12 @@ __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t&
     j = rs->jmin < j ? rs->jmin : j;
 }
 
-// Give every bucket the chunks its count needs (after k_count), from the free
-// ring; chunk ids go to the bucket's table for k_scatter and the next listing.
-__device__ void plan_alloc(const Dev& d, uint64_t* s16, uint64_t& s_head, uint64_t s_tail) {
-    const uint32_t R = d.R, NCH = d.NCH;
-    constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
-    uint32_t need[PER];
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t rb = threadIdx.x * PER + j;
-        need[j] = 0;
-        if (rb < R) {
-            const uint64_t want = ((uint64_t)d.bcnt[rb] + CH - 1) >> CH_SHIFT;
-            const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
-            const uint32_t have = d.nal[rb];
-            need[j] = w > have ? w - have : 0;
-        }
-        mine += need[j];
-    }
-    uint64_t total;
-    uint64_t off = block_excl_scan(mine, s16, &total);
-    const uint64_t head = s_head;
-    const uint64_t avail = s_tail - head;
-    if (total > avail && threadIdx.x == 0) flag(d, OV_POOL);
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t rb = threadIdx.x * PER + j;
-        if (rb >= R || !need[j]) continue;
-        uint32_t have = d.nal[rb];
-        uint32_t* tab = d.btab + (size_t)rb * NCH;
-        uint32_t k = 0;
-        for (; k < need[j] && off + k < avail; ++k) tab[have + k] = d.fring[(head + off + k) % NCH];
-        d.nal[rb] = have + k;
-        off += need[j];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_head = head + (total < avail ? total : avail);
-    __syncthreads();
-}
+// k_plan keeps the ring's bucket metadata in LDS for the whole launch: one
+// coalesced load, scans and updates in LDS, one write-back.
+struct PlanLds {
+    uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
+    uint64_t mn[RMAX];
+};
 
 // mode 0: single shard, end of round.  mode 1: multi-shard, window from the
 // received headers (or the end of a drain step).  mode 2: boot (list the
@@ -992,12 +1153,19 @@ __device__ void plan_alloc(const Dev& d, uint64_t* s16, uint64_t& s_head, uint64
 __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int mode) {
     RoundState* rs = d.rs;
     if (rs->done) return;
+    __shared__ PlanLds B;
     __shared__ uint64_t s16[16];
-    __shared__ uint32_t s_nfree;
     __shared__ uint64_t s_head, s_tail, s_S, s_E, s_done, s_more, s_spent, s_m, s_j, s_ovf;
+    constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
     const uint32_t R = d.R, NCH = d.NCH;
     const uint64_t W = d.W;
     const uint32_t tid = threadIdx.x;
+    for (uint32_t rb = tid; rb < R; rb += PL_T) {
+        B.cnt[rb] = d.bcnt[rb];
+        B.tomb[rb] = d.btomb[rb];
+        B.nal[rb] = d.nal[rb];
+        B.mn[rb] = d.bmin[rb];
+    }
     if (tid == 0) {
         s_head = rs->fl_head;
         s_tail = rs->fl_tail;
@@ -1006,7 +1174,6 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         s_done = 0;
         s_more = 0;
         s_spent = UINT64_MAX;
-        s_nfree = 0;
         if (mode == 1) {
             uint64_t more = 0, m = UINT64_MAX, j = UINT64_MAX, ovf = 0;
             for (uint32_t p = 0; p < d.G; ++p) {
@@ -1029,51 +1196,94 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             s_ovf = ovf;
         }
     }
-    __syncthreads();
-    const bool round_done = mode == 0 || (mode == 1 && !s_more);
     uint64_t m = 0, j = 0, ovf = 0;
     if (mode == 0) {
-        reduce_local(d, s16, m, j);
+        reduce_local(d, s16, m, j);  // barriers inside
         ovf = rs->overflow;
-    } else if (mode == 1) {
+    }
+    __syncthreads();
+    if (mode == 1) {
         m = s_m;
         j = s_j;
         ovf = s_ovf;
     }
+    const bool round_done = mode == 0 || (mode == 1 && !s_more);
     if (round_done) {
         // free the chunks of the window just executed (not the retained
         // bucket's) and reset its fully consumed buckets
         const uint64_t nd = rs->ndue, tail = s_tail, ndb = rs->ndueb;
+        uint64_t mine = 0;
+        for (uint64_t i = tid; i < nd; i += PL_T) {
+            const DueEnt de = d.due[i];
+            mine += !(de.nflags & RETAINED) && de.id < NCH;
+        }
+        uint64_t tot;
+        uint64_t k = block_excl_scan(mine, s16, &tot);
         for (uint64_t i = tid; i < nd; i += PL_T) {
             const DueEnt de = d.due[i];
             if ((de.nflags & RETAINED) || de.id >= NCH) continue;
-            d.fring[(tail + atomicAdd(&s_nfree, 1u)) % NCH] = de.id;
+            d.fring[(tail + k++) % NCH] = de.id;
         }
         for (uint64_t i = 0; i < ndb; ++i) {
             const uint32_t rb = d.dueb[i];
-            const uint32_t nc = d.nal[rb];
+            const uint32_t nc = B.nal[rb];
             for (uint32_t ci = tid; ci < nc; ci += PL_T) d.btab[(size_t)rb * NCH + ci] = EMPTY;
         }
         __syncthreads();
-        for (uint64_t i = tid; i < ndb; i += PL_T) reset_bucket(d, d.dueb[i]);
+        for (uint64_t i = tid; i < ndb; i += PL_T) {
+            const uint32_t rb = d.dueb[i];
+            B.cnt[rb] = 0;
+            B.tomb[rb] = 0;
+            B.nal[rb] = 0;
+            B.mn[rb] = UINT64_MAX;
+        }
+        if (tid == 0) s_tail = tail + tot;
+        __syncthreads();
+    }
+    if (mode != 2) {
+        // every bucket gets the chunks its count needs (k_count ran), from the ring
+        uint32_t need[PER];
+        uint64_t mine = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t rb = tid * PER + q;
+            need[q] = 0;
+            if (rb < R) {
+                const uint64_t want = ((uint64_t)B.cnt[rb] + CH - 1) >> CH_SHIFT;
+                const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
+                need[q] = w > B.nal[rb] ? w - B.nal[rb] : 0;
+            }
+            mine += need[q];
+        }
+        uint64_t total;
+        uint64_t off = block_excl_scan(mine, s16, &total);
+        const uint64_t head = s_head, avail = s_tail - head;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t rb = tid * PER + q;
+            if (rb >= R || !need[q]) continue;
+            const uint32_t have = B.nal[rb];
+            uint32_t* tab = d.btab + (size_t)rb * NCH;
+            uint32_t k = 0;
+            for (; k < need[q] && off + k < avail; ++k) tab[have + k] = d.fring[(head + off + k) % NCH];
+            B.nal[rb] = have + k;
+            off += need[q];
+        }
         __syncthreads();
         if (tid == 0) {
-            s_tail = tail + s_nfree;
-            s_nfree = 0;
+            if (total > avail) flag(d, OV_POOL);
+            s_head = head + (total < avail ? total : avail);
         }
         __syncthreads();
     }
-    if (mode != 2) plan_alloc(d, s16, s_head, s_tail);
+    bool list = true;
     if (mode == 1 && s_more) {  // drain step: same window, more exchange
+        list = false;
         if (tid == 0) {
             rs->phase = 1;
             rs->overflow |= ovf;
-            rs->fl_head = s_head;
-            rs->fl_tail = s_tail;
         }
-        return;
-    }
-    if (round_done) {
+    } else if (round_done) {
         if (tid == 0) {
             rs->phase = 0;
             rs->jmin = j;
@@ -1082,74 +1292,83 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             s_S = rs->S;
             s_E = rs->E;
             s_done = rs->done;
-            if (s_done) {
-                rs->fl_head = s_head;
-                rs->fl_tail = s_tail;
+        }
+        __syncthreads();
+        list = !s_done;
+    }
+    if (list) {
+        // list the due chunks of the new window [S, E)
+        const uint64_t S = s_S, E = s_E;
+        const uint64_t bS = S / W, bL = (E - 1) / W;
+        const uint64_t pr = rs->ret_b;
+        if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
+            const uint32_t rb = (uint32_t)(pr % R);
+            const uint32_t nc = B.nal[rb];
+            const uint64_t tail = s_tail;
+            for (uint32_t ci = tid; ci < nc; ci += PL_T) {
+                uint32_t* e = &d.btab[(size_t)rb * NCH + ci];
+                d.fring[(tail + ci) % NCH] = *e;
+                *e = EMPTY;
             }
+            __syncthreads();
+            if (tid == 0) {
+                s_tail = tail + nc;
+                s_spent = rb;
+                B.cnt[rb] = 0;
+                B.tomb[rb] = 0;
+                B.nal[rb] = 0;
+                B.mn[rb] = UINT64_MAX;
+            }
+            __syncthreads();
+        }
+        // Fully due buckets keep their tables until the next plan (k_scatter of
+        // this round still writes the events k_count counted into them).
+        const bool straddle = E < (bL + 1) * W;
+        uint64_t nd = 0, ndb = 0;
+        for (uint64_t b = bS; b <= bL; ++b) {
+            const uint32_t rb = (uint32_t)(b % R);
+            const uint32_t c = B.cnt[rb], nc = B.nal[rb];
+            const bool ret = straddle && b == bL;
+            const uint32_t* tab = d.btab + (size_t)rb * NCH;
+            for (uint32_t ci = tid; ci < nc; ci += PL_T) {
+                const uint32_t left = c - (ci << CH_SHIFT);
+                const uint32_t n = left < CH ? left : CH;
+                d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
+            }
+            nd += nc;
+            if (tid == 0 && !ret && c) d.dueb[ndb] = rb;
+            if (!ret && c) ++ndb;
         }
         __syncthreads();
-        if (s_done) return;
-    }
-    // list the due chunks of the new window [S, E)
-    const uint64_t S = s_S, E = s_E;
-    const uint64_t bS = S / W, bL = (E - 1) / W;
-    const uint64_t pr = rs->ret_b;
-    if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
-        const uint32_t rb = (uint32_t)(pr % R);
-        const uint32_t nc = d.nal[rb];
-        const uint64_t tail = s_tail;
-        for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-            uint32_t* e = &d.btab[(size_t)rb * NCH + ci];
-            d.fring[(tail + ci) % NCH] = *e;
-            *e = EMPTY;
+        if (straddle && tid == 0) B.mn[bL % R] = UINT64_MAX;  // k_gather's carry min and k_count restore it
+        // exact min beyond the window: the first non-empty bucket in (bL, bS + R)
+        // (the window's own slots lie outside that range; the spent slot is empty)
+        uint64_t first = UINT64_MAX;
+        const uint32_t span = (uint32_t)(bL - bS);
+        for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
+            const uint64_t b = bL + o;
+            const uint32_t rb = (uint32_t)(b % R);
+            if (rb == s_spent) continue;
+            if (B.cnt[rb] > B.tomb[rb]) first = b < first ? b : first;
         }
-        __syncthreads();
+        first = block_min(first, s16);  // barriers inside
         if (tid == 0) {
-            s_tail = tail + nc;
-            s_spent = rb;
-            reset_bucket(d, rb);
+            rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : B.mn[first % R];
+            rs->bS = bS;
+            rs->bL = bL;
+            rs->ndue = nd;
+            rs->ndueb = ndb;
+            rs->ret_b = straddle ? bL : UINT64_MAX;
         }
-        __syncthreads();
     }
-    // Fully due buckets keep their tables until the next plan (k_scatter of
-    // this round still writes the events k_count counted into them).
-    uint64_t nd = 0, ndb = 0;
-    const bool straddle = E < (bL + 1) * W;
-    for (uint64_t b = bS; b <= bL; ++b) {
-        const uint32_t rb = (uint32_t)(b % R);
-        const uint32_t c = d.bcnt[rb], nc = d.nal[rb];
-        const bool ret = straddle && b == bL;
-        const uint32_t* tab = d.btab + (size_t)rb * NCH;
-        for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-            const uint32_t left = c - (ci << CH_SHIFT);
-            const uint32_t n = left < CH ? left : CH;
-            d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
-        }
-        nd += nc;
-        if (tid == 0) {
-            if (ret) d.bmin[rb] = UINT64_MAX;  // k_gather's carry min and k_count restore it
-            else if (c) d.dueb[ndb] = rb;
-        }
-        if (!ret && c) ++ndb;
+    __syncthreads();
+    for (uint32_t rb = tid; rb < R; rb += PL_T) {
+        d.bcnt[rb] = B.cnt[rb];
+        d.btomb[rb] = B.tomb[rb];
+        d.nal[rb] = B.nal[rb];
+        d.bmin[rb] = B.mn[rb];
     }
-    // exact min beyond the window: the first non-empty bucket in (bL, bS + R)
-    // (the window's own slots lie outside that range; the spent slot is empty)
-    uint64_t first = UINT64_MAX;
-    const uint32_t span = (uint32_t)(bL - bS);
-    for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
-        const uint64_t b = bL + o;
-        const uint32_t rb = (uint32_t)(b % R);
-        if (rb == s_spent) continue;
-        if (d.bcnt[rb] > d.btomb[rb]) first = b < first ? b : first;
-    }
-    first = block_min(first, s16);
     if (tid == 0) {
-        rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : d.bmin[first % R];
-        rs->bS = bS;
-        rs->bL = bL;
-        rs->ndue = nd;
-        rs->ndueb = ndb;
-        rs->ret_b = straddle ? bL : UINT64_MAX;
         rs->fl_head = s_head;
         rs->fl_tail = s_tail;
     }
@@ -1525,6 +1744,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.extras, P * K2_T * XCAP);
     ALLOC(D.rcnt, P);
     ALLOC(D.loc, P * D.ECAP);
+    ALLOC(D.sends, P * D.ECAP);
     ALLOC(D.c1min, D.G1);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
@@ -1542,6 +1762,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, P * 8);
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
@@ -1882,6 +2103,17 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
         return SG_ERR_INVAL;
     }
     return enqueue_insert_plan(e, recv, 1);
+}
+
+int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
+    if (!e) return SG_ERR_INVAL;
+    const uint64_t n = e->d.stamps ? (uint64_t)e->d.P * 8 : 0;
+    if (n_out) *n_out = n;
+    if (out && capacity && n) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d.stamps, (n < capacity ? n : capacity) * 8, hipMemcpyDeviceToHost));
+    }
+    return SG_OK;
 }
 
 int sg_engine_set_timing(sg_engine* e, int enabled) {

@@ -127,6 +127,15 @@ class Engine:
         L.check(L.lib().sg_engine_geometry(self.h, C.byref(g)))
         return g.as_dict()
 
+    def stamps(self) -> np.ndarray:
+        """[P, 8] k_proc phase stamps of the last round (SG_STAMPS=1), or empty."""
+        n = C.c_uint64()
+        L.check(L.lib().sg_engine_stamps(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.uint64)
+        if n.value:
+            L.check(L.lib().sg_engine_stamps(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out.reshape(-1, 8)
+
     # ---------------------------------------------------------- multi shard
     def exchange_rows(self) -> int:
         r = C.c_uint64()
