@@ -50,6 +50,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "shadowgpu.h"
@@ -73,8 +74,6 @@ constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
-constexpr uint32_t SRCMAX = PMAX + MAXG;              // k_count / k_scatter sources
-constexpr uint32_t SRC_PER = (SRCMAX + K3_T - 1) / K3_T;
 constexpr uint32_t RETAINED = 1u << 31;
 // exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
 constexpr int HDR = 2;
@@ -115,9 +114,9 @@ struct PairRec {
 struct HostState {
     uint32_t rng;     // host Random (host.c:176)
     uint32_t pad;
-    uint64_t evc;     // eventIDCounter (host.c:397-400)
     uint64_t pops;
     uint64_t digest;
+    uint64_t evc;     // eventIDCounter (host.c:397-400); k_proc writes it last (phase C)
 };
 
 struct RoundState {
@@ -147,6 +146,7 @@ struct RoundState {
 struct Dev {
     uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
     uint32_t R, NCH, HP, hp_shift, P, CAPP, ECAP, G1, G3;
+    uint32_t EVL, ev_off, proc_lds;  // k_proc: due events sorted in LDS, their offset, dynamic LDS bytes
     uint64_t W;
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
@@ -161,7 +161,8 @@ struct Dev {
     uint64_t* bmin;           // [R] min live time
     uint32_t* fring;          // [NCH] free chunk ring
     uint32_t* nal;            // [R] chunks allocated to each bucket
-    uint32_t* wbase;          // [G3][R] k_count's reserved base per (workgroup, bucket)
+    uint32_t* wbase;          // [P + G3][R] reserved base per (source, bucket): rows < P
+                              // partitions (k_proc), then k_count's received-block split
     DueEnt* due;              // [NCH]
     uint32_t* dueb;           // [R] ring slots of the listed non-retained buckets
     // partitions
@@ -231,34 +232,51 @@ __device__ __forceinline__ uint64_t digest_mix(uint64_t pos, uint64_t t, uint32_
 // and the chosen host's info record.  Weights rule: the first i with
 // x <= wt[i] (non-decreasing thresholds); the uniform-position guess and its
 // two neighbours are loaded together, which settles near-uniform weights in
-// one round trip, and anything else is bisected.
-__device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
+// one round trip, and anything else is bisected.  Split in three steps
+// (guess, probe loads, resolve) so a lane can have several draws' loads in
+// flight at once.
+struct Probe {
+    HostInfo cur, prev, next;
+};
+__device__ __forceinline__ uint32_t dst_guess(const Dev& d, int32_t x) {
     const uint32_t N = d.N;
-    const HostInfo* w = d.hinfo;
     if (d.dst_rule == SG_DST_UNIFORM_FLOOR) {
         double r = (double)x / 2147483647.0;
         double f = floor(r * (double)N);
         uint32_t dd = (uint32_t)f;
-        dd = dd >= N ? N - 1 : dd;
-        info = w[dd];
-        return dd;
+        return dd >= N ? N - 1 : dd;
     }
     uint32_t g = (uint32_t)(((uint64_t)(uint32_t)x * N) >> 31);
-    if (g >= N) g = N - 1;
-    const HostInfo cur = w[g];
-    const HostInfo prev = w[g > 0 ? g - 1 : 0];
-    const HostInfo next = w[g + 1 < N ? g + 1 : N - 1];
+    return g >= N ? N - 1 : g;
+}
+__device__ __forceinline__ Probe dst_probe(const Dev& d, uint32_t g) {
+    Probe pb;
+    pb.cur = d.hinfo[g];
+    if (d.dst_rule != SG_DST_UNIFORM_FLOOR) {
+        pb.prev = d.hinfo[g > 0 ? g - 1 : 0];
+        pb.next = d.hinfo[g + 1 < d.N ? g + 1 : d.N - 1];
+    }
+    return pb;
+}
+__device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_t g, const Probe& pb,
+                                                HostInfo& info) {
+    if (d.dst_rule == SG_DST_UNIFORM_FLOOR) {
+        info = pb.cur;
+        return g;
+    }
+    const uint32_t N = d.N;
+    const HostInfo* w = d.hinfo;
     uint32_t lo, hi;
-    if (x <= cur.wt) {
-        if (g == 0 || x > prev.wt) {
-            info = cur;
+    if (x <= pb.cur.wt) {
+        if (g == 0 || x > pb.prev.wt) {
+            info = pb.cur;
             return g;
         }
         lo = 0;
         hi = g - 1;  // x <= wt[g-1]: the answer is in [0, g-1]
     } else {
-        if (g + 1 < N && x <= next.wt) {
-            info = next;
+        if (g + 1 < N && x <= pb.next.wt) {
+            info = pb.next;
             return g + 1;
         }
         if (g + 1 >= N || x > w[N - 1].wt) return N;
@@ -271,6 +289,10 @@ __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo
     }
     info = w[lo];
     return lo;
+}
+__device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
+    const uint32_t g = dst_guess(d, x);
+    return dst_resolve(d, x, g, dst_probe(d, g), info);
 }
 
 __device__ __forceinline__ uint32_t owner_of(const Dev& d, uint32_t h) {
@@ -544,8 +566,9 @@ struct ProcShared {
     uint32_t peer[MAXG];
 };
 
-// Stage one new event (time already bumped) for k_count (this shard's hosts) or
-// for the outbox (other shards).
+// Stage one new event (time already bumped) for the calendar (this shard's
+// hosts; k_proc counts them by bucket after phase C) or for the outbox (other
+// shards).
 __device__ __forceinline__ void stage_event(const Dev& d, uint64_t S, uint32_t part, ProcShared& sh,
                                             Acc& a, uint32_t dst, uint64_t tn, uint64_t key) {
     const uint32_t dl = dst - d.lo;
@@ -570,8 +593,7 @@ __device__ __forceinline__ void stage_event(const Dev& d, uint64_t S, uint32_t p
 
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
 // Self events that fall inside the window go to the lane's same-round list
-// through `append`; everything else is staged for k_count (this shard) or for
-// the outbox (other shards).
+// through `append`; everything else is staged.
 template <class Append>
 __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t E, uint32_t part,
                                               HostCtx& c, Acc& a, uint64_t bt, uint64_t bk,
@@ -634,35 +656,62 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
     }
 }
 
+// Sort a host's due segment by (time, key): event_compare with equal dst.
+// Selection sort; segments are short (a few events per host per window).
+__device__ __forceinline__ void sort_segment(Rec* seg, uint32_t cnt) {
+    for (uint32_t i = 0; i + 1 < cnt; ++i) {
+        Best b{UINT64_MAX, 0, i};
+        for (uint32_t k = i; k < cnt; ++k) {
+            const Rec r = seg[k];
+            best_take(b, r.a & M52, r.k, k);
+        }
+        if (b.slot != i) {
+            const Rec t = seg[i];
+            seg[i] = seg[b.slot];
+            seg[b.slot] = t;
+        }
+    }
+}
+
 // One workgroup per partition of HP hosts.
-//   sort     the partition's due events by host (LDS counting sort) and list
-//            the active hosts;
+//   sort     the partition's due events by host (LDS counting sort into an LDS
+//            image of the events when they fit, else into part2) and list the
+//            active hosts;
 //   phase A  per active host: pop order (event_compare), trace digest, and the
 //            host's rand_r draws, which are pure arithmetic: one record
 //            {time, x, c} per send with a destination.  A host that could
 //            create an event for itself inside this window (its earliest event
 //            + its self-path delay < barrier) runs the whole sequential body
 //            here instead (same-round self events, host_single.c:237-267);
-//   phase B  one lane per send, balanced across the workgroup: destination,
+//   phase B  one lane per send, two sends in flight per lane: destination,
 //            path record, reliability test, delivery time;
 //   phase C  per active host, in send order: srcHostEventID, endTime drop,
-//            barrier bump, staging.
-constexpr uint32_t HPT = HPMAX / K2_T;  // active hosts per lane, at most
+//            barrier bump, staging;
+//   count    the staged local events by calendar bucket (LDS bins over the
+//            dead event image) and one reservation per (partition, bucket).
+constexpr uint32_t HPT = HPMAX / K2_T;     // active hosts per lane, at most
+constexpr uint32_t EVLMAX = 6144;          // due events sorted in LDS, at most
+constexpr uint32_t EPT = EVLMAX / K2_T;    // of them per lane
 
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
-    const RoundState* rs = d.rs;
+    RoundState* rs = d.rs;
     if (rs->done | rs->phase) return;
-    __shared__ uint32_t s_n[HPMAX];    // events per host
-    __shared__ uint32_t s_c[HPMAX];    // start offset, then end (scatter cursor)
-    __shared__ uint16_t s_act[HPMAX];  // active hosts, ascending
-    __shared__ uint32_t s_vh[HPMAX];   // vertex of active host j
+    extern __shared__ __align__(16) unsigned char dyn[];
+    const uint32_t HP = d.HP, R = d.R;
+    uint32_t* s_n = (uint32_t*)dyn;             // [HP] events per host
+    uint32_t* s_c = s_n + HP;                   // [HP] start offset, then end (scatter cursor)
+    uint32_t* s_vh = s_c + HP;                  // [HP] vertex of active host j
+    uint16_t* s_act = (uint16_t*)(s_vh + HP);   // [HP] active hosts, ascending
+    Rec* s_ev = (Rec*)(dyn + d.ev_off);         // [EVL] due events grouped by host
+    uint32_t* s_bc = (uint32_t*)(dyn + d.ev_off);  // [R] after phase A: staged events per bucket
+    uint32_t* s_bm = s_bc + R;                     // [R] their min time offset in the bucket
     __shared__ uint32_t s_nsend;
     __shared__ int32_t s_last;         // last weight threshold: x above it selects no host
     __shared__ ProcShared sh;
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
     const uint64_t S = rs->S, E = rs->E;
-    const uint32_t p = blockIdx.x, HP = d.HP;
+    const uint32_t p = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * 8 : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
@@ -674,15 +723,38 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         sh.nrem = 0;
         s_nsend = 0;
         s_last = d.dst_rule == SG_DST_WEIGHTS ? d.hinfo[d.N - 1].wt : INT32_MAX;
+        if (p == 0) {  // k_scatter takes this step's staged local events
+            rs->ins_local = 1;
+            rs->ins_S = S;
+        }
     }
     if (tid < MAXG) sh.peer[tid] = 0;
-    __syncthreads();
     const Rec* part = d.part + (size_t)p * d.CAPP;
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
-    for (uint32_t i = tid; i < n; i += K2_T) {
-        const uint32_t hl = (uint32_t)(part[i].a >> 52);
-        if (hl < HP) atomicAdd(&s_n[hl], 1u);
-        else flag(d, OV_BUG);
+    const bool in_lds = n <= d.EVL;
+    Rec rr[EPT];
+    if (in_lds) {
+#pragma unroll
+        for (uint32_t q = 0; q < EPT; ++q) {
+            const uint32_t i = tid + q * K2_T;
+            rr[q] = i < n ? part[i] : Rec{0, 0};
+        }
+    }
+    __syncthreads();
+    if (in_lds) {
+#pragma unroll
+        for (uint32_t q = 0; q < EPT; ++q) {
+            if (tid + q * K2_T >= n) continue;
+            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
+            if (hl < HP) atomicAdd(&s_n[hl], 1u);
+            else flag(d, OV_BUG);
+        }
+    } else {
+        for (uint32_t i = tid; i < n; i += K2_T) {
+            const uint32_t hl = (uint32_t)(part[i].a >> 52);
+            if (hl < HP) atomicAdd(&s_n[hl], 1u);
+            else flag(d, OV_BUG);
+        }
     }
     __syncthreads();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
@@ -710,14 +782,25 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint32_t nact = (uint32_t)tot;
     __syncthreads();
     if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
-    for (uint32_t i = tid; i < n; i += K2_T) {
-        const Rec r = part[i];
-        const uint32_t hl = (uint32_t)(r.a >> 52);
-        if (hl >= HP) continue;
-        const uint32_t pos = atomicAdd(&s_c[hl], 1u);
-        if (pos < n) part2[pos] = r;
+    if (in_lds) {
+#pragma unroll
+        for (uint32_t q = 0; q < EPT; ++q) {
+            if (tid + q * K2_T >= n) continue;
+            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
+            if (hl >= HP) continue;
+            const uint32_t pos = atomicAdd(&s_c[hl], 1u);
+            if (pos < n) s_ev[pos] = rr[q];
+        }
+    } else {
+        for (uint32_t i = tid; i < n; i += K2_T) {
+            const Rec r = part[i];
+            const uint32_t hl = (uint32_t)(r.a >> 52);
+            if (hl >= HP) continue;
+            const uint32_t pos = atomicAdd(&s_c[hl], 1u);
+            if (pos < n) part2[pos] = r;
+        }
     }
-    __syncthreads();  // part2 is read back by other lanes of this workgroup
+    __syncthreads();  // the grouped events are read back by other lanes
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
     Acc a;
@@ -730,155 +813,172 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     Rec* snd = d.sends + (size_t)p * d.ECAP;
     const uint32_t hbase = d.lo + p * HP;
     const int32_t last = s_last;
-    uint32_t sbase[HPT], scnt[HPT];  // this lane's hosts' send ranges (UINT32_MAX: sequential)
+    uint32_t sbase[HPT], scnt[HPT];  // sbase UINT32_MAX: no phase C (sequential or idle)
+    uint64_t evc_r[HPT];
 
-    // ---- phase A
+    // ---- phase A (segments in LDS or in part2: two instantiations)
+    auto phase_a = [&](auto seg_in_lds) {
+        Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
 #pragma unroll
-    for (uint32_t q = 0; q < HPT; ++q) {
-        sbase[q] = UINT32_MAX;
-        scnt[q] = 0;
-        const uint32_t j = tid + q * K2_T;
-        if (j >= nact) continue;
-        const uint32_t hl = s_act[j];
-        const uint32_t cnt = s_n[hl];
-        Rec* seg = part2 + (s_c[hl] - cnt);
-        HostCtx c;
-        c.h = hbase + hl;
-        const uint32_t lh = c.h - d.lo;
-        if (lh >= d.L) {
-            a.overflow = true;
-            continue;
-        }
-        c.s = d.hs[lh];
-        c.vh = d.hinfo[c.h].vertex;
-        s_vh[j] = c.vh;
-        ++a.ctr[C_ACTIVE];
-        // pop order: selection sort of the (small) segment by (time, key)
-        for (uint32_t i = 0; i + 1 < cnt; ++i) {
-            Best b{UINT64_MAX, 0, i};
-            for (uint32_t k = i; k < cnt; ++k) {
-                const Rec r = seg[k];
-                best_take(b, r.a & M52, r.k, k);
+        for (uint32_t q = 0; q < HPT; ++q) {
+            sbase[q] = UINT32_MAX;
+            scnt[q] = 0;
+            const uint32_t j = tid + q * K2_T;
+            if (j >= nact) continue;
+            const uint32_t hl = s_act[j];
+            const uint32_t cnt = s_n[hl];
+            Rec* seg = segs + (s_c[hl] - cnt);
+            HostCtx c;
+            c.h = hbase + hl;
+            const uint32_t lh = c.h - d.lo;
+            if (lh >= d.L) {
+                a.overflow = true;
+                continue;
             }
-            if (b.slot != i) {
-                const Rec t = seg[i];
-                seg[i] = seg[b.slot];
-                seg[b.slot] = t;
-            }
-        }
-        const uint64_t self_delay = d.pairs[(size_t)c.vh * d.V + c.vh].delay;
-        if (S + (seg[0].a & M52) + self_delay < E) {
-            // sequential body: a self event may land inside this window
-            uint32_t nx = 0;
-            auto append = [&](uint64_t trel, uint64_t key) -> bool {
-                if (nx >= XCAP) return false;
-                xs[nx++] = Rec{trel, key};
-                return true;
-            };
-            uint32_t ns = cnt, i0 = 0;
-            for (;;) {
-                Best b{UINT64_MAX, 0, UINT32_MAX};
-                for (uint32_t i = i0; i < ns; ++i) {
-                    const Rec r = seg[i];
-                    best_take(b, r.a & M52, r.k, i);
+            c.s = d.hs[lh];
+            c.vh = d.hinfo[c.h].vertex;
+            s_vh[j] = c.vh;
+            ++a.ctr[C_ACTIVE];
+            sort_segment(seg, cnt);  // pop order
+            const uint64_t self_delay = d.pairs[(size_t)c.vh * d.V + c.vh].delay;
+            if (S + (seg[0].a & M52) + self_delay < E) {
+                // sequential body: a self event may land inside this window
+                uint32_t nx = 0;
+                auto append = [&](uint64_t trel, uint64_t key) -> bool {
+                    if (nx >= XCAP) return false;
+                    xs[nx++] = Rec{trel, key};
+                    return true;
+                };
+                uint32_t ns = cnt, i0 = 0;
+                for (;;) {
+                    Best b{UINT64_MAX, 0, UINT32_MAX};
+                    for (uint32_t i = i0; i < ns; ++i) {
+                        const Rec r = seg[i];
+                        best_take(b, r.a & M52, r.k, i);
+                    }
+                    for (uint32_t i = 0; i < nx; ++i) {
+                        const Rec r = xs[i];
+                        best_take(b, r.a, r.k, 0x80000000u | i);
+                    }
+                    if (b.slot == UINT32_MAX) break;
+                    if (b.slot & 0x80000000u) {
+                        const uint32_t i = b.slot & 0x7FFFFFFFu;
+                        --nx;
+                        if (i != nx) xs[i] = xs[nx];
+                    } else {
+                        --ns;
+                        if (b.slot != ns) seg[b.slot] = seg[ns];
+                    }
+                    execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
                 }
-                for (uint32_t i = 0; i < nx; ++i) {
-                    const Rec r = xs[i];
-                    best_take(b, r.a, r.k, 0x80000000u | i);
-                }
-                if (b.slot == UINT32_MAX) break;
-                if (b.slot & 0x80000000u) {
-                    const uint32_t i = b.slot & 0x7FFFFFFFu;
-                    --nx;
-                    if (i != nx) xs[i] = xs[nx];
-                } else {
-                    --ns;
-                    if (b.slot != ns) seg[b.slot] = seg[ns];
-                }
-                execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
+                d.hs[lh] = c.s;
+                continue;
             }
-            d.hs[lh] = c.s;
-            continue;
-        }
-        // count this host's sends (arithmetic only), reserve, then record them
-        uint32_t r = c.s.rng, ns = 0;
-        for (uint32_t i = 0; i < cnt; ++i) {
-            const uint64_t bk = seg[i].k;
-            const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
-            const uint32_t nsend = boot ? d.load : 1u;
-            for (uint32_t m = 0; m < nsend; ++m) {
-                const int32_t x = dev_rand_r(r);
-                if (x > last) continue;
-                (void)dev_rand_r(r);
-                ++ns;
-            }
-        }
-        const uint32_t base = atomicAdd(&s_nsend, ns);
-        if (base + ns > d.ECAP) {
-            a.overflow = true;
-            continue;
-        }
-        sbase[q] = base;
-        scnt[q] = ns;
-        uint32_t k = base;
-        for (uint32_t i = 0; i < cnt; ++i) {
-            const Rec ev = seg[i];
-            const uint64_t trel = ev.a & M52, bt = S + trel;
-            const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
-            const uint64_t bseq = ev.k & SEQ_MASK;
-            c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
-            if (d.trace) {
-                const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
-                if (ts < d.trace_cap) {
-                    sg_trace_rec tr;
-                    tr.time = bt;
-                    tr.seq = bseq;
-                    tr.host = c.h;
-                    tr.src = bsrc;
-                    tr.pos = c.s.pops;
-                    d.trace[ts] = tr;
-                } else {
-                    a.overflow = true;
+            // count this host's sends (arithmetic only), reserve, then record them
+            uint32_t r = c.s.rng, ns = 0;
+            for (uint32_t i = 0; i < cnt; ++i) {
+                const uint64_t bk = seg[i].k;
+                const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
+                const uint32_t nsend = boot ? d.load : 1u;
+                for (uint32_t m = 0; m < nsend; ++m) {
+                    const int32_t x = dev_rand_r(r);
+                    if (x > last) continue;
+                    (void)dev_rand_r(r);
+                    ++ns;
                 }
             }
-            ++c.s.pops;
-            ++a.ctr[C_POPS];
-            const bool boot = (bsrc == c.h) & (bseq == 0);
-            a.ctr[C_BOOTS] += boot;
-            const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
-            for (uint32_t m = 0; m < nsend; ++m) {
-                const int32_t x = dev_rand_r(c.s.rng);
-                if (x > last) {  // no host selected (test_phold.c:176-177)
-                    ++a.ctr[C_NULL];
-                    continue;
-                }
-                const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
-                ++a.ctr[C_SENDS];
-                snd[k++] = Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
+            const uint32_t base = atomicAdd(&s_nsend, ns);
+            if (base + ns > d.ECAP) {
+                a.overflow = true;
+                continue;
             }
+            sbase[q] = base;
+            scnt[q] = ns;
+            uint32_t k = base;
+            for (uint32_t i = 0; i < cnt; ++i) {
+                const Rec ev = seg[i];
+                const uint64_t trel = ev.a & M52, bt = S + trel;
+                const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
+                const uint64_t bseq = ev.k & SEQ_MASK;
+                c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
+                if (d.trace) {
+                    const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
+                    if (ts < d.trace_cap) {
+                        sg_trace_rec tr;
+                        tr.time = bt;
+                        tr.seq = bseq;
+                        tr.host = c.h;
+                        tr.src = bsrc;
+                        tr.pos = c.s.pops;
+                        d.trace[ts] = tr;
+                    } else {
+                        a.overflow = true;
+                    }
+                }
+                ++c.s.pops;
+                ++a.ctr[C_POPS];
+                const bool boot = (bsrc == c.h) & (bseq == 0);
+                a.ctr[C_BOOTS] += boot;
+                const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+                for (uint32_t m = 0; m < nsend; ++m) {
+                    const int32_t x = dev_rand_r(c.s.rng);
+                    if (x > last) {  // no host selected (test_phold.c:176-177)
+                        ++a.ctr[C_NULL];
+                        continue;
+                    }
+                    const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
+                    ++a.ctr[C_SENDS];
+                    snd[k++] = Rec{((uint64_t)j << 52) | trel,
+                                   (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
+                }
+            }
+            // {rng, pops, digest} now; evc after phase C
+            HostState* hp = d.hs + lh;
+            reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
+            hp->digest = c.s.digest;
+            evc_r[q] = c.s.evc;
         }
-        HostState* hp = d.hs + lh;
-        hp->rng = c.s.rng;
-        hp->pops = c.s.pops;
-        hp->digest = c.s.digest;
-    }
+    };
+    if (in_lds) phase_a(std::true_type{});
+    else phase_a(std::false_type{});
     __syncthreads();
     if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- phase B: one lane per send
+    // the event image is dead: its LDS becomes the bucket bins
+    for (uint32_t rb = tid; rb < R; rb += K2_T) {
+        s_bc[rb] = 0;
+        s_bm[rb] = UINT32_MAX;
+    }
+    // ---- phase B: one lane per send, two in flight
     const uint32_t nsend = s_nsend < d.ECAP ? s_nsend : d.ECAP;
-    for (uint32_t i = tid; i < nsend; i += K2_T) {
-        const Rec r = snd[i];
-        const uint32_t j = (uint32_t)(r.a >> 52);
-        const uint64_t bt = S + (r.a & M52);
-        const int32_t x = (int32_t)(uint32_t)r.k, ch = (int32_t)(uint32_t)(r.k >> 32);
-        HostInfo di;
-        const uint32_t dst = choose_dst(d, x, di);
-        const PairRec pr = d.pairs[(size_t)s_vh[j] * d.V + di.vertex];
-        a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
-        const bool keep = bt < d.bootstrap_end || ch <= pr.keep;  // worker.c:268-273
-        const uint64_t tn = bt + pr.delay;                        // worker.c:275-277
-        snd[i] = Rec{((uint64_t)keep << 63) | (tn - S), dst};
+    for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
+        const uint32_t i1 = i0 + K2_T;
+        const bool v1 = i1 < nsend;
+        const Rec r0 = snd[i0];
+        const Rec r1 = v1 ? snd[i1] : r0;
+        const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
+        const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
+        const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
+        HostInfo di0, di1;
+        const uint32_t dst0 = dst_resolve(d, x0, g0, pb0, di0);
+        const uint32_t dst1 = dst_resolve(d, x1, g1, pb1, di1);
+        const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
+        const PairRec pr0 = d.pairs[(size_t)s_vh[j0] * d.V + di0.vertex];
+        const PairRec pr1 = d.pairs[(size_t)s_vh[j1] * d.V + di1.vertex];
+        {
+            const uint64_t bt = S + (r0.a & M52);
+            const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
+            a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
+            const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
+            snd[i0] = Rec{((uint64_t)keep << 63) | (bt + pr0.delay - S), dst0};  // worker.c:275-277
+        }
+        if (v1) {
+            const uint64_t bt = S + (r1.a & M52);
+            const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
+            a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
+            const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
+            snd[i1] = Rec{((uint64_t)keep << 63) | (bt + pr1.delay - S), dst1};
+        }
     }
     __syncthreads();
     if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
@@ -889,8 +989,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if (sbase[q] == UINT32_MAX) continue;
         const uint32_t j = tid + q * K2_T;
         const uint32_t h = hbase + s_act[j];
-        HostState* hp = d.hs + (h - d.lo);
-        uint64_t evc = hp->evc;
+        uint64_t evc = evc_r[q];
         for (uint32_t k = sbase[q]; k < sbase[q] + scnt[q]; ++k) {
             const Rec r = snd[k];
             if (!(r.a >> 63)) {
@@ -911,8 +1010,30 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq);
         }
-        hp->evc = evc;
+        d.hs[h - d.lo].evc = evc;
     }
+    __syncthreads();  // staging done: sh.nloc is final, loc[] visible to the workgroup
+
+    // ---- count: staged local events by bucket, then one reservation per bucket
+    const uint64_t W = d.W, bS = rs->bS;
+    const uint32_t bSr = (uint32_t)(bS % R);
+    const uint32_t nl = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
+    const Rec* lp = d.loc + (size_t)p * d.ECAP;
+    bool horizon = false;
+    for (uint32_t i = tid; i < nl; i += K2_T) {
+        const Rec r = lp[i];
+        const uint64_t t = S + (r.a & M40);
+        const uint64_t b = t / W;
+        if (b < bS || b - bS >= R) {
+            horizon = true;
+            continue;
+        }
+        uint32_t rb = bSr + (uint32_t)(b - bS);
+        rb = rb >= R ? rb - R : rb;
+        atomicAdd(&s_bc[rb], 1u);
+        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
+    }
+    if (horizon) flag(d, OV_HORIZON);
 
     // workgroup partials: cumulative counters, this round's two minima
     const int lane = tid & 63, wid = tid >> 6;
@@ -927,6 +1048,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
+    uint32_t* wb = d.wbase + (size_t)p * R;
+    for (uint32_t rb = tid; rb < R; rb += K2_T) {
+        const uint32_t c = s_bc[rb];
+        if (!c) continue;
+        const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
+        wb[rb] = atomicAdd(&d.bcnt[rb], c);
+        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
+    }
     if (tid < NCTR + 2) {
         const int i = tid;
         uint64_t r = s_red[0][i];
@@ -939,7 +1068,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
-        d.rcnt[p] = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
+        d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
     if (d.G > 1 && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
@@ -952,90 +1081,67 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 }
 
 // --------------------------------------------------------------- insert ----
-// Staged events (process steps) and received exchange blocks (multi-shard)
-// → buckets.  The sources' events are split evenly over the grid; k_count and
-// k_scatter compute the same split.
+// Events → calendar buckets.  Local events were counted and reserved per
+// (partition, bucket) by k_proc; received exchange blocks (multi-shard) are
+// counted here by k_count, split evenly over its grid.  k_scatter writes both
+// into the chunks k_plan allocated: one workgroup per partition, then the
+// received-block split (wbase rows P + workgroup).
 
-// Event `idx` of the concatenated sources: t (absolute), key, dst_local.
-__device__ __forceinline__ bool src_event(const Dev& d, const int64_t* recv, const uint32_t* s_off,
-                                          uint32_t nsrc, uint64_t S, uint32_t idx, uint64_t& t,
-                                          uint64_t& k, uint32_t& dl) {
-    uint32_t lo = 0, hi = nsrc - 1;  // last source with s_off <= idx
+// Exclusive offsets of the received blocks' event counts (own block: 0).
+__device__ uint64_t recv_offsets(const Dev& d, const int64_t* recv, uint32_t* s_off, uint64_t* s16,
+                                 bool check) {
+    const uint32_t s = threadIdx.x;
+    uint64_t c = 0;
+    if (s < d.G && s != d.g) {
+        const uint64_t n = (uint64_t)recv[(size_t)s * d.xrows * 3 + H_N];
+        if (n <= d.xcap) c = n;
+        else if (check) flag(d, OV_XCHG);
+    }
+    uint64_t total;
+    const uint64_t run = block_excl_scan(c, s16, &total);
+    if (s < d.G) s_off[s] = (uint32_t)run;
+    __syncthreads();
+    return total;
+}
+
+// Received event `idx` of the concatenated blocks: t, key, dst_local.
+__device__ __forceinline__ bool recv_event(const Dev& d, const int64_t* recv, const uint32_t* s_off,
+                                           uint32_t idx, uint64_t& t, uint64_t& k, uint32_t& dl) {
+    uint32_t lo = 0, hi = d.G - 1;  // last block with s_off <= idx
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (s_off[mid] <= idx) lo = mid; else hi = mid - 1;
     }
-    const uint32_t off = idx - s_off[lo];
-    if (lo < d.P) {
-        const Rec r = d.loc[(size_t)lo * d.ECAP + off];
-        t = S + (r.a & M40);
-        k = r.k;
-        dl = (uint32_t)(r.a >> 40);
-        return dl < d.L;
-    }
-    const int64_t* row = recv + ((size_t)(lo - d.P) * d.xrows + HDR + off) * 3;
+    const int64_t* row = recv + ((size_t)lo * d.xrows + HDR + (idx - s_off[lo])) * 3;
     t = (uint64_t)row[0];
     k = (uint64_t)row[1];
     dl = (uint32_t)row[2] - d.lo;
     return dl < d.L;
 }
 
-// Exclusive offsets of the sources' event counts into s_off; returns the total.
-__device__ uint64_t src_offsets(const Dev& d, const int64_t* recv, bool local, uint32_t nsrc,
-                                uint32_t* s_off, uint64_t* s16, bool check) {
-    uint32_t cs[SRC_PER];
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < SRC_PER; ++j) {
-        const uint32_t s = threadIdx.x * SRC_PER + j;
-        uint32_t c = 0;
-        if (s < d.P) {
-            c = local ? d.rcnt[s] : 0;
-        } else if (s < nsrc && s - d.P != d.g) {
-            const uint64_t n = (uint64_t)recv[(size_t)(s - d.P) * d.xrows * 3 + H_N];
-            if (n <= d.xcap) c = (uint32_t)n;
-            else if (check) flag(d, OV_XCHG);
-        }
-        cs[j] = c;
-        mine += c;
-    }
-    uint64_t total;
-    uint64_t run = block_excl_scan(mine, s16, &total);
-#pragma unroll
-    for (uint32_t j = 0; j < SRC_PER; ++j) {
-        const uint32_t s = threadIdx.x * SRC_PER + j;
-        if (s < nsrc) s_off[s] = (uint32_t)run;
-        run += cs[j];
-    }
-    __syncthreads();
-    return total;
-}
-
+// Multi-shard only: received events → bucket counts, one reservation per
+// (workgroup, bucket).  Every step runs it; it records whether this step's
+// k_scatter also takes the staged local events (process steps only).
 __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     RoundState* rs = d.rs;
     if (rs->done) return;
-    __shared__ uint32_t s_off[SRCMAX];
+    __shared__ uint32_t s_off[MAXG];
     __shared__ uint32_t s_bc[RMAX];  // per bucket: events of this workgroup
     __shared__ uint32_t s_bm[RMAX];  // per bucket: min time offset within the bucket
     __shared__ uint64_t s16[16];
-    const bool local = rs->phase == 0;
-    const uint64_t S = rs->S, W = d.W, bS = rs->bS;
+    const uint64_t W = d.W, bS = rs->bS;
     const uint32_t R = d.R;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        rs->ins_local = local;
-        rs->ins_S = S;
-    }
-    const uint32_t nsrc = d.P + (recv ? d.G : 0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) rs->ins_local = rs->phase == 0;
     for (uint32_t b = threadIdx.x; b < R; b += K3_T) {
         s_bc[b] = 0;
         s_bm[b] = UINT32_MAX;
     }
-    const uint64_t total = src_offsets(d, recv, local, nsrc, s_off, s16, true);
+    const uint64_t total = recv_offsets(d, recv, s_off, s16, true);
     const uint64_t lo = total * blockIdx.x / gridDim.x, hi = total * (blockIdx.x + 1) / gridDim.x;
     for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
         uint64_t t, k;
         uint32_t dl;
-        if (!src_event(d, recv, s_off, nsrc, S, (uint32_t)idx, t, k, dl)) {
+        if (!recv_event(d, recv, s_off, (uint32_t)idx, t, k, dl)) {
             flag(d, OV_XCHG);
             continue;
         }
@@ -1049,7 +1155,7 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
         atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
     }
     __syncthreads();
-    uint32_t* wb = d.wbase + (size_t)blockIdx.x * R;
+    uint32_t* wb = d.wbase + (size_t)(d.P + blockIdx.x) * R;
     for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) {
         const uint32_t c = s_bc[rb];
         if (!c) continue;
@@ -1059,31 +1165,47 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     }
 }
 
+// One event into its reserved slot of bucket t / W.
+__device__ __forceinline__ void place_event(const Dev& d, uint32_t* s_cur, uint64_t t, uint64_t k, uint32_t dl) {
+    const uint64_t b = t / d.W;
+    const uint32_t rb = (uint32_t)(b % d.R);
+    const uint32_t pos = atomicAdd(&s_cur[rb], 1u);
+    if ((pos >> CH_SHIFT) >= d.nal[rb]) return;  // beyond the pool (flagged by k_plan)
+    const uint32_t id = d.btab[(size_t)rb * d.NCH + (pos >> CH_SHIFT)];
+    if (id >= d.NCH) return;
+    d.pool[((size_t)id << CH_SHIFT) + (pos & (CH - 1))] = Rec{((uint64_t)dl << 40) | (t - b * d.W), k};
+}
+
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     const RoundState* rs = d.rs;
     if (rs->done) return;
-    __shared__ uint32_t s_off[SRCMAX];
+    __shared__ uint32_t s_off[MAXG];
     __shared__ uint32_t s_cur[RMAX];
     __shared__ uint64_t s16[16];
-    const bool local = rs->ins_local != 0;
-    const uint64_t S = rs->ins_S, W = d.W;
-    const uint32_t R = d.R, NCH = d.NCH;
-    const uint32_t nsrc = d.P + (recv ? d.G : 0);
-    const uint32_t* wb = d.wbase + (size_t)blockIdx.x * R;
+    const uint32_t R = d.R, blk = blockIdx.x;
+    const uint32_t* wb = d.wbase + (size_t)blk * R;
+    if (blk < d.P) {  // partition blk's staged local events
+        if (!rs->ins_local) return;
+        const uint32_t n = d.rcnt[blk];
+        if (n == 0) return;
+        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+        __syncthreads();
+        const uint64_t S = rs->ins_S;
+        const Rec* src = d.loc + (size_t)blk * d.ECAP;
+        for (uint32_t i = threadIdx.x; i < n; i += K3_T) {
+            const Rec r = src[i];
+            place_event(d, s_cur, S + (r.a & M40), r.k, (uint32_t)(r.a >> 40));
+        }
+        return;
+    }
     for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
-    const uint64_t total = src_offsets(d, recv, local, nsrc, s_off, s16, false);
-    const uint64_t lo = total * blockIdx.x / gridDim.x, hi = total * (blockIdx.x + 1) / gridDim.x;
+    const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
+    const uint32_t g3 = gridDim.x - d.P, w = blk - d.P;
+    const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
     for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
         uint64_t t, k;
         uint32_t dl;
-        if (!src_event(d, recv, s_off, nsrc, S, (uint32_t)idx, t, k, dl)) continue;
-        const uint64_t b = t / W;
-        const uint32_t rb = (uint32_t)(b % R);
-        const uint32_t pos = atomicAdd(&s_cur[rb], 1u);
-        if ((pos >> CH_SHIFT) >= d.nal[rb]) continue;  // beyond the pool (flagged by k_plan)
-        const uint32_t id = d.btab[(size_t)rb * NCH + (pos >> CH_SHIFT)];
-        if (id >= NCH) continue;
-        d.pool[((size_t)id << CH_SHIFT) + (pos & (CH - 1))] = Rec{((uint64_t)dl << 40) | (t - b * W), k};
+        if (recv_event(d, recv, s_off, (uint32_t)idx, t, k, dl)) place_event(d, s_cur, t, k, dl);
     }
 }
 
@@ -1687,14 +1809,37 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
-    // host partitions: HP hosts per k_proc workgroup (power of two)
-    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, next_pow2((d.L + 255) / 256)));
+    // host partitions: HP hosts per k_proc workgroup (power of two), about
+    // one partition per CU
+    const uint32_t hp_env = env_u32("SG_HP", 0);
+    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, next_pow2(hp_env ? hp_env : (d.L + 255) / 256)));
     d.hp_shift = 0;
     while ((1u << d.hp_shift) < d.HP) ++d.hp_shift;
     d.P = (d.L + d.HP - 1) / d.HP;
     if (d.P > PMAX) {
         sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
         return SG_ERR_INVAL;
+    }
+    // k_proc dynamic LDS: per-host arrays (14 B per host), then the event image
+    // (EVL due events, 16 B each), which later holds 2 x R bucket bins.  Two
+    // workgroups per CU when there are more partitions than CUs.
+    d.ev_off = (d.HP * 14 + 15) & ~15u;
+    {
+        const uint32_t bins = 8 * d.R;
+        uint32_t wgs = d.P > 256 ? 2 : 1, evl = 0;
+        for (;;) {
+            const uint32_t dyn = (160u << 10) / wgs - (4u << 10);
+            evl = dyn > d.ev_off ? (dyn - d.ev_off) / 16 : 0;
+            if (wgs == 1 || (evl >= 1024 && evl * 16 >= bins)) break;
+            wgs = 1;
+        }
+        evl = std::min<uint32_t>(std::min<uint32_t>(evl, EVLMAX), env_u32("SG_EVL", EVLMAX));
+        d.EVL = evl;
+        d.proc_lds = d.ev_off + std::max<uint32_t>(evl * 16, bins);
+        if (d.proc_lds > (156u << 10)) {
+            sg_set_error("sg_engine_create: k_proc needs %u B of LDS (HP=%u, R=%u)", d.proc_lds, d.HP, d.R);
+            return SG_ERR_INVAL;
+        }
     }
     const uint32_t per_host = std::max<uint32_t>(32, 2 * d.load);
     d.CAPP = d.HP * per_host;
@@ -1735,7 +1880,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.bmin, D.R);
     ALLOC(D.fring, D.NCH);
     ALLOC(D.nal, D.R);
-    ALLOC(D.wbase, (size_t)D.G3 * D.R);
+    ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.due, D.NCH);
     ALLOC(D.dueb, D.R);
     ALLOC(D.pcnt, P);
@@ -1798,7 +1943,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     std::vector<PairRec> pr(VV);
     for (size_t i = 0; i < VV; ++i) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
     std::vector<HostState> hs(L);
-    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};
+    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};  // evc 0 until boot
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
@@ -1861,6 +2006,7 @@ int sg_engine_boot(sg_engine* e) {
     }
     HIPCHK(hipSetDevice(e->device));
     const Dev& d = e->d;
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)d.R * d.NCH * sizeof(uint32_t), e->stream));
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
@@ -1878,24 +2024,28 @@ static int enqueue_process(sg_engine* e) {
     });
     if (rc) return rc;
     return timed_launch(e, SG_K_PROCESS, [&] {
-        hipLaunchKernelGGL(k_proc, dim3(d.P), dim3(K2_T), 0, e->stream, d);
+        hipLaunchKernelGGL(k_proc, dim3(d.P), dim3(K2_T), d.proc_lds, e->stream, d);
     });
 }
 
-// k_count → k_plan (mode) → k_scatter: the new (and received) events into the
-// calendar, the window and the next round's due list.
+// [k_count →] k_plan (mode) → k_scatter: the new (and received) events into
+// the calendar, the window and the next round's due list.  k_proc already
+// counted the local events; k_count counts received blocks (multi-shard).
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
     const Dev& d = e->d;
-    int rc = timed_launch(e, SG_K_INSERT, [&] {
-        hipLaunchKernelGGL(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, d, recv);
-    });
-    if (rc) return rc;
+    int rc;
+    if (recv) {
+        rc = timed_launch(e, SG_K_INSERT, [&] {
+            hipLaunchKernelGGL(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, d, recv);
+        });
+        if (rc) return rc;
+    }
     rc = timed_launch(e, SG_K_PLAN, [&] {
         hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, recv, mode);
     });
     if (rc) return rc;
     return timed_launch(e, SG_K_INSERT, [&] {
-        hipLaunchKernelGGL(k_scatter, dim3(d.G3), dim3(K3_T), 0, e->stream, d, recv);
+        hipLaunchKernelGGL(k_scatter, dim3(d.P + (recv ? d.G3 : 0)), dim3(K3_T), 0, e->stream, d, recv);
     });
 }
 
