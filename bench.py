@@ -66,6 +66,9 @@ def parse():
                     help="rounds after the timed region that are re-run with per-kernel HIP events")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N > 1: nccl (RCCL, the measured path) or gloo (rehearsal only)")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the multi-rank step path even at N=1 (a world-1 RCCL job: "
+                         "rehearses the collective path on a one-GPU box)")
     ap.add_argument("--same-device", action="store_true",
                     help="N > 1 rehearsal: every rank on GPU 0 (needs --dist-backend gloo)")
     return ap.parse_args()
@@ -187,7 +190,7 @@ def run_single(args):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.dist:
         from shadow_amd import dist
         res = dist.bench(args)
         if res is not None:

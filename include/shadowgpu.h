@@ -153,7 +153,9 @@ typedef struct sg_phold_params {
     sg_simtime fixed_jump;   /* SG_WINDOW_FIXED */
     sg_simtime runahead_min; /* -r in ns, SG_WINDOW_DISCOVERED */
     uint64_t trace_capacity; /* pop records kept for trace diffs (0 = off) */
-    uint64_t exchange_cap;   /* per-peer outbox slots (multi-shard) */
+    uint64_t exchange_cap;   /* per-peer outbox slots of the step API (multi-shard;
+                                a single shard with exchange_cap != 0 runs the
+                                step API too, one rank of a world-1 job) */
 } sg_phold_params;
 
 typedef struct sg_phold_tables {        /* host pointers, copied to HBM at create */

@@ -146,12 +146,14 @@ struct RoundState {
 struct Dev {
     uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
     uint32_t R, NCH, HP, hp_shift, P, CAPP, ECAP, G1, G3;
-    uint32_t EVL, ev_off, proc_lds;  // k_proc: due events sorted in LDS, their offset, dynamic LDS bytes
+    uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
+                                              // events at, dynamic bytes
     uint64_t W;
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
     const PairRec* pairs;     // [V*V]
+    const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
     HostState* hs;            // [L]
     // calendar
     Rec* pool;                // [NCH][CH]
@@ -188,7 +190,7 @@ struct Dev {
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
-    uint64_t* stamps;         // [P][8] s_memrealtime per k_proc phase (SG_STAMPS=1), else null
+    uint64_t* stamps;         // [P][16] k_proc phase stamps + [16] k_plan's (SG_STAMPS=1), else null
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
@@ -258,10 +260,18 @@ __device__ __forceinline__ Probe dst_probe(const Dev& d, uint32_t g) {
     }
     return pb;
 }
+// Keeps a value in a register at this point: stops the compiler from merging
+// per-branch values into a load through a selected address (which demotes
+// the sources to scratch and the loads to flat).
+template <class T>
+__device__ __forceinline__ T opaque(T v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 __device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_t g, const Probe& pb,
-                                                HostInfo& info) {
+                                                uint32_t& vert) {
     if (d.dst_rule == SG_DST_UNIFORM_FLOOR) {
-        info = pb.cur;
+        vert = pb.cur.vertex;
         return g;
     }
     const uint32_t N = d.N;
@@ -269,32 +279,34 @@ __device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_
     uint32_t lo, hi;
     if (x <= pb.cur.wt) {
         if (g == 0 || x > pb.prev.wt) {
-            info = pb.cur;
+            vert = opaque(pb.cur.vertex);
             return g;
         }
         lo = 0;
         hi = g - 1;  // x <= wt[g-1]: the answer is in [0, g-1]
     } else {
         if (g + 1 < N && x <= pb.next.wt) {
-            info = pb.next;
+            vert = opaque(pb.next.vertex);
             return g + 1;
         }
         if (g + 1 >= N || x > w[N - 1].wt) return N;
         lo = g + 2;
-        hi = N - 1;  // wt[g+1] < x <= wt[N-1]
+        hi = N - 1;  // x > wt[g+1] and x <= wt[N-1]
     }
     while (lo < hi) {
-        const uint32_t mid = lo + (hi - lo) / 2;
+        const uint32_t mid = (lo + hi) >> 1;
         if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
     }
-    info = w[lo];
+    vert = opaque(w[lo].vertex);
     return lo;
 }
 __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
     const uint32_t g = dst_guess(d, x);
-    return dst_resolve(d, x, g, dst_probe(d, g), info);
+    uint32_t v = 0;
+    const uint32_t r = dst_resolve(d, x, g, dst_probe(d, g), v);
+    info.vertex = v;
+    return r;
 }
-
 __device__ __forceinline__ uint32_t owner_of(const Dev& d, uint32_t h) {
     uint32_t p = 0;
     while (p + 1 < d.G && h >= d.bounds[p + 1]) ++p;
@@ -354,6 +366,33 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s16, u
     }
     *total = tot;
     return x - v + add;
+}
+
+// Wave-aggregated LDS reservations: one atomic per wave instead of one per
+// lane (same-address LDS atomics serialise across the workgroup's lanes).
+// wave_reserve: n slots per lane, every lane of the wave must call it.
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(x, o, 64);
+        if (lane >= o) x += u;
+    }
+    uint32_t base = 0;
+    if (lane == 63 && x) base = atomicAdd(ctr, x);
+    base = __shfl(base, 63, 64);
+    return base + x - n;
+}
+// wave_slot: one slot for each ACTIVE lane (divergent code allowed).
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
+    const uint64_t m = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ULL << lane) - 1));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, (int)leader, 64);
+    return base + rank;
 }
 
 // event_compare with equal dst (event.c:122-148) on (time, src<<40|seq).
@@ -569,15 +608,18 @@ struct ProcShared {
 // Stage one new event (time already bumped) for the calendar (this shard's
 // hosts; k_proc counts them by bucket after phase C) or for the outbox (other
 // shards).
-__device__ __forceinline__ void stage_event(const Dev& d, uint64_t S, uint32_t part, ProcShared& sh,
+__device__ __forceinline__ bool stage_event(const Dev& d, uint64_t S, uint32_t part, ProcShared& sh,
                                             Acc& a, uint32_t dst, uint64_t tn, uint64_t key) {
     const uint32_t dl = dst - d.lo;
+    a.emin = tn < a.emin ? tn : a.emin;
+    ++a.ctr[C_EMIT];
     if (dl < d.L) {
-        const uint32_t slot = atomicAdd(&sh.nloc, 1u);
+        const uint32_t slot = wave_slot(&sh.nloc);
         if (slot < d.ECAP) d.loc[(size_t)part * d.ECAP + slot] = Rec{((uint64_t)dl << 40) | (tn - S), key};
         else a.overflow = true;
+        return true;
     } else {
-        const uint32_t slot = atomicAdd(&sh.nrem, 1u);
+        const uint32_t slot = wave_slot(&sh.nrem);
         if (slot < d.ECAP) {
             const size_t so = (size_t)part * d.ECAP + slot;
             d.rem[so] = Slot{tn, key};
@@ -586,18 +628,17 @@ __device__ __forceinline__ void stage_event(const Dev& d, uint64_t S, uint32_t p
         } else {
             a.overflow = true;
         }
+        return false;
     }
-    a.emin = tn < a.emin ? tn : a.emin;
-    ++a.ctr[C_EMIT];
 }
 
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
 // Self events that fall inside the window go to the lane's same-round list
 // through `append`; everything else is staged.
-template <class Append>
+template <class Append, class Count>
 __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t E, uint32_t part,
                                               HostCtx& c, Acc& a, uint64_t bt, uint64_t bk,
-                                              ProcShared& sh, Append append) {
+                                              ProcShared& sh, Append append, Count count) {
     const uint32_t bsrc = (uint32_t)(bk >> SRC_SHIFT);
     const uint64_t bseq = bk & SEQ_MASK;
     c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
@@ -652,7 +693,78 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             tn = E;
             ++a.ctr[C_BUMPED];
         }
-        stage_event(d, S, part, sh, a, dst, tn, key);
+        if (stage_event(d, S, part, sh, a, dst, tn, key)) count(tn);
+    }
+}
+
+// One resolved send of a host whose sends cannot land in this window at the
+// host itself: reliability test (worker.c:268-273), delivery time
+// (worker.c:275-277), srcHostEventID (event.c:38), endTime drop
+// (scheduler.c:343-346), barrier bump (host_single.c:180-184), staging.
+template <class Count>
+__device__ __forceinline__ void commit_send(const Dev& d, uint64_t S, uint64_t E, uint32_t part, HostCtx& c,
+                                            Acc& a, ProcShared& sh, uint64_t bt, int32_t ch, uint32_t dst,
+                                            const PairRec& pr, Count count) {
+    a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
+    if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
+        ++a.ctr[C_DROPREL];
+        return;
+    }
+    uint64_t tn = bt + pr.delay;
+    const uint64_t sq = c.s.evc++;
+    if (tn >= d.end_time) {
+        ++a.ctr[C_DROPEND];
+        return;
+    }
+    if (dst == c.h && tn < E) a.overflow = true;  // excluded by the caller's self-path test
+    if (dst != c.h && tn < E) {
+        tn = E;
+        ++a.ctr[C_BUMPED];
+    }
+    if (stage_event(d, S, part, sh, a, dst, tn, ((uint64_t)c.h << SRC_SHIFT) | sq)) count(tn);
+}
+
+// Pop a host's sorted segment (worker.c:165-176): trace digest, counters and
+// the PHOLD body's draws (test_phold.c:160-178, worker.c:268-269); every send
+// with a destination goes to on_send(x, chance, time offset).
+template <class OnSend>
+__device__ __forceinline__ void pop_segment(const Dev& d, RoundState* rs, uint64_t S, HostCtx& c, Acc& a,
+                                            const Rec* seg, uint32_t cnt, int32_t last, OnSend on_send) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const Rec ev = seg[i];
+        const uint64_t trel = ev.a & M52, bt = S + trel;
+        const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
+        const uint64_t bseq = ev.k & SEQ_MASK;
+        c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
+        if (d.trace) {
+            const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
+            if (ts < d.trace_cap) {
+                sg_trace_rec tr;
+                tr.time = bt;
+                tr.seq = bseq;
+                tr.host = c.h;
+                tr.src = bsrc;
+                tr.pos = c.s.pops;
+                d.trace[ts] = tr;
+            } else {
+                a.overflow = true;
+            }
+        }
+        ++c.s.pops;
+        ++a.ctr[C_POPS];
+        const bool boot = (bsrc == c.h) & (bseq == 0);
+        a.ctr[C_BOOTS] += boot;
+        const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+        for (uint32_t m = 0; m < nsend; ++m) {
+            const int32_t x = dev_rand_r(c.s.rng);
+            if (x > last) {  // no host selected (test_phold.c:176-177)
+                ++a.ctr[C_NULL];
+                continue;
+            }
+            const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
+            ++a.ctr[C_SENDS];
+            on_send(x, ch, trel);
+        }
     }
 }
 
@@ -671,6 +783,13 @@ __device__ __forceinline__ void sort_segment(Rec* seg, uint32_t cnt) {
             seg[b.slot] = t;
         }
     }
+}
+
+// Diagnostics (SG_STAMPS): a timestamp once this wave's outstanding memory
+// operations have landed.
+__device__ __forceinline__ uint64_t wait_stamp() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memrealtime();
 }
 
 // One workgroup per partition of HP hosts.
@@ -700,11 +819,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint32_t HP = d.HP, R = d.R;
     uint32_t* s_n = (uint32_t*)dyn;             // [HP] events per host
     uint32_t* s_c = s_n + HP;                   // [HP] start offset, then end (scatter cursor)
-    uint32_t* s_vh = s_c + HP;                  // [HP] vertex of active host j
-    uint16_t* s_act = (uint16_t*)(s_vh + HP);   // [HP] active hosts, ascending
-    Rec* s_ev = (Rec*)(dyn + d.ev_off);         // [EVL] due events grouped by host
-    uint32_t* s_bc = (uint32_t*)(dyn + d.ev_off);  // [R] after phase A: staged events per bucket
-    uint32_t* s_bm = s_bc + R;                     // [R] their min time offset in the bucket
+    uint32_t* s_vh = s_c + HP;                  // [HP] active host j: vertex | phase C sends << 16
+    uint32_t* s_sb = s_vh + HP;                 // [HP] active host j: first phase B/C send, or UINT32_MAX
+    uint16_t* s_act = (uint16_t*)(s_sb + HP);   // [HP] active hosts, ascending
+    uint32_t* s_bc = (uint32_t*)(dyn + d.bin_off);  // [R] staged local events per bucket
+    uint32_t* s_bm = s_bc + R;                      // [R] their min time offset in the bucket
+    Rec* s_ev = (Rec*)(dyn + d.ev_off);             // [EVL] due events grouped by host
     __shared__ uint32_t s_nsend;
     __shared__ int32_t s_last;         // last weight threshold: x above it selects no host
     __shared__ ProcShared sh;
@@ -713,11 +833,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint64_t S = rs->S, E = rs->E;
     const uint32_t p = blockIdx.x;
     const uint32_t tid = threadIdx.x;
-    uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * 8 : nullptr;
+    uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * 16 : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
     for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
+    for (uint32_t rb = tid; rb < R; rb += K2_T) {
+        s_bc[rb] = 0;
+        s_bm[rb] = UINT32_MAX;
+    }
     if (tid == 0) {
         sh.nloc = 0;
         sh.nrem = 0;
@@ -781,6 +905,29 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     const uint32_t nact = (uint32_t)tot;
     __syncthreads();
+    const uint32_t hbase = d.lo + p * HP;
+    // phase A's first NPRE hosts of every lane: state loads issued now, under
+    // the LDS scatter below
+    constexpr uint32_t NPRE = 2;
+    // HostState as two 16-B words per host, kept in plain scalars
+    ulonglong2 pre_a0 = make_ulonglong2(0, 0), pre_b0 = pre_a0, pre_a1 = pre_a0, pre_b1 = pre_a0;
+    uint32_t pre_v0 = 0, pre_v1 = 0;
+    {
+        const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
+        const uint32_t h0 = hbase + (tid < nact ? s_act[tid] : 0u);
+        if (tid < nact && h0 - d.lo < d.L) {
+            pre_a0 = hsw[2 * (size_t)(h0 - d.lo)];
+            pre_b0 = hsw[2 * (size_t)(h0 - d.lo) + 1];
+            pre_v0 = d.hinfo[h0].vertex;
+        }
+        const uint32_t j1 = tid + K2_T;
+        const uint32_t h1 = hbase + (j1 < nact ? s_act[j1] : 0u);
+        if (j1 < nact && h1 - d.lo < d.L) {
+            pre_a1 = hsw[2 * (size_t)(h1 - d.lo)];
+            pre_b1 = hsw[2 * (size_t)(h1 - d.lo) + 1];
+            pre_v1 = d.hinfo[h1].vertex;
+        }
+    }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
     if (in_lds) {
 #pragma unroll
@@ -811,132 +958,169 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     a.overflow = false;
     Rec* xs = d.extras + ((size_t)p * K2_T + tid) * XCAP;
     Rec* snd = d.sends + (size_t)p * d.ECAP;
-    const uint32_t hbase = d.lo + p * HP;
     const int32_t last = s_last;
-    uint32_t sbase[HPT], scnt[HPT];  // sbase UINT32_MAX: no phase C (sequential or idle)
-    uint64_t evc_r[HPT];
 
     // ---- phase A (segments in LDS or in part2: two instantiations)
-    auto phase_a = [&](auto seg_in_lds) {
+    const uint64_t W = d.W, bS = rs->bS;
+    const uint32_t bSr = (uint32_t)(bS % R);
+    bool horizon = false;
+    auto count_local = [&](uint64_t t) {  // one staged local event into the bucket bins
+        const uint64_t b = t / W;
+        if (b < bS || b - bS >= R) {
+            horizon = true;
+            return;
+        }
+        uint32_t rb = bSr + (uint32_t)(b - bS);
+        rb = rb >= R ? rb - R : rb;
+        atomicAdd(&s_bc[rb], 1u);
+        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
+    };
+    auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
         Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
-#pragma unroll
+#pragma unroll 1
         for (uint32_t q = 0; q < HPT; ++q) {
-            sbase[q] = UINT32_MAX;
-            scnt[q] = 0;
             const uint32_t j = tid + q * K2_T;
-            if (j >= nact) continue;
-            const uint32_t hl = s_act[j];
-            const uint32_t cnt = s_n[hl];
-            Rec* seg = segs + (s_c[hl] - cnt);
+            if (__builtin_amdgcn_readfirstlane(tid & ~63u) + q * K2_T >= nact) break;  // wave-uniform
+            bool go = false;  // this lane records sends (phase B/C path)
+            uint32_t ns = 0, cnt = 0, lh = 0;
+            Rec* seg = nullptr;
             HostCtx c;
-            c.h = hbase + hl;
-            const uint32_t lh = c.h - d.lo;
-            if (lh >= d.L) {
-                a.overflow = true;
-                continue;
-            }
-            c.s = d.hs[lh];
-            c.vh = d.hinfo[c.h].vertex;
-            s_vh[j] = c.vh;
-            ++a.ctr[C_ACTIVE];
-            sort_segment(seg, cnt);  // pop order
-            const uint64_t self_delay = d.pairs[(size_t)c.vh * d.V + c.vh].delay;
-            if (S + (seg[0].a & M52) + self_delay < E) {
-                // sequential body: a self event may land inside this window
-                uint32_t nx = 0;
-                auto append = [&](uint64_t trel, uint64_t key) -> bool {
-                    if (nx >= XCAP) return false;
-                    xs[nx++] = Rec{trel, key};
-                    return true;
-                };
-                uint32_t ns = cnt, i0 = 0;
-                for (;;) {
-                    Best b{UINT64_MAX, 0, UINT32_MAX};
-                    for (uint32_t i = i0; i < ns; ++i) {
-                        const Rec r = seg[i];
-                        best_take(b, r.a & M52, r.k, i);
-                    }
-                    for (uint32_t i = 0; i < nx; ++i) {
-                        const Rec r = xs[i];
-                        best_take(b, r.a, r.k, 0x80000000u | i);
-                    }
-                    if (b.slot == UINT32_MAX) break;
-                    if (b.slot & 0x80000000u) {
-                        const uint32_t i = b.slot & 0x7FFFFFFFu;
-                        --nx;
-                        if (i != nx) xs[i] = xs[nx];
+            const bool st0 = stamp && tid == 0 && q == 0;
+            if (j < nact) {
+                s_sb[j] = UINT32_MAX;
+                const uint32_t hl = s_act[j];
+                cnt = s_n[hl];
+                seg = segs + (s_c[hl] - cnt);
+                c.h = hbase + hl;
+                lh = c.h - d.lo;
+                if (lh >= d.L) {
+                    a.overflow = true;
+                } else {
+                    if (q < NPRE) {  // selects of values, not of addresses
+                        c.s.rng = (uint32_t)opaque(q == 0 ? pre_a0.x : pre_a1.x);
+                        c.s.pad = 0;
+                        c.s.pops = opaque(q == 0 ? pre_a0.y : pre_a1.y);
+                        c.s.digest = opaque(q == 0 ? pre_b0.x : pre_b1.x);
+                        c.s.evc = opaque(q == 0 ? pre_b0.y : pre_b1.y);
+                        c.vh = opaque(q == 0 ? pre_v0 : pre_v1);
                     } else {
-                        --ns;
-                        if (b.slot != ns) seg[b.slot] = seg[ns];
+                        c.s = d.hs[lh];
+                        c.vh = d.hinfo[c.h].vertex;
                     }
-                    execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append);
+                    s_vh[j] = c.vh;
+                    ++a.ctr[C_ACTIVE];
+                    const uint64_t self_delay = d.vself[c.vh];
+                    if (st0) stamp[8] = wait_stamp();
+                    sort_segment(seg, cnt);  // pop order
+                    if (st0) stamp[9] = wait_stamp();
+                    if (S + (seg[0].a & M52) + self_delay < E) {
+                        // sequential body: a self event may land inside this window
+                        uint32_t nx = 0;
+                        auto append = [&](uint64_t trel, uint64_t key) -> bool {
+                            if (nx >= XCAP) return false;
+                            xs[nx++] = Rec{trel, key};
+                            return true;
+                        };
+                        uint32_t nl = cnt, i0 = 0;
+                        for (;;) {
+                            Best b{UINT64_MAX, 0, UINT32_MAX};
+                            for (uint32_t i = i0; i < nl; ++i) {
+                                const Rec r = seg[i];
+                                best_take(b, r.a & M52, r.k, i);
+                            }
+                            for (uint32_t i = 0; i < nx; ++i) {
+                                const Rec r = xs[i];
+                                best_take(b, r.a, r.k, 0x80000000u | i);
+                            }
+                            if (b.slot == UINT32_MAX) break;
+                            if (b.slot & 0x80000000u) {
+                                const uint32_t i = b.slot & 0x7FFFFFFFu;
+                                --nx;
+                                if (i != nx) xs[i] = xs[nx];
+                            } else {
+                                --nl;
+                                if (b.slot != nl) seg[b.slot] = seg[nl];
+                            }
+                            execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append, count_local);
+                        }
+                        d.hs[lh] = c.s;
+                    } else {
+                        // count this host's sends (arithmetic only)
+                        uint32_t r = c.s.rng;
+                        for (uint32_t i = 0; i < cnt; ++i) {
+                            const uint64_t bk = seg[i].k;
+                            const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
+                            const uint32_t nsend = boot ? d.load : 1u;
+                            for (uint32_t m = 0; m < nsend; ++m) {
+                                const int32_t x = dev_rand_r(r);
+                                if (x > last) continue;
+                                (void)dev_rand_r(r);
+                                ++ns;
+                            }
+                        }
+                        if (ns <= 2) {
+                            // light host (most hosts in steady state): the whole
+                            // body here, both sends' loads in flight together
+                            int32_t x0 = 0, x1 = 0, c0 = 0, c1 = 0;
+                            uint64_t t0 = 0, t1 = 0;
+                            uint32_t nsd = 0;
+                            pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
+                                if (nsd == 0) {
+                                    x0 = x;
+                                    c0 = ch;
+                                    t0 = trel;
+                                } else {
+                                    x1 = x;
+                                    c1 = ch;
+                                    t1 = trel;
+                                }
+                                ++nsd;
+                            });
+                            const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
+                            Probe pb0{}, pb1{};
+                            if (nsd > 0) pb0 = dst_probe(d, g0);
+                            if (nsd > 1) pb1 = dst_probe(d, g1);
+                            uint32_t vd0 = 0, vd1 = 0;
+                            const uint32_t dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
+                            const uint32_t dst1 = nsd > 1 ? dst_resolve(d, x1, g1, pb1, vd1) : 0;
+                            PairRec pr0{}, pr1{};
+                            if (nsd > 0) pr0 = d.pairs[(size_t)c.vh * d.V + vd0];
+                            if (nsd > 1) pr1 = d.pairs[(size_t)c.vh * d.V + vd1];
+                            if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, pr0, count_local);
+                            if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, pr1, count_local);
+                            ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
+                            hp[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
+                            hp[1] = make_ulonglong2(c.s.digest, c.s.evc);
+                            ns = 0;
+                        } else {
+                            go = true;
+                        }
+                    }
                 }
-                d.hs[lh] = c.s;
-                continue;
             }
-            // count this host's sends (arithmetic only), reserve, then record them
-            uint32_t r = c.s.rng, ns = 0;
-            for (uint32_t i = 0; i < cnt; ++i) {
-                const uint64_t bk = seg[i].k;
-                const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
-                const uint32_t nsend = boot ? d.load : 1u;
-                for (uint32_t m = 0; m < nsend; ++m) {
-                    const int32_t x = dev_rand_r(r);
-                    if (x > last) continue;
-                    (void)dev_rand_r(r);
-                    ++ns;
-                }
-            }
-            const uint32_t base = atomicAdd(&s_nsend, ns);
+            if (st0) stamp[10] = wait_stamp();
+            const uint32_t base = wave_reserve(&s_nsend, ns);  // wave converged here
+            if (st0) stamp[11] = wait_stamp();
+            if (!go) continue;
             if (base + ns > d.ECAP) {
                 a.overflow = true;
                 continue;
             }
-            sbase[q] = base;
-            scnt[q] = ns;
-            uint32_t k = base;
-            for (uint32_t i = 0; i < cnt; ++i) {
-                const Rec ev = seg[i];
-                const uint64_t trel = ev.a & M52, bt = S + trel;
-                const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
-                const uint64_t bseq = ev.k & SEQ_MASK;
-                c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
-                if (d.trace) {
-                    const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
-                    if (ts < d.trace_cap) {
-                        sg_trace_rec tr;
-                        tr.time = bt;
-                        tr.seq = bseq;
-                        tr.host = c.h;
-                        tr.src = bsrc;
-                        tr.pos = c.s.pops;
-                        d.trace[ts] = tr;
-                    } else {
-                        a.overflow = true;
-                    }
-                }
-                ++c.s.pops;
-                ++a.ctr[C_POPS];
-                const bool boot = (bsrc == c.h) & (bseq == 0);
-                a.ctr[C_BOOTS] += boot;
-                const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
-                for (uint32_t m = 0; m < nsend; ++m) {
-                    const int32_t x = dev_rand_r(c.s.rng);
-                    if (x > last) {  // no host selected (test_phold.c:176-177)
-                        ++a.ctr[C_NULL];
-                        continue;
-                    }
-                    const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
-                    ++a.ctr[C_SENDS];
-                    snd[k++] = Rec{((uint64_t)j << 52) | trel,
-                                   (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
-                }
+            if (ns > 0xFFFFu) {
+                a.overflow = true;
+                continue;
             }
+            s_sb[j] = base;
+            s_vh[j] = c.vh | (ns << 16);
+            uint32_t k = base;
+            pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
+                snd[k++] = Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
+            });
             // {rng, pops, digest} now; evc after phase C
             HostState* hp = d.hs + lh;
             reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
             hp->digest = c.s.digest;
-            evc_r[q] = c.s.evc;
+            if (st0) stamp[12] = wait_stamp();
         }
     };
     if (in_lds) phase_a(std::true_type{});
@@ -944,11 +1128,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
 
-    // the event image is dead: its LDS becomes the bucket bins
-    for (uint32_t rb = tid; rb < R; rb += K2_T) {
-        s_bc[rb] = 0;
-        s_bm[rb] = UINT32_MAX;
-    }
     // ---- phase B: one lane per send, two in flight
     const uint32_t nsend = s_nsend < d.ECAP ? s_nsend : d.ECAP;
     for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
@@ -959,12 +1138,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
         const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
-        HostInfo di0, di1;
-        const uint32_t dst0 = dst_resolve(d, x0, g0, pb0, di0);
-        const uint32_t dst1 = dst_resolve(d, x1, g1, pb1, di1);
+        uint32_t vd0 = 0, vd1 = 0;
+        const uint32_t dst0 = dst_resolve(d, x0, g0, pb0, vd0);
+        const uint32_t dst1 = dst_resolve(d, x1, g1, pb1, vd1);
         const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
-        const PairRec pr0 = d.pairs[(size_t)s_vh[j0] * d.V + di0.vertex];
-        const PairRec pr1 = d.pairs[(size_t)s_vh[j1] * d.V + di1.vertex];
+        const PairRec pr0 = d.pairs[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0];
+        const PairRec pr1 = d.pairs[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1];
         {
             const uint64_t bt = S + (r0.a & M52);
             const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
@@ -983,14 +1162,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- phase C: per host, in send order
-#pragma unroll
+    // ---- phase C: hosts with phase B sends, per host in send order
+#pragma unroll 1
     for (uint32_t q = 0; q < HPT; ++q) {
-        if (sbase[q] == UINT32_MAX) continue;
         const uint32_t j = tid + q * K2_T;
+        if (j >= nact) break;
+        const uint32_t sb = s_sb[j];
+        if (sb == UINT32_MAX) continue;
         const uint32_t h = hbase + s_act[j];
-        uint64_t evc = evc_r[q];
-        for (uint32_t k = sbase[q]; k < sbase[q] + scnt[q]; ++k) {
+        const uint32_t ns = s_vh[j] >> 16;
+        uint64_t evc = d.hs[h - d.lo].evc;  // untouched by phase A on this path
+        for (uint32_t k = sb; k < sb + ns; ++k) {
             const Rec r = snd[k];
             if (!(r.a >> 63)) {
                 ++a.ctr[C_DROPREL];
@@ -1008,31 +1190,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 tn = E;
                 ++a.ctr[C_BUMPED];
             }
-            stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq);
+            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
         }
         d.hs[h - d.lo].evc = evc;
     }
-    __syncthreads();  // staging done: sh.nloc is final, loc[] visible to the workgroup
-
-    // ---- count: staged local events by bucket, then one reservation per bucket
-    const uint64_t W = d.W, bS = rs->bS;
-    const uint32_t bSr = (uint32_t)(bS % R);
+    __syncthreads();  // staging done: sh.nloc final, bins complete
     const uint32_t nl = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
-    const Rec* lp = d.loc + (size_t)p * d.ECAP;
-    bool horizon = false;
-    for (uint32_t i = tid; i < nl; i += K2_T) {
-        const Rec r = lp[i];
-        const uint64_t t = S + (r.a & M40);
-        const uint64_t b = t / W;
-        if (b < bS || b - bS >= R) {
-            horizon = true;
-            continue;
-        }
-        uint32_t rb = bSr + (uint32_t)(b - bS);
-        rb = rb >= R ? rb - R : rb;
-        atomicAdd(&s_bc[rb], 1u);
-        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
-    }
     if (horizon) flag(d, OV_HORIZON);
 
     // workgroup partials: cumulative counters, this round's two minima
@@ -1071,7 +1234,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
-    if (d.G > 1 && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
+    if (d.peercnt && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
     if (stamp && tid == 0) {
         stamp[4] = __builtin_amdgcn_s_memrealtime();
         stamp[5] = n;
@@ -1266,6 +1429,7 @@ __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t&
 // coalesced load, scans and updates in LDS, one write-back.
 struct PlanLds {
     uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
+    uint32_t off[RMAX];  // allocation: first new chunk of each bucket in this launch's run
     uint64_t mn[RMAX];
 };
 
@@ -1282,11 +1446,22 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     const uint32_t R = d.R, NCH = d.NCH;
     const uint64_t W = d.W;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t rb = tid; rb < R; rb += PL_T) {
-        B.cnt[rb] = d.bcnt[rb];
-        B.tomb[rb] = d.btomb[rb];
-        B.nal[rb] = d.nal[rb];
-        B.mn[rb] = d.bmin[rb];
+    uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * 16 : nullptr;
+#define PSTAMP(k) \
+    if (pst) pst[k] = __builtin_amdgcn_s_memrealtime()
+    PSTAMP(0);
+    // bucket metadata: loads issued together with reduce_local's, LDS stores after
+    uint32_t rc[PER], rt[PER], rn[PER];
+    uint64_t rm[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * PL_T;
+        if (rb < R) {
+            rc[q] = d.bcnt[rb];
+            rt[q] = d.btomb[rb];
+            rn[q] = d.nal[rb];
+            rm[q] = d.bmin[rb];
+        }
     }
     if (tid == 0) {
         s_head = rs->fl_head;
@@ -1323,7 +1498,18 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         reduce_local(d, s16, m, j);  // barriers inside
         ovf = rs->overflow;
     }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * PL_T;
+        if (rb < R) {
+            B.cnt[rb] = rc[q];
+            B.tomb[rb] = rt[q];
+            B.nal[rb] = rn[q];
+            B.mn[rb] = rm[q];
+        }
+    }
     __syncthreads();
+    PSTAMP(1);
     if (mode == 1) {
         m = s_m;
         j = s_j;
@@ -1334,6 +1520,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // free the chunks of the window just executed (not the retained
         // bucket's) and reset its fully consumed buckets
         const uint64_t nd = rs->ndue, tail = s_tail, ndb = rs->ndueb;
+        const uint32_t tail_r = (uint32_t)(tail % NCH);
         uint64_t mine = 0;
         for (uint64_t i = tid; i < nd; i += PL_T) {
             const DueEnt de = d.due[i];
@@ -1344,7 +1531,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         for (uint64_t i = tid; i < nd; i += PL_T) {
             const DueEnt de = d.due[i];
             if ((de.nflags & RETAINED) || de.id >= NCH) continue;
-            d.fring[(tail + k++) % NCH] = de.id;
+            const uint64_t pos = tail_r + k++;  // k < NCH: one wrap at most
+            d.fring[pos >= NCH ? pos - NCH : pos] = de.id;
         }
         for (uint64_t i = 0; i < ndb; ++i) {
             const uint32_t rb = d.dueb[i];
@@ -1362,8 +1550,12 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         if (tid == 0) s_tail = tail + tot;
         __syncthreads();
     }
+    PSTAMP(2);
     if (mode != 2) {
-        // every bucket gets the chunks its count needs (k_count ran), from the ring
+        // every bucket gets the chunks its count needs (k_proc / k_count
+        // reserved the slots), from the ring: per-bucket offsets into the run
+        // of new chunks, then one cooperative pass over the run (a bucket
+        // search in LDS per chunk) so every ring load is independent
         uint32_t need[PER];
         uint64_t mine = 0;
 #pragma unroll
@@ -1379,25 +1571,42 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         }
         uint64_t total;
         uint64_t off = block_excl_scan(mine, s16, &total);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t rb = tid * PER + q;
+            if (rb < R) B.off[rb] = (uint32_t)off;
+            off += need[q];
+        }
+        __syncthreads();
         const uint64_t head = s_head, avail = s_tail - head;
+        const uint32_t give = (uint32_t)(total < avail ? total : avail);
+        const uint32_t head_r = (uint32_t)(head % NCH);
+        for (uint32_t i = tid; i < give; i += PL_T) {
+            uint32_t lo = 0, hi = R - 1;  // the last bucket whose run starts at or before i
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (B.off[mid] <= i) lo = mid; else hi = mid - 1;
+            }
+            const uint32_t pos = head_r + i;  // give <= NCH: one wrap at most
+            d.btab[(size_t)lo * NCH + B.nal[lo] + (i - B.off[lo])] = d.fring[pos >= NCH ? pos - NCH : pos];
+        }
+        __syncthreads();
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;
             if (rb >= R || !need[q]) continue;
-            const uint32_t have = B.nal[rb];
-            uint32_t* tab = d.btab + (size_t)rb * NCH;
-            uint32_t k = 0;
-            for (; k < need[q] && off + k < avail; ++k) tab[have + k] = d.fring[(head + off + k) % NCH];
-            B.nal[rb] = have + k;
-            off += need[q];
+            const uint32_t o = B.off[rb];
+            const uint32_t got = give <= o ? 0 : (give - o < need[q] ? give - o : need[q]);
+            B.nal[rb] += got;
         }
         __syncthreads();
         if (tid == 0) {
             if (total > avail) flag(d, OV_POOL);
-            s_head = head + (total < avail ? total : avail);
+            s_head = head + give;
         }
         __syncthreads();
     }
+    PSTAMP(3);
     bool list = true;
     if (mode == 1 && s_more) {  // drain step: same window, more exchange
         list = false;
@@ -1418,6 +1627,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         __syncthreads();
         list = !s_done;
     }
+    PSTAMP(4);
     if (list) {
         // list the due chunks of the new window [S, E)
         const uint64_t S = s_S, E = s_E;
@@ -1462,16 +1672,19 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             if (!ret && c) ++ndb;
         }
         __syncthreads();
+        PSTAMP(5);
         if (straddle && tid == 0) B.mn[bL % R] = UINT64_MAX;  // k_gather's carry min and k_count restore it
         // exact min beyond the window: the first non-empty bucket in (bL, bS + R)
         // (the window's own slots lie outside that range; the spent slot is empty)
         uint64_t first = UINT64_MAX;
-        const uint32_t span = (uint32_t)(bL - bS);
+        const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
         for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
-            const uint64_t b = bL + o;
-            const uint32_t rb = (uint32_t)(b % R);
+            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
             if (rb == s_spent) continue;
-            if (B.cnt[rb] > B.tomb[rb]) first = b < first ? b : first;
+            if (B.cnt[rb] > B.tomb[rb]) {
+                const uint64_t b = bL + o;
+                first = b < first ? b : first;
+            }
         }
         first = block_min(first, s16);  // barriers inside
         if (tid == 0) {
@@ -1484,6 +1697,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         }
     }
     __syncthreads();
+    PSTAMP(6);
     for (uint32_t rb = tid; rb < R; rb += PL_T) {
         d.bcnt[rb] = B.cnt[rb];
         d.btomb[rb] = B.tomb[rb];
@@ -1494,6 +1708,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         rs->fl_head = s_head;
         rs->fl_tail = s_tail;
     }
+    PSTAMP(7);
+#undef PSTAMP
 }
 
 // --------------------------------------------------------- multi-shard ----
@@ -1723,11 +1939,11 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     *out = nullptr;
     const sg_phold_params& p = *params;
     const uint32_t G = p.shard_count ? p.shard_count : 1;
-    if (p.n_hosts == 0 || p.n_hosts > (1u << (64 - SRC_SHIFT)) || p.n_vertices == 0 || G > MAXG ||
+    if (p.n_hosts == 0 || p.n_hosts > (1u << (64 - SRC_SHIFT)) || p.n_vertices == 0 || p.n_vertices > 0xFFFFu || G > MAXG ||
         p.shard_index >= G || G > p.n_hosts || !t->host_vertex || !t->host_rng || !t->delay_ns ||
         !t->keep_max || !t->jump_ms || (p.dst_rule == SG_DST_WEIGHTS && !t->weight_thresh) ||
         p.dst_rule > 1 || p.window_rule > 1 || p.load == 0) {
-        sg_set_error("sg_engine_create: invalid parameters (n_hosts must be in [1, 2^24])");
+        sg_set_error("sg_engine_create: invalid parameters (n_hosts must be in [1, 2^24], n_vertices in [1, 65535])");
         return SG_ERR_INVAL;
     }
     int ndev = 0;
@@ -1820,22 +2036,22 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
         return SG_ERR_INVAL;
     }
-    // k_proc dynamic LDS: per-host arrays (14 B per host), then the event image
-    // (EVL due events, 16 B each), which later holds 2 x R bucket bins.  Two
+    // k_proc dynamic LDS: per-host arrays (18 B per host), the bucket bins
+    // (2 x R u32), then the event image (EVL due events, 16 B each).  Two
     // workgroups per CU when there are more partitions than CUs.
-    d.ev_off = (d.HP * 14 + 15) & ~15u;
+    d.bin_off = (d.HP * 18 + 15) & ~15u;
+    d.ev_off = d.bin_off + ((8 * d.R + 15) & ~15u);
     {
-        const uint32_t bins = 8 * d.R;
         uint32_t wgs = d.P > 256 ? 2 : 1, evl = 0;
         for (;;) {
             const uint32_t dyn = (160u << 10) / wgs - (4u << 10);
             evl = dyn > d.ev_off ? (dyn - d.ev_off) / 16 : 0;
-            if (wgs == 1 || (evl >= 1024 && evl * 16 >= bins)) break;
+            if (wgs == 1 || evl >= 1024) break;
             wgs = 1;
         }
         evl = std::min<uint32_t>(std::min<uint32_t>(evl, EVLMAX), env_u32("SG_EVL", EVLMAX));
         d.EVL = evl;
-        d.proc_lds = d.ev_off + std::max<uint32_t>(evl * 16, bins);
+        d.proc_lds = d.ev_off + evl * 16;
         if (d.proc_lds > (156u << 10)) {
             sg_set_error("sg_engine_create: k_proc needs %u B of LDS (HP=%u, R=%u)", d.proc_lds, d.HP, d.R);
             return SG_ERR_INVAL;
@@ -1870,8 +2086,11 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     PairRec* pairs;
     ALLOC(hinfo, N);
     ALLOC(pairs, VV);
+    uint64_t* vself;
+    ALLOC(vself, D.V);
     D.hinfo = hinfo;
     D.pairs = pairs;
+    D.vself = vself;
     ALLOC(D.hs, L);
     ALLOC(D.pool, (size_t)D.NCH * CH);
     ALLOC(D.btab, (size_t)D.R * D.NCH);
@@ -1893,7 +2112,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.c1min, D.G1);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
-    if (G > 1) {
+    if (G > 1 || p.exchange_cap) {  // step API (a single shard may use it too: exchange_cap != 0)
         ALLOC(D.remn, P);
         ALLOC(D.rem, P * D.ECAP);
         ALLOC(D.rem_dst, P * D.ECAP);
@@ -1907,7 +2126,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
-    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, P * 8);
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, P * 16 + 16);  // + k_plan's 16
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
@@ -1942,11 +2161,14 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     std::vector<PairRec> pr(VV);
     for (size_t i = 0; i < VV; ++i) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
+    std::vector<uint64_t> vs(D.V);
+    for (size_t v = 0; v < D.V; ++v) vs[v] = t->delay_ns[v * D.V + v];
     std::vector<HostState> hs(L);
     for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};  // evc 0 until boot
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemcpy(vself, vs.data(), D.V * sizeof(uint64_t), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(D.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemset(D.rs, 0, sizeof(RoundState));
     err = err != hipSuccess ? err : hipMemset(D.pcum, 0, NCTR * P * 8);
@@ -2054,8 +2276,8 @@ int sg_engine_enqueue_round(sg_engine* e) {
         sg_set_error("sg_engine_enqueue_round: engine not booted");
         return SG_ERR_STATE;
     }
-    if (e->d.G != 1) {
-        sg_set_error("sg_engine_enqueue_round: sharded engine, use the step API");
+    if (e->d.G != 1 || e->d.outn) {
+        sg_set_error("sg_engine_enqueue_round: step-mode engine, use the step API");
         return SG_ERR_STATE;
     }
     int rc;
@@ -2192,8 +2414,8 @@ static int need_sharded(sg_engine* e, const char* fn) {
         sg_set_error("%s: engine not booted", fn);
         return SG_ERR_STATE;
     }
-    if (e->d.G < 2) {
-        sg_set_error("%s: single-shard engine, use sg_engine_run / enqueue_round", fn);
+    if (!e->d.outn) {
+        sg_set_error("%s: round-mode engine (one shard, exchange_cap 0), use sg_engine_run / enqueue_round", fn);
         return SG_ERR_STATE;
     }
     return SG_OK;
@@ -2257,7 +2479,7 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
 
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
     if (!e) return SG_ERR_INVAL;
-    const uint64_t n = e->d.stamps ? (uint64_t)e->d.P * 8 : 0;
+    const uint64_t n = e->d.stamps ? (uint64_t)e->d.P * 16 + 16 : 0;
     if (n_out) *n_out = n;
     if (out && capacity && n) {
         HIPCHK(hipStreamSynchronize(e->stream));

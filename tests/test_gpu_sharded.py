@@ -58,7 +58,8 @@ def _check(cfg, shards):
     return st, want
 
 
-@pytest.mark.parametrize("world,kind,xcap", [(2, "tiny", 4096), (3, "probe10", 4096),
+@pytest.mark.parametrize("world,kind,xcap", [(1, "tiny", 4096), (1, "c4small", None),
+                                             (2, "tiny", 4096), (3, "probe10", 4096),
                                              (4, "c4small", None), (2, "tiny", 7),
                                              (3, "lossy", 50)])
 def test_inprocess_shards_match_oracle(world, kind, xcap):

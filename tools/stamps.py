@@ -16,7 +16,8 @@ eng.boot()
 eng.run(40)
 for r in range(3):
     eng.run(1)
-    st = eng.stamps().astype(np.int64)
+    st_all = eng.stamps().astype(np.int64)
+    st, pl = st_all[:-1], st_all[-1]
     t0 = st[:, 0].min()
     ph = np.diff(st[:, :5], axis=1) * 10 / 1e3  # us (100 MHz ticks)
     print(f"round +{r}: kernel span {(st[:, 4].max() - t0) / 100:.1f} us; WG start spread "
@@ -25,3 +26,9 @@ for r in range(3):
         v = ph[:, i]
         print(f"   {nm:<12} median {np.median(v):6.2f} us  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
     print("   due/active/sends per WG median", np.median(st[:, 5:8], axis=0), "max", st[:, 5:8].max(axis=0))
+    a = np.diff(st[:, [1, 8, 9, 10, 11, 12]], axis=1) / 100
+    print("   phase A, lane 0 of wave 0, first host (median us): state loads %.2f  sort %.2f  count draws %.2f  "
+          "reserve %.2f  record+store %.2f" % tuple(np.median(a, axis=0)))
+    d = np.diff(pl[:8]) / 100
+    print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
+          "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
