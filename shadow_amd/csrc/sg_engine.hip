@@ -318,12 +318,38 @@ __device__ __forceinline__ T wave_sum(T v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// DPP wave reductions (row_shr 1/2/4/8, row_bcast 15/31; gfx9 wave64): VALU
+// only, no LDS traffic.  Every lane of the wave must be active; the result is
+// wave-uniform.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    uint32_t w;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xf, 0xf, false);
+    v = w < v ? w : v;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xf, 0xf, false);
+    v = w < v ? w : v;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xf, 0xf, false);
+    v = w < v ? w : v;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xf, 0xf, false);
+    v = w < v ? w : v;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xa, 0xf, false);
+    v = w < v ? w : v;
+    w = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xc, 0xf, false);
+    v = w < v ? w : v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t w = __shfl_xor(v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
+    const uint32_t hi = wave_min_u32((uint32_t)(v >> 32));
+    const uint32_t lo = wave_min_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0xFFFFFFFFu);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // Workgroup-wide reductions through a [16] LDS scratch (blocks of <= 1024);
@@ -1195,6 +1221,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.hs[h - d.lo].evc = evc;
     }
     __syncthreads();  // staging done: sh.nloc final, bins complete
+    if (stamp && tid == 0) stamp[13] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nl = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
     if (horizon) flag(d, OV_HORIZON);
 
@@ -1202,7 +1229,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const int lane = tid & 63, wid = tid >> 6;
     uint64_t v[NCTR + 2];
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum((uint64_t)a.ctr[i]);
+    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum_u32(a.ctr[i]);
     v[NCTR] = wave_min(a.emin);
     v[NCTR + 1] = wave_min(a.jmin);
     if (lane == 0) {
@@ -1211,6 +1238,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
+    if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     uint32_t* wb = d.wbase + (size_t)p * R;
     for (uint32_t rb = tid; rb < R; rb += K2_T) {
         const uint32_t c = s_bc[rb];
@@ -1219,6 +1247,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         wb[rb] = atomicAdd(&d.bcnt[rb], c);
         atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
     }
+    if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid < NCTR + 2) {
         const int i = tid;
         uint64_t r = s_red[0][i];

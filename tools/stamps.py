@@ -29,6 +29,9 @@ for r in range(3):
     a = np.diff(st[:, [1, 8, 9, 10, 11, 12]], axis=1) / 100
     print("   phase A, lane 0 of wave 0, first host (median us): state loads %.2f  sort %.2f  count draws %.2f  "
           "reserve %.2f  record+store %.2f" % tuple(np.median(a, axis=0)))
+    t = np.diff(st[:, [3, 13, 14, 15, 4]], axis=1) / 100
+    print("   after phase B (median us): phase C %.2f  partials %.2f  reservations %.2f  tail %.2f"
+          % tuple(np.median(t, axis=0)))
     d = np.diff(pl[:8]) / 100
     print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
           "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
