@@ -125,6 +125,79 @@ int sg_topology_lognormal(uint32_t n_vertices, uint64_t seed, double median_ms,
                           double* latency_ms_out, double* edge_loss_out);
 
 /* ------------------------------------------------------------------------ */
+/* 1b. Topology: GraphML → per-vertex-pair path tables (sg_topology.c)       */
+/* ------------------------------------------------------------------------ */
+/* Replaces topology_new / _topology_loadGraph (routing/topology.c:554-800) and
+ * the path lookup behind topology_getLatency / topology_getReliability
+ * (topology.c:1969-2087), evaluated for every vertex pair up front so the
+ * device engine does one table read per send. */
+typedef struct sg_graph sg_graph;
+
+typedef struct sg_graph_desc {
+    uint32_t n_vertices, n_edges;
+    int32_t directed;         /* graph edgedefault="directed" */
+    int32_t complete;         /* _topology_isComplete (topology.c:450-552) */
+    int32_t prefers_direct;   /* preferdirectpaths graph attribute (topology.c:760-790) */
+    double min_edge_latency_ms, max_edge_latency_ms;
+} sg_graph_desc;
+
+typedef struct sg_vertex_desc {   /* borrowed strings, NULL when absent */
+    const char *id, *ip, *citycode, *countrycode, *geocode, *type;
+    double packetloss;
+    int32_t has_packetloss;
+    uint64_t bandwidth_down, bandwidth_up;
+} sg_vertex_desc;
+
+/* Attachment hints of one host (host element attributes iphint, citycodehint,
+ * countrycodehint, geocodehint, typehint); NULL = no hint. */
+typedef struct sg_attach_hint {
+    const char *ip, *citycode, *countrycode, *geocode, *type;
+} sg_attach_hint;
+
+enum sg_path_kind {
+    SG_PATH_DIRECT = 0,   /* the edge itself (topology.c:1877-1927) */
+    SG_PATH_SHORTEST = 1, /* source shortest paths (topology.c:1655-1875, 1407-1523) */
+    SG_PATH_SELF = 2      /* shortest path to self (topology.c:1545-1653) */
+};
+
+/* Parse GraphML text (topology.c:554-800): keys by attr.name, vertices in
+ * <node> order, edges with required latency and packetloss.  A GraphML
+ * document embedded in a CDATA section is accepted as is. */
+int sg_graphml_load(const char* text, uint64_t len, sg_graph** out);
+int sg_graph_free(sg_graph* g);
+int sg_graph_info(const sg_graph* g, sg_graph_desc* out);
+int sg_graph_vertex(const sg_graph* g, uint32_t index, sg_vertex_desc* out);
+int sg_graph_edge(const sg_graph* g, uint32_t index, uint32_t* src, uint32_t* dst,
+                  double* latency_ms, double* packetloss);
+
+/* topology_attach (topology.c:2094-2369) for n_hosts hosts in registration
+ * order: hint filters, longest-prefix IP match or one random_nextDouble draw
+ * from the host's RNG (rng_state[h] is advanced in place).  hints may be NULL
+ * (no host has hints: every host draws among all vertices). */
+int sg_graph_attach(const sg_graph* g, uint32_t n_hosts, const sg_attach_hint* hints,
+                    uint32_t* rng_state, uint32_t* vertex_out);
+
+/* The path every lookup (src vertex, dst vertex) resolves to, V*V row-major:
+ * latency (ms) and reliability as _topology_getPathEntry would cache them,
+ * the kind of path, and discovered_ms = the minimum path latency the lookup
+ * makes known to the window logic (topology.c:1374-1385): the path's own
+ * latency for direct and self paths, the minimum over all the source's stored
+ * paths for shortest paths (one source run caches every attached target).
+ * attached (V flags, NULL = all) selects the shortest-path targets
+ * (_topology_getUniqueVertexTargets).  Reverse-direction cache hits of
+ * undirected incomplete graphs (topology.c:1986-1990) are not modelled. */
+int sg_graph_paths(const sg_graph* g, const uint8_t* attached, double* latency_ms,
+                   double* reliability, double* discovered_ms, uint8_t* kind);
+
+/* Device tables from path results: delay_ns = ceil(latency * 1e6)
+ * (worker.c:275-277), keep_max = sg_keep_threshold(reliability)
+ * (worker.c:268-273), jump_ms = (uint64)discovered (master.c:153; latency when
+ * discovered_ms is NULL). */
+int sg_build_path_tables(uint32_t n_vertices, const double* latency_ms, const double* reliability,
+                         const double* discovered_ms, uint64_t* delay_ns, int32_t* keep_max,
+                         uint32_t* jump_ms);
+
+/* ------------------------------------------------------------------------ */
 /* 2. Device engine (synthetic PHOLD-style workload, "Mode S")               */
 /* ------------------------------------------------------------------------ */
 

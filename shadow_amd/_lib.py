@@ -83,7 +83,8 @@ EXPORTS = [
     "sg_last_error", "sg_abi_version", "sg_rand_r", "sg_random_next_double",
     "sg_random_next_uint", "sg_seed_chain", "sg_attach_hosts", "sg_keep_threshold",
     "sg_build_paths", "sg_build_weight_thresholds", "sg_window_note_latency", "sg_window_next",
-    "sg_topology_lognormal", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
+    "sg_topology_lognormal", "sg_graphml_load", "sg_graph_free", "sg_graph_info", "sg_graph_vertex",
+    "sg_graph_edge", "sg_graph_attach", "sg_graph_paths", "sg_build_path_tables", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
     "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",

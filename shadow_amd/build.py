@@ -24,7 +24,7 @@ C_FLAGS = ["-O2", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
              "-fno-fast-math", "-Wall", "-I" + INC, "-I" + CSRC]
 
-C_SOURCES = ["sg_host.c", "sg_policy.c", "sg_sched.c"]
+C_SOURCES = ["sg_host.c", "sg_policy.c", "sg_sched.c", "sg_topology.c"]
 HIP_SOURCES = ["sg_engine.hip", "sg_policy_dev.hip"]
 
 

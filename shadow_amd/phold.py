@@ -149,6 +149,47 @@ def c5_config(n_hosts=100_000, V=256, end_time_s=10.0, load=8, loss=(0.005, 0.05
                        end_time_s=end_time_s, name=f"lossy-c5-{n_hosts}")
 
 
+def topology_config(graph, n_hosts, *, load=16, seed=1, end_time_s=10.0, hints=None,
+                    dst_rule=L.SG_DST_WEIGHTS, window_rule=L.SG_WINDOW_DISCOVERED, runahead_ms=0,
+                    fixed_jump_ms=0, bootstrap_end=0, weights=None, name=None):
+    """PHOLD on a GraphML topology (shadow_amd.topology.Graph): hosts attached
+    by topology_attach from their node seeds (host.c:176, topology.c:2094-2369),
+    paths resolved as topology.c would (direct, shortest or self), the jump table
+    carrying each lookup's discovered minimum latency (topology.c:1374-1385)."""
+    from . import topology as T
+    _, _, node = seed_chain(seed, n_hosts)
+    vertex, rng = graph.attach(node, hints)
+    attached = np.zeros(graph.n_vertices, bool)
+    attached[vertex] = True
+    lat, rel, disc, _ = graph.paths(attached)
+    delay, keep, jump = T.path_tables(lat, rel, disc)
+    wt = None
+    if dst_rule == L.SG_DST_WEIGHTS:
+        wt = weight_thresholds(np.ones(n_hosts) if weights is None else weights)
+    return dict(
+        name=name or f"phold-topology-{n_hosts}", n_hosts=n_hosts, n_vertices=graph.n_vertices,
+        load=load, seed=seed, dst_rule=dst_rule, window_rule=window_rule,
+        attach_rule=L.SG_ATTACH_RANDOM, end_time=int(round(end_time_s * 1e9)),
+        bootstrap_end=int(bootstrap_end), fixed_jump=int(fixed_jump_ms * L.ONE_MS),
+        runahead_min=int(runahead_ms * L.ONE_MS), host_vertex=vertex, host_rng=rng,
+        delay_ns=delay, keep_max=keep, jump_ms=jump, weight_thresh=wt)
+
+
+def c3_config(n_relays=2000, n_clients=8000, end_time_s=10.0, load=4, seed=1):
+    """BASELINE configs[2] shape without tgen (the plugin is not available
+    offline): 2k relay + 8k client hosts on the bundled topology, PHOLD traffic
+    over the resulting paths.  Every bundled vertex is typed "cluster", so the
+    relays carry country-code hints instead (round-robin over the topology's
+    own codes; topology.c:2180-2192 filters on them) and the clients none."""
+    from . import topology as T
+    g = T.Graph.from_file(T.BUNDLED)
+    codes = sorted({g.vertex(i)["countrycode"] for i in range(g.n_vertices)} - {None})
+    n = n_relays + n_clients
+    hints = [{"countrycode": codes[i % len(codes)]} if i < n_relays else None for i in range(n)]
+    return topology_config(g, n, load=load, seed=seed, end_time_s=end_time_s, hints=hints,
+                           name=f"tor-shape-c3-{n}")
+
+
 def tiny_config(n_hosts=64, V=4, load=4, end_time_s=0.5, loss=0.02, runahead_ms=0,
                 window_rule=L.SG_WINDOW_DISCOVERED, dst_rule=L.SG_DST_WEIGHTS, seed=7,
                 weights=None, min_ms=1.0):

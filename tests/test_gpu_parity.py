@@ -150,3 +150,26 @@ def test_queue_capacity_paths(cap):
     cfg = phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.5)
     eng, orc = _run_both(cfg, trace=200_000, queue_cap=cap)
     _assert_same(eng, orc)
+
+
+def test_c3_shape_bundled_topology():
+    """configs[2] shape: hosts attached to the reference's bundled topology
+    (country hints on the relays), direct paths of the complete graph."""
+    cfg = phold.c3_config(n_relays=400, n_clients=1600, end_time_s=0.4)
+    eng, orc = _run_both(cfg)
+    gs = _assert_same(eng, orc)
+    assert gs["pops"] > 20_000 and gs["drop_reliability"] > 0
+
+
+def test_incomplete_topology_shortest_paths():
+    """An incomplete GraphML graph: shortest paths, paths to self and
+    source-wide discovery in the jump table, the same on both sides."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_topology import _graphml, _random_graph
+    from shadow_amd import topology as T
+    rs = np.random.default_rng(11)
+    g = T.Graph(_graphml(30, _random_graph(rs, 30, 0.1), vloss=rs.uniform(0, 0.02, 30)))
+    cfg = phold.topology_config(g, 900, load=4, end_time_s=0.5)
+    eng, orc = _run_both(cfg)
+    _assert_same(eng, orc)
