@@ -513,7 +513,8 @@ __global__ void k_boot(Dev d) {
 // workgroup's due entries are staged in LDS so that every event load of a
 // pass is independent of the others.
 constexpr uint32_t GDMAX = 32;   // due entries staged per batch
-constexpr int GUNR = 4;          // events in flight per thread
+constexpr int GUNR = 4;          // events in flight per thread (two-pass path)
+constexpr int GREG = 16;         // events per thread kept in registers (one-pass path: 4 chunks)
 
 template <bool SCATTER>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
@@ -578,28 +579,85 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         s_cur[p] = 0;
     }
     uint64_t cmin = UINT64_MAX, ntomb = 0;
-    for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
-        const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
-        __syncthreads();
-        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
-        __syncthreads();
-        gather_pass<false>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
-    }
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
-        const uint32_t c = s_cnt[p];
-        if (c) {
-            const uint32_t base = atomicAdd(&d.pcnt[p], c);
-            if (base + c > d.CAPP) flag(d, OV_PART);
-            s_cnt[p] = base;
+    auto reserve = [&]() {  // one reservation per partition this workgroup feeds
+        for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
+            const uint32_t c = s_cnt[p];
+            if (c) {
+                const uint32_t base = atomicAdd(&d.pcnt[p], c);
+                if (base + c > d.CAPP) flag(d, OV_PART);
+                s_cnt[p] = base;
+            }
         }
-    }
-    for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
-        const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
+    };
+    if ((c1 - c0) * CH <= (uint64_t)GREG * K1_T) {
+        // the workgroup's chunks fit in registers: load once, count, reserve, scatter
+        const uint32_t nb = (uint32_t)(c1 - c0), tot = nb * CH;
+        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[c0 + threadIdx.x];
         __syncthreads();
-        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+        const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
+        Rec r[GREG];
+        uint32_t pp[GREG];  // partition of the event, UINT32_MAX: not gathered
+#pragma unroll
+        for (int q = 0; q < GREG; ++q) {  // every load unconditional (clamped address)
+            const uint32_t e = threadIdx.x + q * K1_T;
+            const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
+            const bool v = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
+            r[q] = d.pool[v ? ((size_t)de.id << CH_SHIFT) + (e & (CH - 1)) : 0];
+            if (!v) r[q].a = TOMB;
+        }
+#pragma unroll
+        for (int q = 0; q < GREG; ++q) {
+            pp[q] = UINT32_MAX;
+            if (r[q].a == TOMB) continue;
+            const uint32_t e = threadIdx.x + q * K1_T;
+            const uint64_t t = s_de[e >> CH_SHIFT].base + (r[q].a & M40);
+            const uint32_t dl = (uint32_t)(r[q].a >> 40);
+            if (dl >= d.L) {
+                flag(d, OV_BUG);
+                continue;
+            }
+            if (t >= E) {
+                cmin = t < cmin ? t : cmin;
+                continue;
+            }
+            pp[q] = dl >> sh;
+            r[q].a = ((uint64_t)(dl & hmask) << 52) | (t - S);  // the partition record
+            atomicAdd(&s_cnt[pp[q]], 1u);
+        }
         __syncthreads();
-        gather_pass<true>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+        reserve();
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < GREG; ++q) {
+            if (pp[q] == UINT32_MAX) continue;
+            const uint32_t p = pp[q];
+            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            if (slot < d.CAPP) d.part[(size_t)p * d.CAPP + slot] = r[q];
+            const uint32_t e = threadIdx.x + q * K1_T;
+            const DueEnt de = s_de[e >> CH_SHIFT];
+            if (de.nflags & RETAINED) {
+                d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
+                ++ntomb;
+            }
+        }
+    } else {
+        // more chunks than registers hold (the boot round): two passes over them
+        for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
+            const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
+            __syncthreads();
+            if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+            __syncthreads();
+            gather_pass<false>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+        }
+        __syncthreads();
+        reserve();
+        for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
+            const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
+            __syncthreads();
+            if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+            __syncthreads();
+            gather_pass<true>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+        }
     }
     const uint64_t m = block_min(cmin, s16);
     const uint64_t nt = block_sum(ntomb, s16);
@@ -1102,16 +1160,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                                 }
                                 ++nsd;
                             });
+                            // loads issued unconditionally (unused sends read host 0's
+                            // record): a load under a runtime condition makes hipcc
+                            // branch around it and wait for it before the next one
                             const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
-                            Probe pb0{}, pb1{};
-                            if (nsd > 0) pb0 = dst_probe(d, g0);
-                            if (nsd > 1) pb1 = dst_probe(d, g1);
+                            const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
                             uint32_t vd0 = 0, vd1 = 0;
                             const uint32_t dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
                             const uint32_t dst1 = nsd > 1 ? dst_resolve(d, x1, g1, pb1, vd1) : 0;
-                            PairRec pr0{}, pr1{};
-                            if (nsd > 0) pr0 = d.pairs[(size_t)c.vh * d.V + vd0];
-                            if (nsd > 1) pr1 = d.pairs[(size_t)c.vh * d.V + vd1];
+                            asm volatile("" ::: "memory");  // both pair loads after both resolves
+                            const PairRec pr0 = d.pairs[(size_t)c.vh * d.V + vd0];
+                            const PairRec pr1 = d.pairs[(size_t)c.vh * d.V + vd1];
                             if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, pr0, count_local);
                             if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, pr1, count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
@@ -1160,13 +1219,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const uint32_t i1 = i0 + K2_T;
         const bool v1 = i1 < nsend;
         const Rec r0 = snd[i0];
-        const Rec r1 = v1 ? snd[i1] : r0;
+        const Rec r1 = snd[v1 ? i1 : i0];  // an address select, not a conditional load
         const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
         const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
         uint32_t vd0 = 0, vd1 = 0;
         const uint32_t dst0 = dst_resolve(d, x0, g0, pb0, vd0);
         const uint32_t dst1 = dst_resolve(d, x1, g1, pb1, vd1);
+        asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
         const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
         const PairRec pr0 = d.pairs[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0];
         const PairRec pr1 = d.pairs[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1];
@@ -1382,11 +1442,42 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         if (n == 0) return;
         for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
         __syncthreads();
-        const uint64_t S = rs->ins_S;
+        const uint64_t S = rs->ins_S, W = d.W;
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
-        for (uint32_t i = threadIdx.x; i < n; i += K3_T) {
-            const Rec r = src[i];
-            place_event(d, s_cur, S + (r.a & M40), r.k, (uint32_t)(r.a >> 40));
+        // SU events per thread in flight: every load of a batch is issued
+        // before any is used (staged record, then chunk table + allocation)
+        constexpr int SU = 4;
+        for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+            Rec r[SU];
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                r[q] = src[i < n ? i : 0];
+            }
+            uint32_t rb[SU], pos[SU];
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                const uint64_t t = S + (r[q].a & M40);
+                const uint64_t b = t / W;
+                rb[q] = i < n ? (uint32_t)(b % R) : 0u;
+                pos[q] = i < n ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
+                r[q].a = (r[q].a & ~M40) | (t - b * W);  // {dst_local << 40 | offset in bucket}
+            }
+            uint32_t na[SU], id[SU];
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t ci = pos[q] >> CH_SHIFT;
+                na[q] = d.nal[rb[q]];
+                id[q] = d.btab[(size_t)rb[q] * d.NCH + (ci < d.NCH ? ci : d.NCH - 1)];
+            }
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                // beyond the allocation only when the pool ran out (k_plan flagged it)
+                if (i < n && (pos[q] >> CH_SHIFT) < na[q] && id[q] < d.NCH)
+                    d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r[q];
+            }
         }
         return;
     }
@@ -1563,11 +1654,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             const uint64_t pos = tail_r + k++;  // k < NCH: one wrap at most
             d.fring[pos >= NCH ? pos - NCH : pos] = de.id;
         }
-        for (uint64_t i = 0; i < ndb; ++i) {
-            const uint32_t rb = d.dueb[i];
-            const uint32_t nc = B.nal[rb];
-            for (uint32_t ci = tid; ci < nc; ci += PL_T) d.btab[(size_t)rb * NCH + ci] = EMPTY;
-        }
+        // (their chunk tables are not cleared: nothing reads btab past nal, which resets)
         __syncthreads();
         for (uint64_t i = tid; i < ndb; i += PL_T) {
             const uint32_t rb = d.dueb[i];
@@ -1666,10 +1753,10 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             const uint32_t rb = (uint32_t)(pr % R);
             const uint32_t nc = B.nal[rb];
             const uint64_t tail = s_tail;
+            const uint32_t tail_r = (uint32_t)(tail % NCH);
             for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-                uint32_t* e = &d.btab[(size_t)rb * NCH + ci];
-                d.fring[(tail + ci) % NCH] = *e;
-                *e = EMPTY;
+                const uint32_t pos = tail_r + ci;  // nc <= NCH: one wrap at most
+                d.fring[pos >= NCH ? pos - NCH : pos] = d.btab[(size_t)rb * NCH + ci];
             }
             __syncthreads();
             if (tid == 0) {
