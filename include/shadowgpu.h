@@ -352,6 +352,17 @@ enum sg_kernel_class {
 int sg_engine_kernel_times(sg_engine* e, double* ms, uint64_t* launches);
 int sg_engine_set_timing(sg_engine* e, int enabled);
 
+/* Path packet counters (topology_incrementPathPacketCounter, topology.c:2053-2063,
+ * counted where worker_sendPacket calls it: every send that passes the
+ * reliability test, worker.c:273-279).  enable != 0 allocates a V*V table of
+ * kept sends per (source vertex, destination vertex) and zeroes it; counting
+ * costs one atomic per kept send, so it is off by default.  The reference keeps
+ * one Path per cached direction, so on undirected graphs its count for {s, d}
+ * is table[s][d] + table[d][s].  path_counts copies the table (n_out = V*V, or
+ * 0 while off); sum the tables of all shards. */
+int sg_engine_path_counters(sg_engine* e, int enable);
+int sg_engine_path_counts(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out);
+
 /* ------------------------------------------------------------------------ */
 /* 3. The `gpu` SchedulerPolicy ("Mode P", the drop-in boundary)            */
 /* ------------------------------------------------------------------------ */

@@ -84,6 +84,8 @@ def lib():
         L.orc_trace.restype = C.c_size_t
         L.orc_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orc_windows.restype = C.c_size_t
+        L.orc_path_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orc_path_counts.restype = C.c_size_t
         L.orc_probe_hash.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.orc_probe_hash.restype = C.c_uint64
         L.orc_digest_mix.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64]
@@ -243,6 +245,12 @@ class Sim:
         out = np.zeros(2 * n, np.uint64)
         lib().orc_windows(self.h, out.ctypes.data, n)
         return out.reshape(n, 2)
+
+    def path_counts(self) -> np.ndarray:
+        n = lib().orc_path_counts(self.h, None, 0)
+        out = np.zeros(n, np.uint64)
+        lib().orc_path_counts(self.h, out.ctypes.data, n)
+        return out
 
     def probe_hash(self):
         m = C.c_uint64()

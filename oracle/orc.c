@@ -133,6 +133,7 @@ struct orc_sim {
     /* message-only per-host traces for the probe hash */
     uint64_t* win;
     size_t n_win, cap_win;
+    uint64_t* pcount; /* [V*V] path packet counters (topology.c:2053-2063) */
 };
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
@@ -174,9 +175,10 @@ orc_sim* orc_create(const orc_params* p, const uint32_t* host_vertex, const uint
     s->pops = (uint64_t*)calloc(L, 8);
     s->digest = (uint64_t*)calloc(L, 8);
     s->rng_state = (uint32_t*)malloc(L * 4);
+    s->pcount = (uint64_t*)calloc(VV, 8);
     if (p->trace_capacity) s->trace = (orc_trace_rec*)malloc(p->trace_capacity * sizeof(orc_trace_rec));
     if (!s->vertex || !s->rng || !s->delay || !s->keep || !s->jump || !s->wthresh || !s->q || !s->ev ||
-        !s->pops || !s->digest || !s->rng_state || (p->trace_capacity && !s->trace)) {
+        !s->pops || !s->digest || !s->rng_state || !s->pcount || (p->trace_capacity && !s->trace)) {
         orc_destroy(s);
         snprintf(orc_err, sizeof orc_err, "orc_create: out of memory");
         return NULL;
@@ -212,6 +214,7 @@ void orc_destroy(orc_sim* s) {
     free(s->out);
     free(s->trace);
     free(s->win);
+    free(s->pcount);
     free(s);
 }
 
@@ -289,6 +292,7 @@ static int send_one(orc_sim* s, uint32_t h, uint32_t* rng, uint64_t now, uint64_
         s->st.drop_reliability++;
         return 0;
     }
+    s->pcount[pair]++; /* topology_incrementPathPacketCounter, worker.c:279 */
     orc_event e;
     e.time = now + s->delay[pair];
     e.dst = d;
@@ -576,4 +580,10 @@ void orc_weight_thresholds(uint32_t n, const double* w, int32_t* out) {
         cum += w[i] / total;
         out[i] = orc_prefix(cum);
     }
+}
+
+size_t orc_path_counts(orc_sim* s, uint64_t* out, size_t cap) {
+    const size_t n = (size_t)s->p.n_vertices * s->p.n_vertices;
+    if (out) memcpy(out, s->pcount, (n < cap ? n : cap) * 8);
+    return n;
 }

@@ -80,6 +80,8 @@ size_t orc_windows(orc_sim* s, uint64_t* out_pairs, size_t cap_pairs);
 /* Trace hash of the survey probe (SURVEY.md §0 key finding 2): chained over
  * hosts in index order and each host's message pops in pop order. */
 uint64_t orc_probe_hash(orc_sim* s, uint64_t* n_msgs);
+/* Kept sends per (source vertex, destination vertex), V*V (topology.c:2053-2063). */
+size_t orc_path_counts(orc_sim* s, uint64_t* out, size_t cap);
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq);
 

@@ -154,6 +154,7 @@ struct Dev {
     const HostInfo* hinfo;    // [N]
     const PairRec* pairs;     // [V*V]
     const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
+    uint32_t* pcount;         // [V*V] path packet counters (topology.c:2053-2063), or null
     HostState* hs;            // [L]
     // calendar
     Rec* pool;                // [NCH][CH]
@@ -761,6 +762,7 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             ++a.ctr[C_DROPREL];
             continue;
         }
+        if (d.pcount) atomicAdd(&d.pcount[(size_t)c.vh * d.V + di.vertex], 1u);  // worker.c:279
         uint64_t tn = bt + pr.delay;        // worker.c:275-277
         const uint64_t sq = c.s.evc++;      // event.c:38
         if (tn >= d.end_time) {             // scheduler.c:343-346
@@ -788,12 +790,13 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
 template <class Count>
 __device__ __forceinline__ void commit_send(const Dev& d, uint64_t S, uint64_t E, uint32_t part, HostCtx& c,
                                             Acc& a, ProcShared& sh, uint64_t bt, int32_t ch, uint32_t dst,
-                                            const PairRec& pr, Count count) {
+                                            uint32_t vd, const PairRec& pr, Count count) {
     a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
     if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
         ++a.ctr[C_DROPREL];
         return;
     }
+    if (d.pcount) atomicAdd(&d.pcount[(size_t)c.vh * d.V + vd], 1u);  // worker.c:279
     uint64_t tn = bt + pr.delay;
     const uint64_t sq = c.s.evc++;
     if (tn >= d.end_time) {
@@ -1171,8 +1174,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             asm volatile("" ::: "memory");  // both pair loads after both resolves
                             const PairRec pr0 = d.pairs[(size_t)c.vh * d.V + vd0];
                             const PairRec pr1 = d.pairs[(size_t)c.vh * d.V + vd1];
-                            if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, pr0, count_local);
-                            if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, pr1, count_local);
+                            if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, vd0, pr0, count_local);
+                            if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, vd1, pr1, count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
                             hp[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
                             hp[1] = make_ulonglong2(c.s.digest, c.s.evc);
@@ -1235,6 +1238,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
             a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
             const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
+            if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
             snd[i0] = Rec{((uint64_t)keep << 63) | (bt + pr0.delay - S), dst0};  // worker.c:275-277
         }
         if (v1) {
@@ -1242,6 +1246,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
             a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
             const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
+            if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1], 1u);
             snd[i1] = Rec{((uint64_t)keep << 63) | (bt + pr1.delay - S), dst1};
         }
     }
@@ -1948,6 +1953,7 @@ struct sg_engine {
     bool own_stream;
     bool booted;
     std::vector<void*> allocs;
+    uint32_t* pcount_buf = nullptr;  // path packet counters, once enabled
     RoundState* h_rs;  // pinned
     unsigned long long* d_pend;
     bool timing;
@@ -2600,6 +2606,37 @@ int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n
     if (out && capacity && n) {
         HIPCHK(hipStreamSynchronize(e->stream));
         HIPCHK(hipMemcpy(out, e->d.stamps, (n < capacity ? n : capacity) * 8, hipMemcpyDeviceToHost));
+    }
+    return SG_OK;
+}
+
+int sg_engine_path_counters(sg_engine* e, int enable) {
+    if (!e) return SG_ERR_INVAL;
+    HIPCHK(hipSetDevice(e->device));
+    if (!enable) {
+        e->d.pcount = nullptr;  // the table stays allocated until destroy
+        return SG_OK;
+    }
+    const size_t VV = (size_t)e->d.V * e->d.V;
+    if (!e->pcount_buf) {
+        int rc = dalloc(e, &e->pcount_buf, VV);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemsetAsync(e->pcount_buf, 0, VV * sizeof(uint32_t), e->stream));
+    e->d.pcount = e->pcount_buf;
+    return SG_OK;
+}
+
+int sg_engine_path_counts(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
+    if (!e) return SG_ERR_INVAL;
+    const uint64_t n = e->d.pcount ? (uint64_t)e->d.V * e->d.V : 0;
+    if (n_out) *n_out = n;
+    if (out && capacity && n) {
+        const uint64_t m = n < capacity ? n : capacity;
+        std::vector<uint32_t> tmp(m);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(tmp.data(), e->d.pcount, m * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < m; ++i) out[i] = tmp[i];
     }
     return SG_OK;
 }

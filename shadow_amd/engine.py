@@ -111,6 +111,18 @@ class Engine:
             L.check(L.lib().sg_engine_windows(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out.reshape(-1, 2)
 
+    def path_counters(self, enable: bool = True):
+        """Count kept sends per (src vertex, dst vertex) from now on (zeroed)."""
+        L.check(L.lib().sg_engine_path_counters(self.h, int(enable)))
+
+    def path_counts(self) -> np.ndarray:
+        n = C.c_uint64()
+        L.check(L.lib().sg_engine_path_counts(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.uint64)
+        if n.value:
+            L.check(L.lib().sg_engine_path_counts(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out
+
     def set_timing(self, on: bool):
         L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
 

@@ -173,3 +173,42 @@ def test_incomplete_topology_shortest_paths():
     cfg = phold.topology_config(g, 900, load=4, end_time_s=0.5)
     eng, orc = _run_both(cfg)
     _assert_same(eng, orc)
+
+
+def test_pop_trace_diff_tool():
+    """The trace tool on the device and oracle pop traces of the same config."""
+    from shadow_amd import trace as T
+    cfg = phold.tiny_config(n_hosts=256, V=6, load=4, end_time_s=0.3, loss=0.05)
+    eng, orc = _run_both(cfg, trace=1 << 20)
+    r = T.diff(eng.trace(), orc.trace())
+    assert r["identical"] and r["pops_a"] == eng.stats()["pops"] > 0
+
+
+@pytest.mark.parametrize("kind", ["lossy", "bootstrap_heavy"])
+def test_path_packet_counters(kind):
+    """topology_incrementPathPacketCounter (topology.c:2053-2063): kept sends per
+    vertex pair, identical to the oracle's, across the inline, phase B and
+    same-round paths of k_proc."""
+    cfg = {"lossy": lambda: phold.tiny_config(n_hosts=300, V=7, load=4, end_time_s=0.4, loss=0.2),
+           "bootstrap_heavy": lambda: dict(phold.tiny_config(n_hosts=200, V=5, load=24, end_time_s=0.3,
+                                                             loss=0.3), bootstrap_end=50_000_000)}[kind]()
+    eng = Engine(cfg)
+    eng.path_counters(True)
+    eng.boot()
+    eng.run()
+    orc = O.Sim(cfg)
+    orc.boot()
+    orc.run()
+    _assert_same(eng, orc)
+    g, o = eng.path_counts(), orc.path_counts()
+    assert g.sum() > 0 and np.array_equal(g, o)
+    st = orc.stats()
+    assert int(o.sum()) == st["sends"] - st["drop_reliability"]
+
+
+def test_path_counters_off_by_default():
+    cfg = phold.tiny_config(n_hosts=64)
+    eng = Engine(cfg)
+    eng.boot()
+    eng.run(5)
+    assert eng.path_counts().size == 0
