@@ -345,7 +345,7 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
 enum sg_kernel_class {
     SG_K_PROCESS = 0,  /* k_proc: per-host pops + PHOLD body + send resolution */
     SG_K_INSERT = 1,   /* k_ins: new / received events into time buckets */
-    SG_K_PLAN = 2,     /* k_plan (+ k_locmin, k_pack, k_fill when sharded) */
+    SG_K_PLAN = 2,     /* k_plan (+ k_fill when sharded) */
     SG_K_GATHER = 3,   /* k_gather: due chunks → host partitions */
     SG_KCLASSES = 4
 };

@@ -32,9 +32,11 @@
 //   k_scatter   the counted events into their reserved chunk slots.
 // Chunk tables are written only by k_boot / k_plan and read by later kernels,
 // so no workgroup ever waits on another inside a launch.
-//   multi-shard k_locmin / k_pack / k_fill build the fixed-size exchange blocks
-//               (the header carries the shard's MIN terms); k_plan reads the G
-//               headers back instead of the local minima.
+//   multi-shard k_proc also writes the events for other shards into per-peer
+//               outbox regions (one reservation per peer and partition);
+//               k_fill builds the fixed-size exchange blocks (the header
+//               carries the shard's MIN terms); k_plan reads the G headers back
+//               instead of the local minima.
 //
 // HBM layout: 16-B records everywhere.
 //   bucket record     {dst_local << 40 | (t - b*W),  src << 40 | srcHostEventID}
@@ -137,8 +139,6 @@ struct RoundState {
     uint64_t ins_S;          // their window start (staged times are relative to it)
     // multi-shard step protocol
     uint64_t phase;      // 0: process step, 1: drain step (outbox leftovers only)
-    uint64_t loc_min;    // this shard's MIN next time of the round being exchanged
-    uint64_t loc_jmin;   // this shard's cumulative min discovered latency (ms)
     uint64_t steps;      // exchange steps executed
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
 };
@@ -184,10 +184,8 @@ struct Dev {
     uint32_t* remn;           // [P] staged events for other shards
     Slot* rem;                // [P][ECAP]
     uint32_t* rem_dst;        // [P][ECAP]
-    uint32_t* peercnt;        // [P][G]
-    uint32_t* peeroff;        // [P][G]
-    int64_t* outq;            // [P*ECAP][3] per-peer outbox, peer p at peer_base[p]
-    uint64_t* peer_base;      // [G]
+    int64_t* outq;            // [G][oreg][3] per-peer outbox regions
+    uint64_t oreg;            // rows per peer region (P * ECAP: every staged event fits)
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
@@ -496,15 +494,12 @@ __global__ void k_boot(Dev d) {
         rs->ins_local = 0;
         rs->ins_S = 0;
         rs->phase = 0;
-        rs->loc_min = SIMTIME_MAX;
-        rs->loc_jmin = UINT64_MAX;
         rs->steps = 0;
         rs->peak_peer = 0;
     }
     if (i < d.G && d.outn) {
         d.outn[i] = 0;
         d.sent[i] = 0;
-        d.peer_base[i] = 0;
     }
 }
 
@@ -575,6 +570,10 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
     const uint64_t nd = rs->ndue;
     const uint64_t c0 = nd * blockIdx.x / gridDim.x, c1 = nd * (blockIdx.x + 1) / gridDim.x;
     const uint32_t P = d.P;
+    if (d.outn && blockIdx.x == 0 && threadIdx.x < d.G) {  // a process step refills the outboxes
+        d.outn[threadIdx.x] = 0;
+        d.sent[threadIdx.x] = 0;
+    }
     for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
@@ -917,6 +916,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ ProcShared sh;
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
+    __shared__ uint32_t s_obase[MAXG], s_oslot[MAXG];
     const uint64_t S = rs->S, E = rs->E;
     const uint32_t p = blockIdx.x;
     const uint32_t tid = threadIdx.x;
@@ -1286,6 +1286,28 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.hs[h - d.lo].evc = evc;
     }
     __syncthreads();  // staging done: sh.nloc final, bins complete
+    if (d.outn) {
+        // multi-shard: the partition's events for other shards into their peers'
+        // outbox regions, one reservation per peer
+        if (tid < d.G) {
+            s_oslot[tid] = 0;
+            s_obase[tid] = sh.peer[tid] ? (uint32_t)atomicAdd((unsigned long long*)&d.outn[tid],
+                                                              (unsigned long long)sh.peer[tid]) : 0u;
+        }
+        __syncthreads();
+        const uint32_t nr = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
+        for (uint32_t i = tid; i < nr; i += K2_T) {
+            const size_t so = (size_t)p * d.ECAP + i;
+            const uint32_t dst = d.rem_dst[so];
+            const uint32_t q = owner_of(d, dst);
+            const uint64_t slot = (uint64_t)q * d.oreg + s_obase[q] + atomicAdd(&s_oslot[q], 1u);
+            const Slot ev = d.rem[so];
+            int64_t* o = d.outq + slot * 3;
+            o[0] = (int64_t)ev.t;
+            o[1] = (int64_t)ev.k;
+            o[2] = (int64_t)dst;
+        }
+    }
     if (stamp && tid == 0) stamp[13] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nl = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
     if (horizon) flag(d, OV_HORIZON);
@@ -1328,7 +1350,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
-    if (d.peercnt && tid < d.G) d.peercnt[(size_t)p * d.G + tid] = sh.peer[tid];
     if (stamp && tid == 0) {
         stamp[4] = __builtin_amdgcn_s_memrealtime();
         stamp[5] = n;
@@ -1834,92 +1855,38 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
 }
 
 // --------------------------------------------------------- multi-shard ----
-// After k_proc on a process step: this shard's MIN terms (for the header) and
-// the per-(partition, peer) outbox offsets.
-__global__ __launch_bounds__(PL_T) void k_locmin(Dev d) {
-    RoundState* rs = d.rs;
-    if (rs->done | rs->phase) return;
-    __shared__ uint64_t s16[16];
-    __shared__ uint64_t s_tot[MAXG];
-    uint64_t m, j;
-    reduce_local(d, s16, m, j);
-    const uint32_t P = d.P, G = d.G;
-    const uint32_t chunk = (P + PL_T - 1) / PL_T;
-    const uint32_t b0 = threadIdx.x * chunk;
-    const uint32_t b1 = b0 + chunk < P ? b0 + chunk : P;
-    for (uint32_t p = 0; p < G; ++p) {
-        uint64_t sum = 0;
-        for (uint32_t b = b0; b < b1; ++b) sum += d.peercnt[(size_t)b * G + p];
-        uint64_t tot;
-        uint64_t run = block_excl_scan(sum, s16, &tot);
-        for (uint32_t b = b0; b < b1; ++b) {
-            const size_t k = (size_t)b * G + p;
-            d.peeroff[k] = (uint32_t)run;
-            run += d.peercnt[k];
-        }
-        if (threadIdx.x == 0) s_tot[p] = tot;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        rs->loc_min = m;
-        rs->loc_jmin = j;
-        uint64_t base = 0, peak = rs->peak_peer;
-        for (uint32_t p = 0; p < G; ++p) {
-            const uint64_t n = p == d.g ? 0 : s_tot[p];
-            d.peer_base[p] = base;
-            d.outn[p] = n;
-            d.sent[p] = 0;
-            base += n;
-            peak = n > peak ? n : peak;
-        }
-        rs->peak_peer = peak;
-    }
-}
-
-// Multi-shard, process steps: staged events owned by other shards → outbox
-// triples {time, key, dst}, grouped by owner.  One workgroup per partition.
-__global__ __launch_bounds__(256) void k_pack(Dev d) {
-    if (d.rs->done | d.rs->phase) return;
-    __shared__ uint32_t s_slot[MAXG];
-    if (threadIdx.x < MAXG) s_slot[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = d.remn[b];
-    for (uint32_t i = threadIdx.x; i < n; i += 256) {
-        const size_t so = (size_t)b * d.ECAP + i;
-        const uint32_t dst = d.rem_dst[so];
-        const uint32_t p = owner_of(d, dst);
-        const uint64_t slot = d.peer_base[p] + d.peeroff[(size_t)b * d.G + p] + atomicAdd(&s_slot[p], 1u);
-        const Slot s = d.rem[so];
-        int64_t* o = d.outq + slot * 3;
-        o[0] = (int64_t)s.t;
-        o[1] = (int64_t)s.k;
-        o[2] = (int64_t)dst;
-    }
-}
-
 // Every step: up to xcap outbox events per peer into the peer's exchange
 // block, behind the header {n, sender has more, MIN next, min jump, overflow,
-// round}.  Grid (chunks, G).
+// round}.  Grid (chunks, G).  The header's MIN terms are this shard's
+// reduce_local of the step's process partials (unchanged on drain steps, so
+// a drain step repeats them).
 __global__ __launch_bounds__(256) void k_fill(Dev d, int64_t* send) {
-    const RoundState* rs = d.rs;
+    RoundState* rs = d.rs;
     if (rs->done) return;
+    __shared__ uint64_t s16[16];
     const uint32_t p = blockIdx.y;
     const uint64_t left = d.outn[p] - d.sent[p];
     const uint64_t n = left < d.xcap ? left : d.xcap;
     int64_t* blk = send + (size_t)p * d.xrows * 3;
-    const int64_t* src = d.outq + (d.peer_base[p] + d.sent[p]) * 3;
+    const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * 3;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n * 3; i += (uint64_t)gridDim.x * 256)
         blk[HDR * 3 + i] = src[i];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        uint64_t more = 0;
-        for (uint32_t q = 0; q < d.G; ++q) more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
+    if (blockIdx.x != 0) return;
+    uint64_t m, j;
+    reduce_local(d, s16, m, j);  // the whole block (barriers inside)
+    if (threadIdx.x == 0) {
+        uint64_t more = 0, peak = rs->peak_peer;
+        for (uint32_t q = 0; q < d.G; ++q) {
+            more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
+            peak = q != d.g && d.outn[q] > peak ? d.outn[q] : peak;
+        }
         blk[H_N] = (int64_t)n;
         blk[H_MORE] = (int64_t)more;
-        blk[H_MIN] = (int64_t)rs->loc_min;
-        blk[H_JMIN] = (int64_t)rs->loc_jmin;
+        blk[H_MIN] = (int64_t)m;
+        blk[H_JMIN] = (int64_t)j;
         blk[H_OVF] = (int64_t)rs->overflow;
         blk[H_ROUND] = (int64_t)rs->rounds;
+        if (p == 0) rs->peak_peer = peak;
     }
 }
 
@@ -2238,10 +2205,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         ALLOC(D.remn, P);
         ALLOC(D.rem, P * D.ECAP);
         ALLOC(D.rem_dst, P * D.ECAP);
-        ALLOC(D.peercnt, P * G);
-        ALLOC(D.peeroff, P * G);
-        ALLOC(D.outq, P * D.ECAP * 3);
-        ALLOC(D.peer_base, G);
+        D.oreg = (uint64_t)P * D.ECAP;
+        ALLOC(D.outq, (size_t)G * D.oreg * 3);
         ALLOC(D.outn, G);
         ALLOC(D.sent, G);
     }
@@ -2583,8 +2548,6 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
     if ((rc = enqueue_process(e))) return rc;
     const Dev& d = e->d;
     return timed_launch(e, SG_K_PLAN, [&] {
-        hipLaunchKernelGGL(k_locmin, dim3(1), dim3(PL_T), 0, e->stream, d);
-        hipLaunchKernelGGL(k_pack, dim3(d.P), dim3(256), 0, e->stream, d);
         hipLaunchKernelGGL(k_fill, dim3(fill_chunks(d), d.G), dim3(256), 0, e->stream, d, send);
     });
 }

@@ -104,7 +104,7 @@ class EngineShard:
 
 
 def _all_to_all(recv: torch.Tensor, send: torch.Tensor):
-    if send.is_cuda and dist.get_backend() == "gloo":
+    if send.is_cuda and _backend() == "gloo":
         # rehearsal only (several ranks on one GPU, where RCCL refuses to run):
         # gloo exchanges host tensors
         r = torch.empty(send.shape, dtype=send.dtype)
@@ -112,6 +112,18 @@ def _all_to_all(recv: torch.Tensor, send: torch.Tensor):
         recv.copy_(r)
     else:
         dist.all_to_all_single(recv, send)
+
+
+_BACKEND = None
+
+
+def _backend():
+    """The default group's backend, looked up once (the step loop is host-bound
+    on small shards: every microsecond of Python per step shows)."""
+    global _BACKEND
+    if _BACKEND is None:
+        _BACKEND = dist.get_backend()
+    return _BACKEND
 
 
 def run_step(shard, world: int):
@@ -199,6 +211,8 @@ def bench(args):
     tmax = float(t.item())
     total, rounds_sum, steps_sum, ovf = (int(x) for x in tot.tolist())
     dist.destroy_process_group()
+    global _BACKEND
+    _BACKEND = None
     if ovf:
         raise SystemExit(f"queue/outbox overflow during bench ({ovf:#x})")
     if rank != 0:
