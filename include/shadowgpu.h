@@ -313,8 +313,9 @@ typedef struct sg_engine_geom {
 int sg_engine_geometry(sg_engine* e, sg_engine_geom* out);
 /* Profiling hook: with SG_STAMPS=1 in the environment at create, k_proc records
  * per workgroup {start, sorted, phase A, phase B, end} s_memrealtime ticks
- * (100 MHz) and {due events, active hosts, sends} of the last round, 8 u64 per
- * partition; *n_out = 0 when the hook is off. */
+ * (100 MHz), {due events, active hosts, sends} and finer phase stamps of the
+ * last round in a row of 32 u64 per partition, plus one row for k_plan;
+ * *n_out = 0 when the hook is off. */
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out);
 
 /* Multi-shard step, driven by the caller around ONE all-to-all per step (no

@@ -113,6 +113,10 @@ struct PairRec {
     int32_t keep;     // max rand_r value kept     (worker.c:268-273)
     uint32_t jump;    // (uint64)latency_ms        (master.c:153)
 };
+// Path-record formats: the narrow ones cut the one random read per send to
+// 8 or 4 bytes, so the V*V table stays in an XCD's L2.
+enum PairFmt : uint32_t { PAIR_WIDE = 0, PAIR_NARROW = 1, PAIR_DELAY = 2 };
+
 struct HostState {
     uint32_t rng;     // host Random (host.c:176)
     uint32_t pad;
@@ -152,7 +156,15 @@ struct Dev {
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
-    const PairRec* pairs;     // [V*V]
+    const uint16_t* vtab16;   // [N] attachment vertex only, when dst_exact
+    uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
+    uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
+    const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
+    const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
+    const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
+    const uint32_t* pjump;    // [V*V] discovered ms (narrow formats), read only while it can matter
+    uint32_t pair_fmt;        // PAIR_WIDE / PAIR_NARROW / PAIR_DELAY
+    uint64_t gjmin;           // smallest discovered ms of any pair: jmin can fall no lower
     const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
     uint32_t* pcount;         // [V*V] path packet counters (topology.c:2053-2063), or null
     HostState* hs;            // [L]
@@ -189,12 +201,30 @@ struct Dev {
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
-    uint64_t* stamps;         // [P][16] k_proc phase stamps + [16] k_plan's (SG_STAMPS=1), else null
+    uint64_t* stamps;         // [P][SG_STAMP_W] k_proc phase stamps + [SG_STAMP_W] k_plan's (SG_STAMPS=1), else null
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
     RoundState* rs;
 };
+
+// The path record of vertex pair idx.  want_jump: the discovery minimum can
+// still fall (rs->jmin > gjmin); otherwise the jump field is not read
+// (UINT32_MAX: it could not lower the minimum anyway).
+__device__ __forceinline__ PairRec load_pair(const Dev& d, size_t idx, bool want_jump) {
+    if (d.pair_fmt == PAIR_WIDE) return d.pairs[idx];
+    PairRec pr;
+    if (d.pair_fmt == PAIR_NARROW) {
+        const uint2 v = d.pairs8[idx];
+        pr.delay = v.x;
+        pr.keep = (int32_t)v.y;
+    } else {
+        pr.delay = d.pdelay[idx];
+        pr.keep = SG_RAND_MAX;
+    }
+    pr.jump = want_jump ? d.pjump[idx] : UINT32_MAX;
+    return pr;
+}
 
 __device__ __forceinline__ int32_t dev_rand_r(uint32_t& state) {
     // glibc rand_r, utility/random.c:32-37
@@ -352,15 +382,21 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 }
 
 // Workgroup-wide reductions through a [16] LDS scratch (blocks of <= 1024);
-// every thread of the block must call them.
+// every thread of the block must call them.  The 16 wave partials are read
+// from clamped slots, unconditionally, so all the LDS reads are in flight at
+// once (a read under a condition waits for itself).
 __device__ __forceinline__ uint64_t block_min(uint64_t v, uint64_t* s16) {
     v = wave_min(v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
     __syncthreads();
     if (lane == 0) s16[wid] = v;
     __syncthreads();
-    uint64_t r = s16[0];
-    for (int w = 1; w < nw; ++w) r = s16[w] < r ? s16[w] : r;
+    uint64_t r = UINT64_MAX;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint64_t x = s16[w < nw ? w : 0];  // slot 0 again: harmless for a min
+        r = x < r ? x : r;
+    }
     return r;
 }
 __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
@@ -370,27 +406,46 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
     if (lane == 0) s16[wid] = v;
     __syncthreads();
     uint64_t r = 0;
-    for (int w = 0; w < nw; ++w) r += s16[w];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint64_t x = s16[w < nw ? w : 0];
+        r += w < nw ? x : 0;
+    }
     return r;
 }
-// Exclusive scan across the workgroup; *total gets the sum.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s16, uint64_t* total) {
+// Inclusive scan of a u32 over the wave with DPP row shifts and broadcasts
+// (no LDS round trips).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+// Exclusive scan across the workgroup of two packed u32 counts (hi << 32 | lo;
+// neither total may overflow 32 bits); *total gets the sums.
+__device__ __forceinline__ uint64_t block_excl_scan_2x32(uint64_t v, uint64_t* s16, uint64_t* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    uint64_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t u = __shfl_up(x, o, 64);
-        if (lane >= o) x += u;
-    }
-    __syncthreads();
+    const uint32_t lo = wave_incl_scan_u32((uint32_t)v), hi = wave_incl_scan_u32((uint32_t)(v >> 32));
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    __syncthreads();  // s16 may still be read by a previous use
     if (lane == 63) s16[wid] = x;
     __syncthreads();
     uint64_t add = 0, tot = 0;
-    for (int w = 0; w < nw; ++w) {
-        if (w < wid) add += s16[w];
-        tot += s16[w];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint64_t y = s16[w < nw ? w : 0];
+        add += w < wid ? y : 0;
+        tot += w < nw ? y : 0;
     }
     *total = tot;
     return x - v + add;
+}
+// Exclusive scan of u32 counts whose workgroup total fits 32 bits.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s16, uint64_t* total) {
+    return block_excl_scan_2x32((uint32_t)v, s16, total);
 }
 
 // Wave-aggregated LDS reservations: one atomic per wave instead of one per
@@ -754,7 +809,7 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             continue;
         }
         ++a.ctr[C_SENDS];
-        const PairRec pr = d.pairs[(size_t)c.vh * d.V + di.vertex];
+        const PairRec pr = load_pair(d, (size_t)c.vh * d.V + di.vertex, d.rs->jmin > d.gjmin);
         a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
         const int32_t ch = dev_rand_r(c.s.rng);          // worker.c:268-269
         if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
@@ -871,8 +926,20 @@ __device__ __forceinline__ void sort_segment(Rec* seg, uint32_t cnt) {
     }
 }
 
+__device__ __forceinline__ Rec opaque_rec(const Rec (&rq)[4], uint32_t u) {
+    // a select of values (not of addresses: rq stays in registers)
+    uint64_t a = rq[0].a, k = rq[0].k;
+    a = u == 1 ? rq[1].a : a;
+    k = u == 1 ? rq[1].k : k;
+    a = u == 2 ? rq[2].a : a;
+    k = u == 2 ? rq[2].k : k;
+    a = u == 3 ? rq[3].a : a;
+    k = u == 3 ? rq[3].k : k;
+    return Rec{opaque(a), opaque(k)};
+}
 // Diagnostics (SG_STAMPS): a timestamp once this wave's outstanding memory
 // operations have landed.
+constexpr uint32_t SG_STAMP_W = 32;  // stamp slots per workgroup row
 __device__ __forceinline__ uint64_t wait_stamp() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     return __builtin_amdgcn_s_memrealtime();
@@ -918,9 +985,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
     __shared__ uint32_t s_obase[MAXG], s_oslot[MAXG];
     const uint64_t S = rs->S, E = rs->E;
+    const bool want_jump = rs->jmin > d.gjmin;  // discovery can still lower the window's jump
     const uint32_t p = blockIdx.x;
     const uint32_t tid = threadIdx.x;
-    uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * 16 : nullptr;
+    uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
@@ -951,6 +1019,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             rr[q] = i < n ? part[i] : Rec{0, 0};
         }
     }
+    if (stamp && tid == 0) stamp[20] = wait_stamp();
     __syncthreads();
     if (in_lds) {
 #pragma unroll
@@ -960,6 +1029,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
         }
+        // the records are in registers now: re-defining them through asm keeps
+        // the scatter below from waiting on the state prefetch (vmcnt(0))
+#pragma unroll
+        for (uint32_t q = 0; q < EPT; ++q) {
+            rr[q].a = opaque(rr[q].a);
+            rr[q].k = opaque(rr[q].k);
+        }
     } else {
         for (uint32_t i = tid; i < n; i += K2_T) {
             const uint32_t hl = (uint32_t)(part[i].a >> 52);
@@ -968,6 +1044,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     __syncthreads();
+    if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
     const uint32_t h0 = tid * per;
@@ -980,7 +1057,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     uint64_t tot;
-    uint64_t run = block_excl_scan(mine, s16, &tot);
+    uint64_t run = block_excl_scan_2x32(mine, s16, &tot);
     for (uint32_t j = 0; j < per; ++j) {
         const uint32_t h = h0 + j;
         if (h < HP) {
@@ -992,6 +1069,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     const uint32_t nact = (uint32_t)tot;
     __syncthreads();
+    if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
     const uint32_t hbase = d.lo + p * HP;
     // phase A's first NPRE hosts of every lane: state loads issued now, under
     // the LDS scatter below
@@ -1145,7 +1223,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                                 ++ns;
                             }
                         }
-                        if (ns <= 2) {
+                        if (ns <= d.light_max && q < d.light_q) {
                             // light host (most hosts in steady state): the whole
                             // body here, both sends' loads in flight together
                             int32_t x0 = 0, x1 = 0, c0 = 0, c1 = 0;
@@ -1163,21 +1241,32 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                                 }
                                 ++nsd;
                             });
+                            if (st0) stamp[16] = wait_stamp();
                             // loads issued unconditionally (unused sends read host 0's
                             // record): a load under a runtime condition makes hipcc
                             // branch around it and wait for it before the next one
                             const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
-                            const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
-                            uint32_t vd0 = 0, vd1 = 0;
-                            const uint32_t dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
-                            const uint32_t dst1 = nsd > 1 ? dst_resolve(d, x1, g1, pb1, vd1) : 0;
+                            uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
+                            if (d.dst_exact) {  // launch-uniform: one 2-byte read per send
+                                vd0 = d.vtab16[g0];
+                                vd1 = d.vtab16[g1];
+                                dst0 = g0;
+                                dst1 = g1;
+                            } else {
+                                const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
+                                dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
+                                dst1 = nsd > 1 ? dst_resolve(d, x1, g1, pb1, vd1) : 0;
+                            }
+                            if (st0) stamp[17] = wait_stamp();
                             asm volatile("" ::: "memory");  // both pair loads after both resolves
-                            const PairRec pr0 = d.pairs[(size_t)c.vh * d.V + vd0];
-                            const PairRec pr1 = d.pairs[(size_t)c.vh * d.V + vd1];
+                            const PairRec pr0 = load_pair(d, (size_t)c.vh * d.V + vd0, want_jump);
+                            const PairRec pr1 = load_pair(d, (size_t)c.vh * d.V + vd1, want_jump);
+                            if (st0) stamp[18] = wait_stamp();
                             if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, vd0, pr0, count_local);
                             if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, vd1, pr1, count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
                             hp[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
+                            if (st0) stamp[19] = wait_stamp();
                             hp[1] = make_ulonglong2(c.s.digest, c.s.evc);
                             ns = 0;
                         } else {
@@ -1225,14 +1314,21 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const Rec r1 = snd[v1 ? i1 : i0];  // an address select, not a conditional load
         const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
-        const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
-        uint32_t vd0 = 0, vd1 = 0;
-        const uint32_t dst0 = dst_resolve(d, x0, g0, pb0, vd0);
-        const uint32_t dst1 = dst_resolve(d, x1, g1, pb1, vd1);
+        uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
+        if (d.dst_exact) {
+            vd0 = d.vtab16[g0];
+            vd1 = d.vtab16[g1];
+            dst0 = g0;
+            dst1 = g1;
+        } else {
+            const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
+            dst0 = dst_resolve(d, x0, g0, pb0, vd0);
+            dst1 = dst_resolve(d, x1, g1, pb1, vd1);
+        }
         asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
         const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
-        const PairRec pr0 = d.pairs[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0];
-        const PairRec pr1 = d.pairs[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1];
+        const PairRec pr0 = load_pair(d, (size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0, want_jump);
+        const PairRec pr1 = load_pair(d, (size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1, want_jump);
         {
             const uint64_t bt = S + (r0.a & M52);
             const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
@@ -1263,8 +1359,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const uint32_t h = hbase + s_act[j];
         const uint32_t ns = s_vh[j] >> 16;
         uint64_t evc = d.hs[h - d.lo].evc;  // untouched by phase A on this path
+        Rec rq[4];
+        const uint32_t klast = sb + ns - 1;
         for (uint32_t k = sb; k < sb + ns; ++k) {
-            const Rec r = snd[k];
+            const uint32_t u = (k - sb) & 3u;
+            if (u == 0) {  // the next four records in flight together (clamped addresses)
+#pragma unroll
+                for (uint32_t v = 0; v < 4; ++v) rq[v] = snd[k + v < klast ? k + v : klast];
+            }
+            const Rec r = opaque_rec(rq, u);
             if (!(r.a >> 63)) {
                 ++a.ctr[C_DROPREL];
                 continue;
@@ -1592,7 +1695,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     const uint32_t R = d.R, NCH = d.NCH;
     const uint64_t W = d.W;
     const uint32_t tid = threadIdx.x;
-    uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * 16 : nullptr;
+    uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
 #define PSTAMP(k) \
     if (pst) pst[k] = __builtin_amdgcn_s_memrealtime()
     PSTAMP(0);
@@ -2016,6 +2119,13 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
     const long v = strtol(s, nullptr, 10);
     return v > 0 ? (uint32_t)v : dflt;
 }
+// As env_u32, but 0 is a value (debug switches whose 0 setting means something).
+static uint32_t env_u32z(const char* name, uint32_t dflt) {
+    const char* s = getenv(name);
+    if (!s || !*s) return dflt;
+    const long v = strtol(s, nullptr, 10);
+    return v >= 0 ? (uint32_t)v : dflt;
+}
 
 extern "C" {
 
@@ -2172,12 +2282,66 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }                                              \
     } while (0)
     HostInfo* hinfo;
-    PairRec* pairs;
+    uint16_t* vtab16 = nullptr;
+    PairRec* pairs = nullptr;
+    uint2* pairs8 = nullptr;
+    uint32_t *pdelay = nullptr, *pjump = nullptr;
     ALLOC(hinfo, N);
-    ALLOC(pairs, VV);
+    // path-record format: delays below 2^32 ns fit the narrow records
+    uint64_t max_delay_all = 0, gjmin = UINT64_MAX;
+    bool all_keep = true;
+    for (size_t i = 0; i < VV; ++i) {
+        max_delay_all = std::max<uint64_t>(max_delay_all, t->delay_ns[i]);
+        gjmin = std::min<uint64_t>(gjmin, t->jump_ms[i]);
+        all_keep &= t->keep_max[i] >= SG_RAND_MAX;
+    }
+    D.pair_fmt = max_delay_all >> 32 ? PAIR_WIDE : all_keep ? PAIR_DELAY : PAIR_NARROW;
+    const uint32_t fmt_env = env_u32z("SG_PAIR_FMT", 99);  // debugging: force a wider format
+    if (fmt_env < D.pair_fmt) D.pair_fmt = fmt_env;
+    D.gjmin = gjmin;
+    if (D.pair_fmt == PAIR_WIDE) {
+        ALLOC(pairs, VV);
+    } else {
+        if (D.pair_fmt == PAIR_NARROW) ALLOC(pairs8, VV);
+        else ALLOC(pdelay, VV);
+        ALLOC(pjump, VV);
+    }
+    D.pairs8 = pairs8;
+    D.pdelay = pdelay;
+    D.pjump = pjump;
     uint64_t* vself;
     ALLOC(vself, D.V);
     D.hinfo = hinfo;
+    // exact guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
+    // must map to i under the (monotone) guess, so checking both ends suffices
+    // a lane's later light hosts record their sends for phase B instead: their
+    // chains then overlap every other lane's instead of running after them
+    D.light_q = env_u32z("SG_LIGHT_Q", 1);
+    D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
+    D.dst_exact = 0;
+    if (D.V <= 65536 && env_u32("SG_NO_EXACT_DST", 0) == 0) {
+        bool ok = true;
+        if (p.dst_rule == SG_DST_WEIGHTS) {
+            auto guess = [&](int64_t x) {
+                const uint64_t g = ((uint64_t)x * N) >> 31;
+                return g >= N ? N - 1 : g;
+            };
+            int64_t prev = -1;
+            for (size_t i = 0; i < N && ok; ++i) {
+                const int64_t hi = t->weight_thresh ? t->weight_thresh[i] : 0;
+                if (hi > prev && hi >= 0) {
+                    const int64_t lo = prev + 1 > 0 ? prev + 1 : 0;
+                    const int64_t hc = hi < SG_RAND_MAX ? hi : SG_RAND_MAX;
+                    if (lo <= hc) ok = guess(lo) == i && guess(hc) == i;
+                }
+                prev = hi > prev ? hi : prev;
+            }
+            ok = ok && t->weight_thresh != nullptr;
+        }
+        D.dst_exact = ok ? 1 : 0;
+    }
+    if (D.dst_exact) ALLOC(vtab16, N);
+    D.vtab16 = vtab16;
     D.pairs = pairs;
     D.vself = vself;
     ALLOC(D.hs, L);
@@ -2213,7 +2377,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
-    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, P * 16 + 16);  // + k_plan's 16
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (P + 1) * SG_STAMP_W);  // + k_plan's row
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
@@ -2246,15 +2410,30 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
             return SG_ERR_INVAL;
         }
     }
-    std::vector<PairRec> pr(VV);
-    for (size_t i = 0; i < VV; ++i) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
+    std::vector<PairRec> pr(D.pair_fmt == PAIR_WIDE ? VV : 0);
+    std::vector<uint2> pr8(D.pair_fmt == PAIR_NARROW ? VV : 0);
+    std::vector<uint32_t> pd(D.pair_fmt == PAIR_DELAY ? VV : 0), pj(D.pair_fmt != PAIR_WIDE ? VV : 0);
+    for (size_t i = 0; i < VV; ++i) {
+        if (D.pair_fmt == PAIR_WIDE) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
+        else if (D.pair_fmt == PAIR_NARROW) pr8[i] = make_uint2((uint32_t)t->delay_ns[i], (uint32_t)t->keep_max[i]);
+        else pd[i] = (uint32_t)t->delay_ns[i];
+        if (D.pair_fmt != PAIR_WIDE) pj[i] = t->jump_ms[i];
+    }
     std::vector<uint64_t> vs(D.V);
     for (size_t v = 0; v < D.V; ++v) vs[v] = t->delay_ns[v * D.V + v];
     std::vector<HostState> hs(L);
     for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};  // evc 0 until boot
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
-    err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
+    if (vtab16) {
+        std::vector<uint16_t> vt(N);
+        for (size_t i = 0; i < N; ++i) vt[i] = (uint16_t)hi[i].vertex;
+        err = err != hipSuccess ? err : hipMemcpy(vtab16, vt.data(), N * 2, hipMemcpyHostToDevice);
+    }
+    if (pairs) err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
+    if (pairs8) err = err != hipSuccess ? err : hipMemcpy(pairs8, pr8.data(), VV * sizeof(uint2), hipMemcpyHostToDevice);
+    if (pdelay) err = err != hipSuccess ? err : hipMemcpy(pdelay, pd.data(), VV * 4, hipMemcpyHostToDevice);
+    if (pjump) err = err != hipSuccess ? err : hipMemcpy(pjump, pj.data(), VV * 4, hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(vself, vs.data(), D.V * sizeof(uint64_t), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(D.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemset(D.rs, 0, sizeof(RoundState));
@@ -2564,7 +2743,7 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
 
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
     if (!e) return SG_ERR_INVAL;
-    const uint64_t n = e->d.stamps ? (uint64_t)e->d.P * 16 + 16 : 0;
+    const uint64_t n = e->d.stamps ? ((uint64_t)e->d.P + 1) * SG_STAMP_W : 0;
     if (n_out) *n_out = n;
     if (out && capacity && n) {
         HIPCHK(hipStreamSynchronize(e->stream));

@@ -140,14 +140,14 @@ class Engine:
         return g.as_dict()
 
     def stamps(self) -> np.ndarray:
-        """[P + 1, 16] k_proc phase stamps of the last round (SG_STAMPS=1), the last
+        """[P + 1, 32] k_proc phase stamps of the last round (SG_STAMPS=1), the last
         row k_plan's, or empty."""
         n = C.c_uint64()
         L.check(L.lib().sg_engine_stamps(self.h, None, 0, C.byref(n)))
         out = np.zeros(n.value, np.uint64)
         if n.value:
             L.check(L.lib().sg_engine_stamps(self.h, out.ctypes.data, n.value, C.byref(n)))
-        return out.reshape(-1, 16)
+        return out.reshape(-1, 32)
 
     # ---------------------------------------------------------- multi shard
     def exchange_rows(self) -> int:

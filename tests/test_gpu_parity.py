@@ -212,3 +212,36 @@ def test_path_counters_off_by_default():
     eng.boot()
     eng.run(5)
     assert eng.path_counts().size == 0
+
+
+@pytest.mark.parametrize("fmt,probe,light,light_q", [(0, False, 2, 1), (1, False, 2, 1), (2, True, 2, 1),
+                                                    (2, False, 0, 1), (2, False, 2, 99)])
+def test_forced_wide_tables(fmt, probe, light, light_q, monkeypatch):
+    """configs[3] keeps every packet and has uniform weights, so the engine picks
+    the 4-byte delay-only path records and the 2-byte vertex table (the guessed
+    host is the drawn one for every x).  Forcing the 16-byte (0) or 8-byte (1)
+    path records, or the three-record destination probe, or sending every
+    host's sends through phases B and C, or running every light host inline,
+    must give the same bits (the switches are read at sg_engine_create)."""
+    monkeypatch.setenv("SG_PAIR_FMT", str(fmt))
+    if probe:
+        monkeypatch.setenv("SG_NO_EXACT_DST", "1")
+    monkeypatch.setenv("SG_LIGHT_MAX", str(light))  # 0: every host's sends through phases B and C
+    monkeypatch.setenv("SG_LIGHT_Q", str(light_q))  # 99: every light host inline in phase A
+    cfg = phold.c4_config(n_hosts=20_000)
+    eng, orc = _run_both(cfg, max_rounds=40)
+    _assert_same(eng, orc)
+
+
+def test_long_paths_use_wide_records():
+    """A path delay of 2^32 ns (4.29 s) or more does not fit the narrow records:
+    the engine keeps the 16-byte ones and the arithmetic stays 64-bit."""
+    lat, el = phold.lognormal_topology(6, 11, median_ms=2000.0, sigma=1.0, min_ms=1.0, edge_loss=0.05)
+    lat = lat.reshape(6, 6)
+    lat[0, 5] = lat[5, 0] = 6000.0
+    cfg = phold.make_config(n_hosts=48, latency_ms=lat, edge_loss=el, load=3, seed=5,
+                            end_time_s=30.0, name="long-paths")
+    assert int(cfg["delay_ns"].max()) >= 1 << 32
+    eng, orc = _run_both(cfg, trace=200_000)
+    gs = _assert_same(eng, orc)
+    assert gs["pops"] > 0

@@ -32,6 +32,12 @@ for r in range(3):
     t = np.diff(st[:, [3, 13, 14, 15, 4]], axis=1) / 100
     print("   after phase B (median us): phase C %.2f  partials %.2f  reservations %.2f  tail %.2f"
           % tuple(np.median(t, axis=0)))
+    g = np.diff(st[:, [0, 20, 21, 22, 1]], axis=1) / 100
+    print("   sort (median us): part loads %.2f  histogram %.2f  scan %.2f  prefetch+scatter %.2f"
+          % tuple(np.median(g, axis=0)))
+    f = np.diff(st[:, [9, 16, 17, 18, 19]], axis=1) / 100
+    print("   light host, lane 0 (median us): pop+draws %.2f  dst loads %.2f  pair loads %.2f  commit %.2f"
+          % tuple(np.median(f, axis=0)))
     d = np.diff(pl[:8]) / 100
     print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
           "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
