@@ -62,6 +62,11 @@ def parse():
                     default=min(16, len(os.sched_getaffinity(0))),
                     help="CPU baseline worker threads (the GPU box's share is 16 cores)")
     ap.add_argument("--batch", type=int, default=32, help="rounds enqueued per host sync")
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("SG_GRAPH", "0")),
+                    help="capture every GRAPH rounds / steps into a hipGraph and replay it (0: off)")
+    ap.add_argument("--py-steps", action="store_true",
+                    help="N > 1: drive each step from Python around torch's all_to_all_single "
+                         "instead of sg_engine_run_steps")
     ap.add_argument("--kernel-rounds", type=int, default=50,
                     help="rounds after the timed region that are re-run with per-kernel HIP events")
     ap.add_argument("--dist-backend", default="nccl",
@@ -115,19 +120,14 @@ def run_single(args):
     cfg = phold.c4_config(n_hosts=args.hosts)
     eng = Engine(cfg, device=0)
     eng.boot()
-    eng.run(args.warmup, batch=args.batch)
+    eng.set_graph(args.graph)
+    eng.run(args.warmup, batch=args.graph or args.batch)
     s0 = eng.stats()
     eng.sync()
-    # timed region: K rounds, nothing but the rounds on the stream
+    # timed region: K rounds, nothing but the rounds on the stream (at most two
+    # batches queued, no read-back)
     t0 = time.perf_counter()
-    left = args.steps
-    while left > 0:
-        n = min(args.batch, left)
-        for _ in range(n):
-            eng.enqueue_round()
-        left -= n
-        if left > 0:
-            eng.sync()  # bounded queue depth; the same host round-trips sg_engine_run makes
+    eng.enqueue_rounds(args.steps)
     eng.sync()
     dt = time.perf_counter() - t0
     s1 = eng.stats()
@@ -172,7 +172,9 @@ def run_single(args):
                                "latency (median 30 ms, sigma 0.9, min 1 ms), runahead 1 ms, "
                                "weights rule, seed 1",
                    "n_hosts": args.hosts, "rounds_timed": rounds, "events_timed": pops,
-                   "parallelism": "hosts sharded 1 way"},
+                   "parallelism": "hosts sharded 1 way",
+                   "round_loop": f"sg_engine_enqueue_rounds, hipGraph batch {args.graph}" if args.graph
+                                 else "sg_engine_enqueue_rounds, eager launches"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,

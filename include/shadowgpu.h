@@ -286,6 +286,9 @@ int sg_engine_boot(sg_engine* e);
 int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch);
 /* Enqueue one round (gather + process + insert + plan) without synchronising. */
 int sg_engine_enqueue_round(sg_engine* e);
+/* n rounds without reading the round state back (graph-batched when
+ * sg_engine_set_graph is on); at most two batches stay queued on the stream. */
+int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds);
 int sg_engine_sync(sg_engine* e);
 int sg_engine_stats(sg_engine* e, sg_round_stats* out);   /* synchronises */
 /* Per local host (index - first_host): trace digest, pops, rng state, event counter. */
@@ -340,6 +343,27 @@ int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap);
 int sg_engine_exchange_peak(sg_engine* e, uint64_t* peak, int reset);
 int sg_engine_step_send(sg_engine* e, int64_t* send);
 int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
+
+/* Native step loop: the whole step (step_send, RCCL all-to-all over xGMI,
+ * step_recv) issued from C on the engine stream, so no interpreter sits in the
+ * round loop.  A communicator is made from a 128-byte RCCL unique id that rank 0
+ * creates (sg_comm_unique_id) and the caller broadcasts; RCCL is opened with
+ * dlopen, so the library the process already loaded (e.g. torch's) is the one
+ * used.  run_steps enqueues n steps without synchronising; send / recv are
+ * device buffers of [G][rows][3] int64.  With sg_engine_set_graph(e, b > 0)
+ * (and for sg_engine_run in round mode) every b steps / rounds are captured once
+ * into a hipGraph and replayed; a graph is rebuilt when the buffers, the
+ * communicator, exchange_cap or the path-counter table change.  set_graph
+ * always drops the current graph: call it (e.g. with 0) before destroying a
+ * communicator a graph captured, since RCCL frees a captured collective's
+ * resources only with its graph.  Errors of the
+ * collective are SG_ERR_HIP with the RCCL message in sg_last_error. */
+typedef struct sg_comm sg_comm;
+int sg_comm_unique_id(uint8_t id_out[128]);
+int sg_comm_create(const uint8_t id[128], int rank, int world, int device, sg_comm** out);
+int sg_comm_destroy(sg_comm* c);
+int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, uint64_t n_steps);
+int sg_engine_set_graph(sg_engine* e, uint32_t batch);
 
 /* Kernel timing since sg_engine_set_timing(e, 1) (HIP events on the engine
  * stream): total ms and launches per kernel class, arrays of SG_KCLASSES. */

@@ -88,7 +88,9 @@ EXPORTS = [
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
     "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
-    "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv", "sg_engine_kernel_times",
+    "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv",
+    "sg_engine_enqueue_rounds", "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy",
+    "sg_engine_run_steps", "sg_engine_set_graph", "sg_engine_kernel_times",
     "sg_engine_set_timing", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
@@ -148,6 +150,12 @@ def lib():
     L.sg_engine_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_path_counters.argtypes = [C.c_void_p, C.c_int]
     L.sg_engine_path_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.sg_engine_enqueue_rounds.argtypes = [C.c_void_p, C.c_uint64]
+    L.sg_comm_unique_id.argtypes = [C.c_void_p]
+    L.sg_comm_create.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.sg_comm_destroy.argtypes = [C.c_void_p]
+    L.sg_engine_run_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+    L.sg_engine_set_graph.argtypes = [C.c_void_p, C.c_uint32]
     _lib = L
     return L
 

@@ -46,7 +46,9 @@
 // (time, src << 40 | srcHostEventID).  Compiled with -ffp-contract=off: the
 // only FP is the FP64 floor destination rule, which must round as the
 // reference does.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -2033,6 +2035,19 @@ struct sg_engine {
     std::vector<hipEvent_t> free_ev;
     double ms[SG_KCLASSES];
     uint64_t launches[SG_KCLASSES];
+    // hipGraph replay of batches of rounds / steps (sg_engine_set_graph)
+    uint32_t graph_batch = 0;
+    uint64_t gen = 0;  // bumped whenever a kernel argument captured in a graph changes
+    hipGraphExec_t gexec = nullptr;
+    hipEvent_t batch_ev[2] = {nullptr, nullptr};  // sg_engine_enqueue_rounds' queue bound
+    struct GraphKey {
+        uint64_t gen;
+        const void *send, *recv, *comm;
+        uint32_t n;
+        bool operator==(const GraphKey& o) const {
+            return gen == o.gen && send == o.send && recv == o.recv && comm == o.comm && n == o.n;
+        }
+    } gkey{};
 };
 
 #define HIPCHK(x)                                                                      \
@@ -2458,6 +2473,9 @@ int sg_engine_destroy(sg_engine* e) {
     }
     for (auto ev : e->free_ev) (void)hipEventDestroy(ev);
     if (e->h_rs) (void)hipHostFree(e->h_rs);
+    if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+    for (hipEvent_t ev : e->batch_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return SG_OK;
@@ -2551,6 +2569,70 @@ int sg_engine_enqueue_round(sg_engine* e) {
     return enqueue_insert_plan(e, nullptr, 0);
 }
 
+// Enqueues n iterations of body (one round or one step each) on the engine
+// stream.  With graphs on (sg_engine_set_graph) and a full batch, the
+// iterations are captured once into a hipGraph and the graph is replayed while
+// its key (buffers, communicator, captured kernel arguments) is unchanged.
+extern "C++" template <typename F>
+static int enqueue_batch(sg_engine* e, const sg_engine::GraphKey& key, uint32_t n, F&& body) {
+    const bool use = e->graph_batch && n == e->graph_batch && !e->timing && !e->debug_sync;
+    if (!use) {
+        for (uint32_t i = 0; i < n; ++i)
+            if (int rc = body()) return rc;
+        return SG_OK;
+    }
+    if (!e->gexec || !(e->gkey == key)) {
+        if (e->gexec) {
+            HIPCHK(hipGraphExecDestroy(e->gexec));
+            e->gexec = nullptr;
+        }
+        HIPCHK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeRelaxed));
+        int rc = SG_OK;
+        for (uint32_t i = 0; i < n && rc == SG_OK; ++i) rc = body();
+        hipGraph_t g = nullptr;
+        const hipError_t ce = hipStreamEndCapture(e->stream, &g);
+        if (rc != SG_OK || ce != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            if (rc == SG_OK) sg_set_error("hipStreamEndCapture failed: %s", hipGetErrorString(ce));
+            return rc != SG_OK ? rc : SG_ERR_HIP;
+        }
+        const hipError_t ie = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ie != hipSuccess) {
+            e->gexec = nullptr;
+            sg_set_error("hipGraphInstantiate failed: %s", hipGetErrorString(ie));
+            return SG_ERR_HIP;
+        }
+        e->gkey = key;
+    }
+    HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+    return SG_OK;
+}
+
+int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds) {
+    if (!e || !e->booted) {
+        sg_set_error("sg_engine_enqueue_rounds: engine not booted");
+        return SG_ERR_STATE;
+    }
+    const uint32_t b = e->graph_batch ? e->graph_batch : 32;
+    if (!e->batch_ev[0]) {
+        HIPCHK(hipEventCreateWithFlags(&e->batch_ev[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->batch_ev[1], hipEventDisableTiming));
+    }
+    int rc;
+    for (uint32_t k = 0; n_rounds; ++k) {
+        const uint32_t n = n_rounds < b ? (uint32_t)n_rounds : b;
+        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, n};
+        if ((rc = enqueue_batch(e, key, n, [&] { return sg_engine_enqueue_round(e); }))) return rc;
+        n_rounds -= n;
+        // at most two batches queued: wait for the one before this
+        hipEvent_t& ev = e->batch_ev[k & 1];
+        if (k) HIPCHK(hipEventSynchronize(e->batch_ev[(k + 1) & 1]));
+        HIPCHK(hipEventRecord(ev, e->stream));
+    }
+    return SG_OK;
+}
+
 int sg_engine_sync(sg_engine* e) {
     if (!e) return SG_ERR_INVAL;
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -2575,8 +2657,9 @@ int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch) {
     while (done_rounds < max_rounds && !e->h_rs->done) {
         uint64_t n = max_rounds - done_rounds;
         if (n > batch) n = batch;
-        for (uint64_t i = 0; i < n; ++i)
-            if ((rc = sg_engine_enqueue_round(e))) return rc;
+        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, (uint32_t)n};
+        if ((rc = enqueue_batch(e, key, (uint32_t)n, [&] { return sg_engine_enqueue_round(e); })))
+            return rc;
         done_rounds += n;
         if ((rc = read_rs(e))) return rc;
         if (e->h_rs->overflow) {
@@ -2705,6 +2788,7 @@ int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap) {
     }
     e->d.xcap = exchange_cap;
     e->d.xrows = HDR + exchange_cap;
+    e->gen++;
     return SG_OK;
 }
 
@@ -2757,6 +2841,7 @@ int sg_engine_path_counters(sg_engine* e, int enable) {
     HIPCHK(hipSetDevice(e->device));
     if (!enable) {
         e->d.pcount = nullptr;  // the table stays allocated until destroy
+        e->gen++;
         return SG_OK;
     }
     const size_t VV = (size_t)e->d.V * e->d.V;
@@ -2766,6 +2851,7 @@ int sg_engine_path_counters(sg_engine* e, int enable) {
     }
     HIPCHK(hipMemsetAsync(e->pcount_buf, 0, VV * sizeof(uint32_t), e->stream));
     e->d.pcount = e->pcount_buf;
+    e->gen++;
     return SG_OK;
 }
 
@@ -2800,6 +2886,138 @@ int sg_engine_kernel_times(sg_engine* e, double* ms, uint64_t* launches) {
     for (int i = 0; i < SG_KCLASSES; ++i) {
         if (ms) ms[i] = e->ms[i];
         if (launches) launches[i] = e->launches[i];
+    }
+    return SG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------- native step loop ----
+// RCCL through dlopen: the copy the process already loaded (torch links one)
+// is reused, so this library neither links RCCL nor brings a second copy.
+namespace {
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*allToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*errStr)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+
+int rccl_open() {
+    if (g_rccl.ok) return SG_OK;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!h) {
+        sg_set_error("RCCL not found (dlopen librccl.so.1): %s", dlerror());
+        return SG_ERR_STATE;
+    }
+    g_rccl.getUniqueId = (decltype(g_rccl.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    g_rccl.commInitRank = (decltype(g_rccl.commInitRank))dlsym(h, "ncclCommInitRank");
+    g_rccl.commDestroy = (decltype(g_rccl.commDestroy))dlsym(h, "ncclCommDestroy");
+    g_rccl.allToAll = (decltype(g_rccl.allToAll))dlsym(h, "ncclAllToAll");
+    g_rccl.errStr = (decltype(g_rccl.errStr))dlsym(h, "ncclGetErrorString");
+    if (!g_rccl.getUniqueId || !g_rccl.commInitRank || !g_rccl.commDestroy || !g_rccl.allToAll ||
+        !g_rccl.errStr) {
+        sg_set_error("librccl.so.1 lacks an ncclGetUniqueId / ncclCommInitRank / ncclAllToAll symbol");
+        return SG_ERR_STATE;
+    }
+    g_rccl.ok = true;
+    return SG_OK;
+}
+}  // namespace
+
+#define RCCLCHK(x)                                                                      \
+    do {                                                                                \
+        ncclResult_t _r = (x);                                                          \
+        if (_r != ncclSuccess) {                                                        \
+            sg_set_error("%s failed: %s (%s:%d)", #x, g_rccl.errStr(_r), __FILE__, __LINE__); \
+            return SG_ERR_HIP;                                                          \
+        }                                                                               \
+    } while (0)
+
+struct sg_comm {
+    ncclComm_t comm;
+    int rank, world, device;
+};
+
+extern "C" {
+
+int sg_comm_unique_id(uint8_t id_out[128]) {
+    if (!id_out) return SG_ERR_INVAL;
+    int rc = rccl_open();
+    if (rc) return rc;
+    ncclUniqueId id;
+    RCCLCHK(g_rccl.getUniqueId(&id));
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(id_out, &id, sizeof id);
+    return SG_OK;
+}
+
+int sg_comm_create(const uint8_t id_in[128], int rank, int world, int device, sg_comm** out) {
+    if (!id_in || !out || world < 1 || rank < 0 || rank >= world) {
+        sg_set_error("sg_comm_create: bad arguments (rank %d, world %d)", rank, world);
+        return SG_ERR_INVAL;
+    }
+    int rc = rccl_open();
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(device));
+    ncclUniqueId id;
+    memcpy(&id, id_in, sizeof id);
+    ncclComm_t comm = nullptr;
+    RCCLCHK(g_rccl.commInitRank(&comm, world, id, rank));
+    *out = new sg_comm{comm, rank, world, device};
+    return SG_OK;
+}
+
+int sg_comm_destroy(sg_comm* c) {
+    if (!c) return SG_OK;
+    if (g_rccl.ok && c->comm) (void)g_rccl.commDestroy(c->comm);
+    delete c;
+    return SG_OK;
+}
+
+int sg_engine_set_graph(sg_engine* e, uint32_t batch) {
+    if (!e) return SG_ERR_INVAL;
+    e->graph_batch = batch;
+    // drop the captured graph: RCCL keeps resources of captured collectives
+    // until their graph is destroyed, and a communicator is destroyed only after
+    if (e->gexec) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipGraphExecDestroy(e->gexec));
+        e->gexec = nullptr;
+    }
+    return SG_OK;
+}
+
+int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, uint64_t n_steps) {
+    int rc = need_sharded(e, "sg_engine_run_steps");
+    if (rc) return rc;
+    if (!c || !send || !recv) {
+        sg_set_error("sg_engine_run_steps: NULL communicator or buffer");
+        return SG_ERR_INVAL;
+    }
+    if ((uint32_t)c->world != e->d.G || (uint32_t)c->rank != e->d.g) {
+        sg_set_error("sg_engine_run_steps: communicator rank %d of %d, engine shard %u of %u", c->rank,
+                     c->world, e->d.g, e->d.G);
+        return SG_ERR_INVAL;
+    }
+    const size_t per_peer = (size_t)e->d.xrows * 3;  // int64 elements per peer block
+    auto step = [&]() -> int {
+        int r = sg_engine_step_send(e, send);
+        if (r) return r;
+        RCCLCHK(g_rccl.allToAll(send, recv, per_peer, ncclInt64, c->comm, e->stream));
+        return sg_engine_step_recv(e, recv);
+    };
+    const uint32_t b = e->graph_batch ? e->graph_batch : 32;
+    while (n_steps) {
+        const uint32_t n = n_steps < b ? (uint32_t)n_steps : b;
+        const sg_engine::GraphKey key{e->gen, send, recv, c, n};
+        if ((rc = enqueue_batch(e, key, n, step))) return rc;
+        n_steps -= n;
     }
     return SG_OK;
 }

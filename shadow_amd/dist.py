@@ -71,6 +71,35 @@ class EngineShard:
         self.send = torch.zeros((self.world, rows, 3), dtype=torch.int64, device=self.dev)
         self.recv = torch.zeros_like(self.send)
 
+    def enable_native(self, graph_batch: int = 0):
+        """Issue whole steps from C (sg_engine_run_steps) over a communicator of
+        libshadowgpu's own, made from a unique id rank 0 broadcasts over the
+        default process group; graph_batch > 0 replays captured hipGraphs."""
+        from .engine import Comm
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
+        if _backend() == "nccl":
+            u = uid.to(self.dev)
+            dist.broadcast(u, 0)
+            uid = u.cpu()
+        else:
+            dist.broadcast(uid, 0)
+        self.comm = Comm(bytes(uid.tolist()), self.rank, self.world, self.dev.index)
+        self.eng.set_graph(graph_batch)
+
+    def close_native(self):
+        """Drop the captured graphs, then the communicator (RCCL frees captured
+        collectives' resources with their graph)."""
+        if getattr(self, "comm", None) is not None:
+            self.eng.set_graph(0)
+            self.sync()
+            self.comm.close()
+            self.comm = None
+
+    def run_native(self, n: int):
+        self.eng.run_steps(self.comm, self.send.data_ptr(), self.recv.data_ptr(), n)
+
     def stream_ctx(self):
         return torch.cuda.stream(self.stream)
 
@@ -135,6 +164,15 @@ def run_step(shard, world: int):
 def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16) -> int:
     """Run steps until the simulation is done (checked every check_every steps)
     or max_steps; returns the steps run."""
+    if getattr(shard, "comm", None) is not None:
+        n = 0
+        while n < max_steps:
+            k = min(check_every - n % check_every, max_steps - n)
+            shard.run_native(k)
+            n += k
+            if n % check_every == 0 and shard.done():
+                break
+        return n
     ctx = shard.stream_ctx() if hasattr(shard, "stream_ctx") else contextlib.nullcontext()
     n = 0
     with ctx:
@@ -179,6 +217,8 @@ def bench(args):
         dist.init_process_group(args.dist_backend)
     cfg = phold.c4_config(n_hosts=args.hosts)
     shard = EngineShard(cfg, rank, world, dev)
+    if args.dist_backend == "nccl" and not args.py_steps:
+        shard.enable_native(args.graph)
     shard.boot()
     # warmup: the boot round (its outbox drains over several steps), then size
     # the exchange blocks from the steady-state per-peer peak, the same on every rank
@@ -210,6 +250,7 @@ def bench(args):
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     tmax = float(t.item())
     total, rounds_sum, steps_sum, ovf = (int(x) for x in tot.tolist())
+    shard.close_native()
     dist.destroy_process_group()
     global _BACKEND
     _BACKEND = None
@@ -238,5 +279,7 @@ def bench(args):
                    "exchange_cap": cap,
                    "parallelism": f"hosts block-sharded {world} ways, one "
                                   f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
-                                  "all-to-all per step"},
+                                  "all-to-all per step",
+                   "step_loop": "python" if getattr(shard, "comm", None) is None else
+                                f"native (sg_engine_run_steps, hipGraph batch {args.graph})"},
     }

@@ -69,6 +69,14 @@ class Engine:
     def enqueue_round(self):
         L.check(L.lib().sg_engine_enqueue_round(self.h))
 
+    def enqueue_rounds(self, n: int):
+        """n rounds, no read-back; at most two batches queued."""
+        L.check(L.lib().sg_engine_enqueue_rounds(self.h, n))
+
+    def set_graph(self, batch: int):
+        """Capture every `batch` rounds / steps into a hipGraph and replay it (0: off)."""
+        L.check(L.lib().sg_engine_set_graph(self.h, batch))
+
     def sync(self):
         L.check(L.lib().sg_engine_sync(self.h))
 
@@ -168,6 +176,32 @@ class Engine:
 
     def step_recv(self, recv_ptr: int):
         L.check(L.lib().sg_engine_step_recv(self.h, recv_ptr))
+
+    def run_steps(self, comm: "Comm", send_ptr: int, recv_ptr: int, n: int):
+        """n whole steps (step_send, RCCL all-to-all, step_recv) issued from C."""
+        L.check(L.lib().sg_engine_run_steps(self.h, comm.h, send_ptr, recv_ptr, n))
+
+
+class Comm:
+    """An RCCL communicator owned by libshadowgpu (sg_comm_create): rank 0 makes
+    the 128-byte unique id, the caller broadcasts it."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        L.check(L.lib().sg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, rank: int, world: int, device: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        L.check(L.lib().sg_comm_create(buf, rank, world, device, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib().sg_comm_destroy(self.h)
+            self.h = None
 
 
 def probe_hash(trace: np.ndarray) -> tuple[int, int]:

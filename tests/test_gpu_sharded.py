@@ -86,3 +86,45 @@ def test_sharded_windows_and_trace_match_oracle():
     rt = ref.trace()
     key = ["host", "pos"]
     assert np.array_equal(np.sort(tr, order=key), np.sort(rt, order=key))
+
+
+@pytest.mark.parametrize("graph", [0, 4])
+def test_native_rccl_steps_world1_match_oracle(graph):
+    """sg_engine_run_steps: step_send, RCCL all-to-all (a world-1 communicator of
+    libshadowgpu's own) and step_recv issued from C, optionally replayed from
+    captured hipGraphs; a small exchange_cap forces drain steps."""
+    from shadow_amd.dist import EngineShard
+    from shadow_amd.engine import Comm
+    cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
+    sh = EngineShard(cfg, 0, 1, 0, exchange_cap=4096)
+    sh.comm = Comm(Comm.unique_id(), 0, 1, 0)
+    sh.eng.set_graph(graph)
+    sh.boot()
+    n = 0
+    while not sh.done():
+        sh.run_native(8)
+        n += 8
+        assert n < 100_000
+    sh.sync()
+    _check(cfg, [sh])
+    sh.close_native()
+
+
+@pytest.mark.parametrize("graph", [3, 8])
+def test_graph_rounds_match_oracle(graph):
+    """Round mode replayed from captured hipGraphs (sg_engine_run and
+    sg_engine_enqueue_rounds), including a partial last batch."""
+    from shadow_amd.engine import Engine
+    cfg = phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)
+    eng = Engine(cfg, device=0)
+    eng.boot()
+    eng.set_graph(graph)
+    eng.enqueue_rounds(2 * graph + 1)
+    eng.run(batch=graph)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    g, o = eng.host_state(), ref.host_state()
+    for k in ("digest", "pops", "rng", "ev"):
+        assert np.array_equal(g[k], o[k]), k
+    assert eng.stats()["rounds"] == ref.stats()["rounds"]
