@@ -34,9 +34,11 @@
 // so no workgroup ever waits on another inside a launch.
 //   multi-shard k_proc also writes the events for other shards into per-peer
 //               outbox regions (one reservation per peer and partition);
-//               k_fill builds the fixed-size exchange blocks (the header
-//               carries the shard's MIN terms); k_plan reads the G headers back
-//               instead of the local minima.
+//               The first xcap rows of each peer's outbox are the exchange
+//               block itself; the last k_proc workgroup to finish writes the
+//               block headers (the shard's MIN terms).  On a drain step k_proc
+//               only copies outbox leftovers into the blocks.  k_plan reads the
+//               G headers back instead of the local minima.
 //
 // HBM layout: 16-B records everywhere.
 //   bucket record     {dst_local << 40 | (t - b*W),  src << 40 | srcHostEventID}
@@ -147,6 +149,8 @@ struct RoundState {
     uint64_t phase;      // 0: process step, 1: drain step (outbox leftovers only)
     uint64_t steps;      // exchange steps executed
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
+    uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
+    uint64_t xacc[2];    // emitted min, discovery min of this launch's workgroups (atomics)
 };
 
 struct Dev {
@@ -198,7 +202,9 @@ struct Dev {
     uint32_t* remn;           // [P] staged events for other shards
     Slot* rem;                // [P][ECAP]
     uint32_t* rem_dst;        // [P][ECAP]
-    int64_t* outq;            // [G][oreg][3] per-peer outbox regions
+    int64_t* xsend;           // [G][xrows][3] this step's exchange blocks (set by step_send)
+    int64_t* outq;            // [G][oreg][3] per-peer outbox regions (rows < xcap go
+                              // straight into xsend on a process step)
     uint64_t oreg;            // rows per peer region (P * ECAP: every staged event fits)
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
@@ -553,6 +559,9 @@ __global__ void k_boot(Dev d) {
         rs->phase = 0;
         rs->steps = 0;
         rs->peak_peer = 0;
+        rs->ticket = 0;
+        rs->xacc[0] = UINT64_MAX;
+        rs->xacc[1] = UINT64_MAX;
     }
     if (i < d.G && d.outn) {
         d.outn[i] = 0;
@@ -967,9 +976,66 @@ constexpr uint32_t HPT = HPMAX / K2_T;     // active hosts per lane, at most
 constexpr uint32_t EVLMAX = 6144;          // due events sorted in LDS, at most
 constexpr uint32_t EPT = EVLMAX / K2_T;    // of them per lane
 
+// --------------------------------------------------------- multi-shard ----
+// Exchange blocks: per peer, HDR header rows {n, sender has more, MIN next,
+// min jump, overflow, round} then up to xcap outbox rows.  The MIN terms are
+// this shard's reduce_local of the step's process partials (unchanged on drain
+// steps, so a drain step repeats them).  One workgroup (every thread calls it).
+__device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j);
+__device__ __forceinline__ uint64_t atomic_read(uint64_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// outn / overflow are read atomically: the last k_proc workgroup reads what
+// the others' device-scope atomics performed (their L2 lines may be stale here).
+__device__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
+    RoundState* rs = d.rs;
+    if (threadIdx.x < d.G) {
+        const uint32_t p = threadIdx.x;
+        const uint64_t left = atomic_read(&d.outn[p]) - d.sent[p];
+        int64_t* blk = d.xsend + (size_t)p * d.xrows * 3;
+        blk[H_N] = (int64_t)(left < d.xcap ? left : d.xcap);
+        blk[H_MIN] = (int64_t)m;
+        blk[H_JMIN] = (int64_t)j;
+        blk[H_OVF] = (int64_t)atomic_read(&rs->overflow);
+        blk[H_ROUND] = (int64_t)rs->rounds;
+    }
+    if (threadIdx.x == 0) {
+        uint64_t more = 0, peak = rs->peak_peer;
+        for (uint32_t q = 0; q < d.G; ++q) {
+            const uint64_t on = atomic_read(&d.outn[q]);
+            more |= (on - d.sent[q] > d.xcap) ? 1u : 0u;
+            peak = q != d.g && on > peak ? on : peak;
+        }
+        for (uint32_t q = 0; q < d.G; ++q) d.xsend[(size_t)q * d.xrows * 3 + H_MORE] = (int64_t)more;
+        rs->peak_peer = peak;
+    }
+}
+// Drain step: the next xcap leftovers of every peer's outbox into its block,
+// spread over nblk workgroups; workgroup 0 also writes the headers.
+__device__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t nblk, uint64_t* s16) {
+    for (uint32_t p = 0; p < d.G; ++p) {
+        const uint64_t left = d.outn[p] - d.sent[p];
+        const uint64_t n = left < d.xcap ? left : d.xcap;
+        int64_t* dst = d.xsend + ((size_t)p * d.xrows + HDR) * 3;
+        const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * 3;
+        for (uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x; i < n * 3; i += (uint64_t)nblk * blockDim.x)
+            dst[i] = src[i];
+    }
+    if (blk == 0) {
+        uint64_t m, j;
+        reduce_local(d, s16, m, j);  // barriers inside
+        write_headers(d, m, j);
+    }
+}
+
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
-    if (rs->done | rs->phase) return;
+    if (rs->done) return;
+    if (rs->phase) {  // drain step: outbox leftovers into the exchange blocks
+        __shared__ uint64_t s16d[16];
+        if (d.xsend) fill_blocks(d, blockIdx.x, gridDim.x, s16d);
+        return;
+    }
     extern __shared__ __align__(16) unsigned char dyn[];
     const uint32_t HP = d.HP, R = d.R;
     uint32_t* s_n = (uint32_t*)dyn;             // [HP] events per host
@@ -1405,9 +1471,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const size_t so = (size_t)p * d.ECAP + i;
             const uint32_t dst = d.rem_dst[so];
             const uint32_t q = owner_of(d, dst);
-            const uint64_t slot = (uint64_t)q * d.oreg + s_obase[q] + atomicAdd(&s_oslot[q], 1u);
+            const uint64_t r = s_obase[q] + atomicAdd(&s_oslot[q], 1u);
             const Slot ev = d.rem[so];
-            int64_t* o = d.outq + slot * 3;
+            int64_t* o = r < d.xcap ? d.xsend + ((uint64_t)q * d.xrows + HDR + r) * 3
+                                    : d.outq + ((uint64_t)q * d.oreg + r) * 3;
             o[0] = (int64_t)ev.t;
             o[1] = (int64_t)ev.k;
             o[2] = (int64_t)dst;
@@ -1449,11 +1516,41 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         if (i < NCTR) d.pcum[(size_t)i * d.P + p] += r;
         else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
+        if (i >= NCTR && d.xsend) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
     }
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
         d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
+    }
+    if (d.xsend) {
+        // The last workgroup to finish writes the exchange block headers.  No
+        // fences (an L2 write-back per workgroup costs more than a launch):
+        // everything it reads from the others was performed by device-scope
+        // atomics (MIN accumulators, outbox counts, flags), which the barrier's
+        // vmcnt(0) completes before this workgroup takes its ticket.  No
+        // workgroup waits for another.
+        __shared__ bool s_lastwg;
+        __syncthreads();
+        if (tid == 0)
+            s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
+        __syncthreads();
+        if (s_lastwg) {
+            uint64_t m = UINT64_MAX;
+            for (uint32_t i = tid; i < d.G1; i += K2_T) m = d.c1min[i] < m ? d.c1min[i] : m;
+            m = block_min(m, s16);  // barriers inside
+            const uint64_t em = atomic_read(&rs->xacc[0]), jm = atomic_read(&rs->xacc[1]);
+            m = em < m ? em : m;
+            m = rs->rmin < m ? rs->rmin : m;
+            m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+            const uint64_t j = rs->jmin < jm ? rs->jmin : jm;
+            write_headers(d, m, j);
+            if (tid == 0) {
+                rs->ticket = 0;
+                rs->xacc[0] = UINT64_MAX;
+                rs->xacc[1] = UINT64_MAX;
+            }
+        }
     }
     if (stamp && tid == 0) {
         stamp[4] = __builtin_amdgcn_s_memrealtime();
@@ -1957,42 +2054,6 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     }
     PSTAMP(7);
 #undef PSTAMP
-}
-
-// --------------------------------------------------------- multi-shard ----
-// Every step: up to xcap outbox events per peer into the peer's exchange
-// block, behind the header {n, sender has more, MIN next, min jump, overflow,
-// round}.  Grid (chunks, G).  The header's MIN terms are this shard's
-// reduce_local of the step's process partials (unchanged on drain steps, so
-// a drain step repeats them).
-__global__ __launch_bounds__(256) void k_fill(Dev d, int64_t* send) {
-    RoundState* rs = d.rs;
-    if (rs->done) return;
-    __shared__ uint64_t s16[16];
-    const uint32_t p = blockIdx.y;
-    const uint64_t left = d.outn[p] - d.sent[p];
-    const uint64_t n = left < d.xcap ? left : d.xcap;
-    int64_t* blk = send + (size_t)p * d.xrows * 3;
-    const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * 3;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n * 3; i += (uint64_t)gridDim.x * 256)
-        blk[HDR * 3 + i] = src[i];
-    if (blockIdx.x != 0) return;
-    uint64_t m, j;
-    reduce_local(d, s16, m, j);  // the whole block (barriers inside)
-    if (threadIdx.x == 0) {
-        uint64_t more = 0, peak = rs->peak_peer;
-        for (uint32_t q = 0; q < d.G; ++q) {
-            more |= (d.outn[q] - d.sent[q] > d.xcap) ? 1u : 0u;
-            peak = q != d.g && d.outn[q] > peak ? d.outn[q] : peak;
-        }
-        blk[H_N] = (int64_t)n;
-        blk[H_MORE] = (int64_t)more;
-        blk[H_MIN] = (int64_t)m;
-        blk[H_JMIN] = (int64_t)j;
-        blk[H_OVF] = (int64_t)rs->overflow;
-        blk[H_ROUND] = (int64_t)rs->rounds;
-        if (p == 0) rs->peak_peer = peak;
-    }
 }
 
 // Cumulative counters (stats on demand) and pending events.
@@ -2770,11 +2831,6 @@ static int need_sharded(sg_engine* e, const char* fn) {
     return SG_OK;
 }
 
-static uint32_t fill_chunks(const Dev& d) {
-    uint64_t c = (d.xcap * 3 + 256 * 4 - 1) / (256 * 4);
-    return (uint32_t)(c < 1 ? 1 : c > 256 ? 256 : c);
-}
-
 int sg_engine_exchange_rows(sg_engine* e, uint64_t* rows) {
     if (!e || !rows) return SG_ERR_INVAL;
     *rows = e->d.xrows;
@@ -2808,11 +2864,10 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
         sg_set_error("sg_engine_step_send: NULL send buffer");
         return SG_ERR_INVAL;
     }
-    if ((rc = enqueue_process(e))) return rc;
-    const Dev& d = e->d;
-    return timed_launch(e, SG_K_PLAN, [&] {
-        hipLaunchKernelGGL(k_fill, dim3(fill_chunks(d), d.G), dim3(256), 0, e->stream, d, send);
-    });
+    e->d.xsend = send;  // k_proc writes the exchange blocks (launch argument)
+    rc = enqueue_process(e);
+    e->d.xsend = nullptr;
+    return rc;
 }
 
 int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
