@@ -76,15 +76,22 @@ class EngineShard:
         libshadowgpu's own, made from a unique id rank 0 broadcasts over the
         default process group; graph_batch > 0 replays captured hipGraphs."""
         from .engine import Comm
-        uid = torch.zeros(128, dtype=torch.uint8)
+        uid = torch.zeros(129, dtype=torch.uint8)  # [0]: rank 0 made an id; [1:]: the id
         if self.rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
+            try:
+                uid[1:].copy_(torch.frombuffer(bytearray(Comm.unique_id()), dtype=torch.uint8))
+                uid[0] = 1
+            except Exception:  # every rank learns it from the broadcast
+                pass
         if _backend() == "nccl":
             u = uid.to(self.dev)
             dist.broadcast(u, 0)
             uid = u.cpu()
         else:
             dist.broadcast(uid, 0)
+        if not int(uid[0]):
+            raise RuntimeError("rank 0 could not create an RCCL unique id")
+        uid = uid[1:]
         self.comm = Comm(bytes(uid.tolist()), self.rank, self.world, self.dev.index)
         self.eng.set_graph(graph_batch)
 
@@ -218,7 +225,13 @@ def bench(args):
     cfg = phold.c4_config(n_hosts=args.hosts)
     shard = EngineShard(cfg, rank, world, dev)
     if args.dist_backend == "nccl" and not args.py_steps:
-        shard.enable_native(args.graph)
+        try:
+            shard.enable_native(args.graph)
+        except Exception as exc:  # same on every rank (e.g. no RCCL symbols): Python steps
+            import sys
+            print(f"native step loop unavailable ({exc}); driving steps from Python",
+                  file=sys.stderr, flush=True)
+            shard.comm = None
     shard.boot()
     # warmup: the boot round (its outbox drains over several steps), then size
     # the exchange blocks from the steady-state per-peer peak, the same on every rank
