@@ -170,6 +170,7 @@ struct Dev {
     const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
     const uint32_t* pjump;    // [V*V] discovered ms (narrow formats), read only while it can matter
     uint32_t pair_fmt;        // PAIR_WIDE / PAIR_NARROW / PAIR_DELAY
+    uint32_t tri;             // narrow tables hold the lower triangle only (symmetric paths)
     uint64_t gjmin;           // smallest discovered ms of any pair: jmin can fall no lower
     const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
     uint32_t* pcount;         // [V*V] path packet counters (topology.c:2053-2063), or null
@@ -216,11 +217,20 @@ struct Dev {
     RoundState* rs;
 };
 
-// The path record of vertex pair idx.  want_jump: the discovery minimum can
-// still fall (rs->jmin > gjmin); otherwise the jump field is not read
-// (UINT32_MAX: it could not lower the minimum anyway).
-__device__ __forceinline__ PairRec load_pair(const Dev& d, size_t idx, bool want_jump) {
-    if (d.pair_fmt == PAIR_WIDE) return d.pairs[idx];
+// The path record of vertex pair (sv, dv).  want_jump: the discovery minimum
+// can still fall (rs->jmin > gjmin); otherwise the jump field is not read
+// (UINT32_MAX: it could not lower the minimum anyway).  When every path equals
+// its reverse (undirected topology, host-checked) the narrow tables keep the
+// lower triangle only: half the bytes, so more of each table stays in an
+// XCD's 4 MB L2 under the per-send random reads.
+__device__ __forceinline__ size_t pair_index(const Dev& d, uint32_t sv, uint32_t dv) {
+    if (!d.tri) return (size_t)sv * d.V + dv;
+    const uint32_t lo = sv < dv ? sv : dv, hi = sv < dv ? dv : sv;
+    return (size_t)hi * (hi + 1) / 2 + lo;
+}
+__device__ __forceinline__ PairRec load_pair(const Dev& d, uint32_t sv, uint32_t dv, bool want_jump) {
+    if (d.pair_fmt == PAIR_WIDE) return d.pairs[(size_t)sv * d.V + dv];
+    const size_t idx = pair_index(d, sv, dv);
     PairRec pr;
     if (d.pair_fmt == PAIR_NARROW) {
         const uint2 v = d.pairs8[idx];
@@ -820,7 +830,7 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             continue;
         }
         ++a.ctr[C_SENDS];
-        const PairRec pr = load_pair(d, (size_t)c.vh * d.V + di.vertex, d.rs->jmin > d.gjmin);
+        const PairRec pr = load_pair(d, c.vh, di.vertex, d.rs->jmin > d.gjmin);
         a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
         const int32_t ch = dev_rand_r(c.s.rng);          // worker.c:268-269
         if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
@@ -1327,8 +1337,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             }
                             if (st0) stamp[17] = wait_stamp();
                             asm volatile("" ::: "memory");  // both pair loads after both resolves
-                            const PairRec pr0 = load_pair(d, (size_t)c.vh * d.V + vd0, want_jump);
-                            const PairRec pr1 = load_pair(d, (size_t)c.vh * d.V + vd1, want_jump);
+                            const PairRec pr0 = load_pair(d, c.vh, vd0, want_jump);
+                            const PairRec pr1 = load_pair(d, c.vh, vd1, want_jump);
                             if (st0) stamp[18] = wait_stamp();
                             if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, vd0, pr0, count_local);
                             if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, vd1, pr1, count_local);
@@ -1395,8 +1405,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
         const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
-        const PairRec pr0 = load_pair(d, (size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0, want_jump);
-        const PairRec pr1 = load_pair(d, (size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1, want_jump);
+        const PairRec pr0 = load_pair(d, s_vh[j0] & 0xFFFFu, vd0, want_jump);
+        const PairRec pr1 = load_pair(d, s_vh[j1] & 0xFFFFu, vd1, want_jump);
         {
             const uint64_t bt = S + (r0.a & M52);
             const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
@@ -2375,12 +2385,21 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     const uint32_t fmt_env = env_u32z("SG_PAIR_FMT", 99);  // debugging: force a wider format
     if (fmt_env < D.pair_fmt) D.pair_fmt = fmt_env;
     D.gjmin = gjmin;
+    bool sym = D.pair_fmt != PAIR_WIDE && env_u32("SG_NO_TRI", 0) == 0;
+    for (size_t a = 0; sym && a < D.V; ++a)
+        for (size_t b = 0; sym && b < a; ++b) {
+            const size_t i = a * D.V + b, j = b * D.V + a;
+            sym = t->delay_ns[i] == t->delay_ns[j] && t->keep_max[i] == t->keep_max[j] &&
+                  t->jump_ms[i] == t->jump_ms[j];
+        }
+    D.tri = sym ? 1 : 0;
+    const size_t NT = D.tri ? (size_t)D.V * (D.V + 1) / 2 : VV;  // narrow table entries
     if (D.pair_fmt == PAIR_WIDE) {
         ALLOC(pairs, VV);
     } else {
-        if (D.pair_fmt == PAIR_NARROW) ALLOC(pairs8, VV);
-        else ALLOC(pdelay, VV);
-        ALLOC(pjump, VV);
+        if (D.pair_fmt == PAIR_NARROW) ALLOC(pairs8, NT);
+        else ALLOC(pdelay, NT);
+        ALLOC(pjump, NT);
     }
     D.pairs8 = pairs8;
     D.pdelay = pdelay;
@@ -2487,13 +2506,16 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }
     }
     std::vector<PairRec> pr(D.pair_fmt == PAIR_WIDE ? VV : 0);
-    std::vector<uint2> pr8(D.pair_fmt == PAIR_NARROW ? VV : 0);
-    std::vector<uint32_t> pd(D.pair_fmt == PAIR_DELAY ? VV : 0), pj(D.pair_fmt != PAIR_WIDE ? VV : 0);
+    std::vector<uint2> pr8(D.pair_fmt == PAIR_NARROW ? NT : 0);
+    std::vector<uint32_t> pd(D.pair_fmt == PAIR_DELAY ? NT : 0), pj(D.pair_fmt != PAIR_WIDE ? NT : 0);
     for (size_t i = 0; i < VV; ++i) {
+        const size_t a = i / D.V, b = i % D.V;
+        if (D.tri && b > a) continue;  // the lower triangle (a >= b) holds every pair
+        const size_t o = D.tri ? a * (a + 1) / 2 + b : i;  // pair_index
         if (D.pair_fmt == PAIR_WIDE) pr[i] = PairRec{t->delay_ns[i], t->keep_max[i], t->jump_ms[i]};
-        else if (D.pair_fmt == PAIR_NARROW) pr8[i] = make_uint2((uint32_t)t->delay_ns[i], (uint32_t)t->keep_max[i]);
-        else pd[i] = (uint32_t)t->delay_ns[i];
-        if (D.pair_fmt != PAIR_WIDE) pj[i] = t->jump_ms[i];
+        else if (D.pair_fmt == PAIR_NARROW) pr8[o] = make_uint2((uint32_t)t->delay_ns[i], (uint32_t)t->keep_max[i]);
+        else pd[o] = (uint32_t)t->delay_ns[i];
+        if (D.pair_fmt != PAIR_WIDE) pj[o] = t->jump_ms[i];
     }
     std::vector<uint64_t> vs(D.V);
     for (size_t v = 0; v < D.V; ++v) vs[v] = t->delay_ns[v * D.V + v];
@@ -2507,9 +2529,9 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         err = err != hipSuccess ? err : hipMemcpy(vtab16, vt.data(), N * 2, hipMemcpyHostToDevice);
     }
     if (pairs) err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
-    if (pairs8) err = err != hipSuccess ? err : hipMemcpy(pairs8, pr8.data(), VV * sizeof(uint2), hipMemcpyHostToDevice);
-    if (pdelay) err = err != hipSuccess ? err : hipMemcpy(pdelay, pd.data(), VV * 4, hipMemcpyHostToDevice);
-    if (pjump) err = err != hipSuccess ? err : hipMemcpy(pjump, pj.data(), VV * 4, hipMemcpyHostToDevice);
+    if (pairs8) err = err != hipSuccess ? err : hipMemcpy(pairs8, pr8.data(), NT * sizeof(uint2), hipMemcpyHostToDevice);
+    if (pdelay) err = err != hipSuccess ? err : hipMemcpy(pdelay, pd.data(), NT * 4, hipMemcpyHostToDevice);
+    if (pjump) err = err != hipSuccess ? err : hipMemcpy(pjump, pj.data(), NT * 4, hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(vself, vs.data(), D.V * sizeof(uint64_t), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(D.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemset(D.rs, 0, sizeof(RoundState));

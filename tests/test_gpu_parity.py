@@ -214,16 +214,22 @@ def test_path_counters_off_by_default():
     assert eng.path_counts().size == 0
 
 
-@pytest.mark.parametrize("fmt,probe,light,light_q", [(0, False, 2, 1), (1, False, 2, 1), (2, True, 2, 1),
-                                                    (2, False, 0, 1), (2, False, 2, 99)])
-def test_forced_wide_tables(fmt, probe, light, light_q, monkeypatch):
+@pytest.mark.parametrize("fmt,probe,light,light_q,tri", [(0, False, 2, 1, 1), (1, False, 2, 1, 1),
+                                                        (2, True, 2, 1, 1), (2, False, 0, 1, 1),
+                                                        (2, False, 2, 99, 1), (2, False, 2, 1, 0),
+                                                        (1, False, 2, 1, 0)])
+def test_forced_wide_tables(fmt, probe, light, light_q, tri, monkeypatch):
     """configs[3] keeps every packet and has uniform weights, so the engine picks
     the 4-byte delay-only path records and the 2-byte vertex table (the guessed
     host is the drawn one for every x).  Forcing the 16-byte (0) or 8-byte (1)
     path records, or the three-record destination probe, or sending every
     host's sends through phases B and C, or running every light host inline,
-    must give the same bits (the switches are read at sg_engine_create)."""
+    must give the same bits (the switches are read at sg_engine_create).  Its
+    paths are symmetric, so the narrow tables hold the lower triangle only;
+    tri=0 forces the full V*V tables."""
     monkeypatch.setenv("SG_PAIR_FMT", str(fmt))
+    if not tri:
+        monkeypatch.setenv("SG_NO_TRI", "1")
     if probe:
         monkeypatch.setenv("SG_NO_EXACT_DST", "1")
     monkeypatch.setenv("SG_LIGHT_MAX", str(light))  # 0: every host's sends through phases B and C
