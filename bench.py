@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--hosts", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-drop-in", action="store_true",
+                    help="skip the Mode P (drop-in gpu SchedulerPolicy) leg")
     ap.add_argument("--cpu-rounds", type=int, default=12)
     ap.add_argument("--cpu-workers", type=int,
                     default=min(16, len(os.sched_getaffinity(0))),
@@ -111,6 +113,22 @@ def cpu_baseline(cfg, warmup, rounds, workers):
                       f"Shadow round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} "
                       f"timed ({r['marked_pops']} events, {r['marked_seconds']:.2f} s); "
                       f"single_thread_value is -w 1 on the same rounds"}
+
+
+def drop_in_policy(cfg, warmup, rounds, workers):
+    """The drop-in `gpu` SchedulerPolicy (Mode P, sg_policy.c + sg_policy_dev.hip)
+    under the same Shadow-style round driver and sample as cpu_baseline: CPU
+    workers execute the PHOLD bodies and push/pop through the C-ABI, the GPU
+    keeps the per-host queues.  PCIe-inclusive by construction (the boundary
+    hands over host records), so it is reported beside `value`, never as it."""
+    from shadow_amd import policy
+    r = policy.run_phold(cfg, workers, policy.gpu_ops(workers, cfg["n_hosts"]),
+                         max_rounds=warmup + rounds, mark_round=warmup)
+    return {"value": r["marked_pops"] / r["marked_seconds"], "unit": "events/s",
+            "workers": workers,
+            "sample": f"gpu SchedulerPolicy (Mode P) with {workers} CPU workers under the Shadow "
+                      f"round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} timed "
+                      f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s)"}
 
 
 def run_single(args):
@@ -186,6 +204,8 @@ def run_single(args):
     }
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)
+    if not args.no_drop_in:
+        res["drop_in_policy"] = drop_in_policy(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)
     return res
 
 

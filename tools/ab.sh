@@ -10,7 +10,7 @@ if [ -z "$NO_TESTS" ]; then
 fi
 for v in "$@"; do
   name=${v%%:*}; envs=${v#*:}
-  env ${envs//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/ab/bench_$name.log 2>&1 || { tail -5 gpurun_out/ab/bench_$name.log; exit 1; }
+  env ${envs//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline --no-drop-in > gpurun_out/ab/bench_$name.log 2>&1 || { tail -5 gpurun_out/ab/bench_$name.log; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/ab/bench_$name.log'));print('$name value %.4g'%d['value'], {k:round(v,2) for k,v in d['roofline']['kernel_us_per_round'].items()})"
 done
 if [ -n "$STAMPS" ]; then

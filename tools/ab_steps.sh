@@ -7,7 +7,7 @@ mkdir -p gpurun_out/ab
 timeout -k 10 300 python -u -m pytest tests/test_gpu_sharded.py -x -q --timeout 120 --timeout-method thread -k "native or graph" > gpurun_out/ab/pytest_new.log 2>&1
 rc=$?; tail -3 gpurun_out/ab/pytest_new.log; [ $rc = 0 ] || exit $rc
 for g in 0 32; do
-  timeout -k 10 200 python bench.py --no-cpu-baseline --graph $g > gpurun_out/ab/single_g$g.json 2> gpurun_out/ab/single_g$g.err || { tail -5 gpurun_out/ab/single_g$g.err; exit 1; }
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-drop-in --graph $g > gpurun_out/ab/single_g$g.json 2> gpurun_out/ab/single_g$g.err || { tail -5 gpurun_out/ab/single_g$g.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/ab/single_g$g.json'));print('single graph=$g', '%.4g'%d['value'], round(d['ms_per_step']*1e3,1),'us/round')"
 done
 port=29541

@@ -12,5 +12,5 @@ for hosts in 125000 1000000; do
     bench.py --gpus 1 --dist --hosts $hosts --steps 200 --warmup 10 > gpurun_out/chk/d_$hosts.log 2>&1 || { tail -20 gpurun_out/chk/d_$hosts.log; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/chk/d_$hosts.log').read().strip().splitlines()[-1]);print('dist $hosts', '%.4g'%d['value'], round(d['ms_per_step']*1e3,1),'us/step')"
 done
-timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/chk/single.json 2> gpurun_out/chk/single.err || { tail -5 gpurun_out/chk/single.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-drop-in > gpurun_out/chk/single.json 2> gpurun_out/chk/single.err || { tail -5 gpurun_out/chk/single.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/chk/single.json'));print('single', '%.4g'%d['value'], round(d['ms_per_step']*1e3,1),'us/round', {k:round(v,2) for k,v in d['roofline']['kernel_us_per_round'].items()})"

@@ -12,5 +12,5 @@ run() {  # name timeout cmd...
   case $rc in 0) return 0;; *) echo "stopping after $name"; exit $rc;; esac
 }
 run cal 300 python -u tools/cal_check.py ${CAL_ARGS:-}
-run bench 300 python -u bench.py --no-cpu-baseline ${BENCH_ARGS:-}
+run bench 300 python -u bench.py --no-cpu-baseline --no-drop-in ${BENCH_ARGS:-}
 [ -n "$NO_TRACE" ] || TAILN=30 run ktrace 400 bash tools/ktrace.sh

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/prof}
 mkdir -p $OUT
-BARGS="${PMC_BENCH_ARGS:---steps 20 --warmup 20 --kernel-rounds 1 --no-cpu-baseline}"
+BARGS="${PMC_BENCH_ARGS:---steps 20 --warmup 20 --kernel-rounds 1 --no-cpu-baseline --no-drop-in}"
 pass() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT/$name -o $name --output-format csv -- python bench.py $BARGS > $OUT/$name.log 2>&1

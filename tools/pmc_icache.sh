@@ -7,7 +7,7 @@ i=0
 for grp in "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE" \
            "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH SQ_IFETCH_LEVEL SQ_BUSY_CYCLES SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp -d gpurun_out/ic/p$i -o p$i --output-format csv -- python bench.py --steps 10 --warmup 20 --no-cpu-baseline > gpurun_out/ic/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/ic/p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d gpurun_out/ic/p$i -o p$i --output-format csv -- python bench.py --steps 10 --warmup 20 --no-cpu-baseline --no-drop-in > gpurun_out/ic/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/ic/p$i.log; exit 1; }
 done
 python - <<'PY'
 import csv, collections, glob
