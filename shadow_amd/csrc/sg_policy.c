@@ -18,8 +18,10 @@
  */
 #define _GNU_SOURCE
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "sg_policy_dev.h"
 #include "shadowgpu.h"
@@ -119,7 +121,16 @@ struct sg_policy {
     uint32_t* self_list;      /* hosts whose CPU heap may hold events */
     uint32_t n_self;
     pthread_mutex_t self_lock;
+    /* SG_POLICY_PROF=1: seconds in the serial sections, printed at destroy */
+    int prof;
+    double t_gather, t_insert, t_min, t_extract, t_runs;
 };
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
 
 static uint32_t hash32(uint32_t x) {
     x ^= x >> 16;
@@ -176,12 +187,18 @@ int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
     pthread_mutex_init(&p->foreign_lock, NULL);
     pthread_mutex_init(&p->self_lock, NULL);
     p->prepared = SG_SIMTIME_INVALID;
+    const char* pe = getenv("SG_POLICY_PROF");
+    p->prof = pe && *pe == '1';
     *out = p;
     return SG_OK;
 }
 
 int sg_policy_destroy(sg_policy* p) {
     if (!p) return SG_OK;
+    if (p->prof)
+        fprintf(stderr, "sg_policy serial sections (s): flush gather %.3f insert %.3f min %.3f; "
+                "prepare extract %.3f runs %.3f\n", p->t_gather, p->t_insert, p->t_min, p->t_extract,
+                p->t_runs);
     if (p->dev) sgp_dev_destroy(p->dev);
     if (p->hosts)
         for (uint32_t i = 0; i < p->n_hosts; i++) {
@@ -304,7 +321,9 @@ static int prepare(sg_policy* p, sg_simtime barrier) {
         const sgp_rec* runs;
         const uint32_t *off, *cnt;
         uint64_t total;
+        double t0 = p->prof ? now_s() : 0;
         int rc = sgp_dev_extract(p->dev, barrier, &runs, &off, &cnt, &total);
+        double t1 = p->prof ? now_s() : 0;
         if (rc == 0) {
             p->runs = runs;
             for (uint32_t i = 0; i < p->n_hosts; i++) {
@@ -312,6 +331,10 @@ static int prepare(sg_policy* p, sg_simtime barrier) {
                 p->hosts[i].run_len = cnt[i];
                 p->hosts[i].run_pos = 0;
             }
+        }
+        if (p->prof) {
+            p->t_extract += t1 - t0;
+            p->t_runs += now_s() - t1;
         }
         pthread_mutex_lock(&p->m);
         if (rc) p->error = rc;
@@ -362,6 +385,7 @@ int sg_policy_pop(sg_policy* p, uint64_t token, sg_simtime barrier, uint64_t* ha
 /* Last arriver: deliver every staged event (and left-over CPU heap entries) to
  * HBM, then reduce the MIN. */
 static int flush(sg_policy* p) {
+    double t0 = p->prof ? now_s() : 0;
     uint64_t total = p->nf;
     for (uint32_t i = 0; i < p->n_threads; i++) total += p->threads[i].na;
     for (uint32_t k = 0; k < p->n_self; k++) total += p->hosts[p->self_list[k]].selfq.n;
@@ -385,10 +409,19 @@ static int flush(sg_policy* p) {
         h->in_self_list = 0;
     }
     p->n_self = 0;
+    double t1 = p->prof ? now_s() : 0;
     int rc = sgp_dev_insert(p->dev, all, n);
     free(all);
     if (rc) return rc;
-    return sgp_dev_min(p->dev, &p->next_min);
+    double t2 = p->prof ? now_s() : 0;
+    rc = sgp_dev_min(p->dev, &p->next_min);
+    if (p->prof) {
+        double t3 = now_s();
+        p->t_gather += t1 - t0;
+        p->t_insert += t2 - t1;
+        p->t_min += t3 - t2;
+    }
+    return rc;
 }
 
 int sg_policy_next_time(sg_policy* p, uint64_t token, sg_simtime* next_out) {

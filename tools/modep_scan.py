@@ -1,0 +1,20 @@
+"""Mode P (drop-in gpu SchedulerPolicy) vs the host_steal restatement at several
+worker counts on the bench workload (rounds 12..24 timed)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from shadow_amd import phold, policy  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+n = int(os.environ.get("HOSTS", "1000000"))
+cfg = phold.c4_config(n_hosts=n)
+for w in [int(x) for x in os.environ.get("WORKERS", "1,4,16").split(",")]:
+    for kind in ("gpu", "steal"):
+        ops = policy.gpu_ops(w, n) if kind == "gpu" else O.cpu_policy_ops(True, w, n)
+        t = time.perf_counter()
+        r = policy.run_phold(cfg, w, ops, max_rounds=24, mark_round=12)
+        print(f"{kind:5s} w={w:2d}: {r['marked_pops'] / r['marked_seconds']:.3e} events/s "
+              f"({r['marked_seconds'] * 1e3 / 12:.1f} ms/round; total {time.perf_counter() - t:.1f} s)",
+              flush=True)
