@@ -141,6 +141,9 @@ struct RoundState {
     uint64_t rmin;           // min time in buckets beyond bL (exact, at plan time)
     uint64_t ndue;           // due chunk entries
     uint64_t ndueb;          // listed non-retained buckets (reset at the next plan)
+    uint64_t nfree;          // due chunks outside the retained bucket (a prefix of the list):
+                             // k_gather returns them to the free ring behind fl_tail
+    uint64_t rmin_todo;      // k_plan listed a window: k_scatter's last workgroup computes rmin
     uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
     uint64_t fl_head, fl_tail;
     uint64_t ins_local;      // k_count took the staged local events (process step)
@@ -649,6 +652,19 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
     if (d.outn && blockIdx.x == 0 && threadIdx.x < d.G) {  // a process step refills the outboxes
         d.outn[threadIdx.x] = 0;
         d.sent[threadIdx.x] = 0;
+    }
+    {
+        // the window's chunks outside the retained bucket go back to the free
+        // ring behind fl_tail (k_plan advances the tail once the round is done;
+        // their events are read below, and nothing allocates before k_plan)
+        const uint64_t nf = rs->nfree, tail = rs->fl_tail;
+        const uint32_t NCH = d.NCH, tail_r = (uint32_t)(tail % NCH);
+        for (uint64_t i = c0 + threadIdx.x; i < c1 && i < nf; i += K1_T) {
+            const DueEnt de = d.due[i];
+            if ((de.nflags & RETAINED) || de.id >= NCH) continue;  // not after the prefix
+            const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
+            d.fring[pos >= NCH ? pos - NCH : pos] = de.id;
+        }
     }
     for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
         s_cnt[p] = 0;
@@ -1667,12 +1683,34 @@ __device__ __forceinline__ void place_event(const Dev& d, uint32_t* s_cur, uint6
 }
 
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
-    const RoundState* rs = d.rs;
+    RoundState* rs = d.rs;
     if (rs->done) return;
     __shared__ uint32_t s_off[MAXG];
     __shared__ uint32_t s_cur[RMAX];
     __shared__ uint64_t s16[16];
     const uint32_t R = d.R, blk = blockIdx.x;
+    if (blk == gridDim.x - 1) {
+        // rmin for the window k_plan just listed: the first non-empty bucket in
+        // (bL, bS + R) and its min time.  k_plan wrote the metadata back; this
+        // launch only writes pool slots, so the counts it reads are final.
+        if (!rs->rmin_todo) return;
+        const uint64_t bS = rs->bS, bL = rs->bL;
+        const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
+        uint64_t first = UINT64_MAX;
+        for (uint32_t o = threadIdx.x + 1; o + span < R; o += K3_T) {
+            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
+            if (d.bcnt[rb] > d.btomb[rb]) {
+                const uint64_t b = bL + o;
+                first = b < first ? b : first;
+            }
+        }
+        first = block_min(first, s16);  // barriers inside
+        if (threadIdx.x == 0) {
+            rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : d.bmin[first % R];
+            rs->rmin_todo = 0;
+        }
+        return;
+    }
     const uint32_t* wb = d.wbase + (size_t)blk * R;
     if (blk < d.P) {  // partition blk's staged local events
         if (!rs->ins_local) return;
@@ -1721,7 +1759,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     }
     for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
     const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
-    const uint32_t g3 = gridDim.x - d.P, w = blk - d.P;
+    const uint32_t g3 = gridDim.x - 1 - d.P, w = blk - d.P;
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
     for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
         uint64_t t, k;
@@ -1875,25 +1913,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     }
     const bool round_done = mode == 0 || (mode == 1 && !s_more);
     if (round_done) {
-        // free the chunks of the window just executed (not the retained
-        // bucket's) and reset its fully consumed buckets
-        const uint64_t nd = rs->ndue, tail = s_tail, ndb = rs->ndueb;
-        const uint32_t tail_r = (uint32_t)(tail % NCH);
-        uint64_t mine = 0;
-        for (uint64_t i = tid; i < nd; i += PL_T) {
-            const DueEnt de = d.due[i];
-            mine += !(de.nflags & RETAINED) && de.id < NCH;
-        }
-        uint64_t tot;
-        uint64_t k = block_excl_scan(mine, s16, &tot);
-        for (uint64_t i = tid; i < nd; i += PL_T) {
-            const DueEnt de = d.due[i];
-            if ((de.nflags & RETAINED) || de.id >= NCH) continue;
-            const uint64_t pos = tail_r + k++;  // k < NCH: one wrap at most
-            d.fring[pos >= NCH ? pos - NCH : pos] = de.id;
-        }
-        // (their chunk tables are not cleared: nothing reads btab past nal, which resets)
-        __syncthreads();
+        // k_gather returned the window's chunks (not the retained bucket's) to
+        // the ring behind the tail: take them, and reset the consumed buckets
+        const uint64_t ndb = rs->ndueb;
         for (uint64_t i = tid; i < ndb; i += PL_T) {
             const uint32_t rb = d.dueb[i];
             B.cnt[rb] = 0;
@@ -1901,7 +1923,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             B.nal[rb] = 0;
             B.mn[rb] = UINT64_MAX;
         }
-        if (tid == 0) s_tail = tail + tot;
+        if (tid == 0) s_tail = s_tail + rs->nfree;
         __syncthreads();
     }
     PSTAMP(2);
@@ -2010,7 +2032,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // Fully due buckets keep their tables until the next plan (k_scatter of
         // this round still writes the events k_count counted into them).
         const bool straddle = E < (bL + 1) * W;
-        uint64_t nd = 0, ndb = 0;
+        uint64_t nd = 0, ndb = 0, nf = 0;
         for (uint64_t b = bS; b <= bL; ++b) {
             const uint32_t rb = (uint32_t)(b % R);
             const uint32_t c = B.cnt[rb], nc = B.nal[rb];
@@ -2022,30 +2044,37 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
                 d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
             }
             nd += nc;
+            nf += ret ? 0 : nc;
             if (tid == 0 && !ret && c) d.dueb[ndb] = rb;
             if (!ret && c) ++ndb;
         }
         __syncthreads();
         PSTAMP(5);
         if (straddle && tid == 0) B.mn[bL % R] = UINT64_MAX;  // k_gather's carry min and k_count restore it
-        // exact min beyond the window: the first non-empty bucket in (bL, bS + R)
-        // (the window's own slots lie outside that range; the spent slot is empty)
+        // exact min beyond the window: the first non-empty bucket in (bL, bS + R).
+        // Off the plan's critical path: k_scatter's last workgroup finds it
+        // from the written-back metadata (first_live_bucket) — except at boot,
+        // where no k_scatter follows.
         uint64_t first = UINT64_MAX;
-        const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
-        for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
-            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
-            if (rb == s_spent) continue;
-            if (B.cnt[rb] > B.tomb[rb]) {
-                const uint64_t b = bL + o;
-                first = b < first ? b : first;
+        if (mode == 2) {
+            const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
+            for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
+                const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
+                if (rb == s_spent) continue;
+                if (B.cnt[rb] > B.tomb[rb]) {
+                    const uint64_t b = bL + o;
+                    first = b < first ? b : first;
+                }
             }
+            first = block_min(first, s16);  // barriers inside
         }
-        first = block_min(first, s16);  // barriers inside
         if (tid == 0) {
-            rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : B.mn[first % R];
+            if (mode == 2) rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : B.mn[first % R];
+            rs->rmin_todo = mode != 2;
             rs->bS = bS;
             rs->bL = bL;
             rs->ndue = nd;
+            rs->nfree = nf;
             rs->ndueb = ndb;
             rs->ret_b = straddle ? bL : UINT64_MAX;
         }
@@ -2634,7 +2663,7 @@ static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
     });
     if (rc) return rc;
     return timed_launch(e, SG_K_INSERT, [&] {
-        hipLaunchKernelGGL(k_scatter, dim3(d.P + (recv ? d.G3 : 0)), dim3(K3_T), 0, e->stream, d, recv);
+        hipLaunchKernelGGL(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + 1), dim3(K3_T), 0, e->stream, d, recv);
     });
 }
 
