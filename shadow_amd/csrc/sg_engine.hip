@@ -154,6 +154,7 @@ struct RoundState {
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
     uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
     uint64_t xacc[2];    // emitted min, discovery min of this launch's workgroups (atomics)
+    uint64_t xcarry;     // carry min of k_gather's workgroups (atomics; read by k_plan mode 0)
 };
 
 struct Dev {
@@ -575,6 +576,7 @@ __global__ void k_boot(Dev d) {
         rs->ticket = 0;
         rs->xacc[0] = UINT64_MAX;
         rs->xacc[1] = UINT64_MAX;
+        rs->xcarry = UINT64_MAX;
     }
     if (i < d.G && d.outn) {
         d.outn[i] = 0;
@@ -755,6 +757,7 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
     const uint64_t nt = block_sum(ntomb, s16);
     if (threadIdx.x == 0) {
         d.c1min[blockIdx.x] = m;
+        if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry, (unsigned long long)m);
         if (rs->ret_b != UINT64_MAX) {
             const uint32_t rb = (uint32_t)(rs->ret_b % d.R);
             if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
@@ -1542,7 +1545,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         if (i < NCTR) d.pcum[(size_t)i * d.P + p] += r;
         else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
-        if (i >= NCTR && d.xsend) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
+        if (i >= NCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
     }
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
@@ -1827,6 +1830,7 @@ struct PlanLds {
     uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
     uint32_t off[RMAX];  // allocation: first new chunk of each bucket in this launch's run
     uint64_t mn[RMAX];
+    uint32_t fr[PL_T];   // the free ring's first PL_T entries from the head, read at launch
 };
 
 // mode 0: single shard, end of round.  mode 1: multi-shard, window from the
@@ -1858,6 +1862,13 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             rn[q] = d.nal[rb];
             rm[q] = d.bmin[rb];
         }
+    }
+    // the free ring from the head, for the allocation below (nothing writes
+    // the ring in this launch before the allocation reads it)
+    uint32_t fr0;
+    {
+        const uint64_t h0 = rs->fl_head;
+        fr0 = d.fring[(h0 + tid) % NCH];  // NCH may be below PL_T (small engines)
     }
     if (tid == 0) {
         s_head = rs->fl_head;
@@ -1891,9 +1902,22 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     }
     uint64_t m = 0, j = 0, ovf = 0;
     if (mode == 0) {
-        reduce_local(d, s16, m, j);  // barriers inside
+        // the local MIN terms, accumulated by k_gather's and k_proc's
+        // workgroups with device-scope atomics (reduce_local's terms)
+        const uint64_t cm = rs->xcarry, em = rs->xacc[0], jm = rs->xacc[1];
+        m = cm < em ? cm : em;
+        m = rs->rmin < m ? rs->rmin : m;
+        m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+        j = rs->jmin < jm ? rs->jmin : jm;
         ovf = rs->overflow;
+        __syncthreads();  // every thread has read them before thread 0 resets them
+        if (tid == 0) {
+            rs->xcarry = UINT64_MAX;
+            rs->xacc[0] = UINT64_MAX;
+            rs->xacc[1] = UINT64_MAX;
+        }
     }
+    B.fr[tid] = fr0;
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t rb = tid + q * PL_T;
@@ -1964,7 +1988,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
                 if (B.off[mid] <= i) lo = mid; else hi = mid - 1;
             }
             const uint32_t pos = head_r + i;  // give <= NCH: one wrap at most
-            d.btab[(size_t)lo * NCH + B.nal[lo] + (i - B.off[lo])] = d.fring[pos >= NCH ? pos - NCH : pos];
+            const uint32_t id = i < PL_T ? B.fr[i] : d.fring[pos >= NCH ? pos - NCH : pos];
+            d.btab[(size_t)lo * NCH + B.nal[lo] + (i - B.off[lo])] = id;
         }
         __syncthreads();
 #pragma unroll
