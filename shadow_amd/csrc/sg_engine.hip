@@ -655,19 +655,16 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         d.outn[threadIdx.x] = 0;
         d.sent[threadIdx.x] = 0;
     }
-    {
-        // the window's chunks outside the retained bucket go back to the free
-        // ring behind fl_tail (k_plan advances the tail once the round is done;
-        // their events are read below, and nothing allocates before k_plan)
-        const uint64_t nf = rs->nfree, tail = rs->fl_tail;
-        const uint32_t NCH = d.NCH, tail_r = (uint32_t)(tail % NCH);
-        for (uint64_t i = c0 + threadIdx.x; i < c1 && i < nf; i += K1_T) {
-            const DueEnt de = d.due[i];
-            if ((de.nflags & RETAINED) || de.id >= NCH) continue;  // not after the prefix
-            const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
-            d.fring[pos >= NCH ? pos - NCH : pos] = de.id;
-        }
-    }
+    // The window's chunks outside the retained bucket go back to the free ring
+    // behind fl_tail, from the due entries as they are staged below (k_plan
+    // advances the tail once the round is done; nothing allocates before it).
+    const uint64_t nfree = rs->nfree;
+    const uint32_t tail_r = (uint32_t)(rs->fl_tail % d.NCH);
+    auto free_chunk = [&](const DueEnt& de, uint64_t i) {
+        if (i >= nfree || (de.nflags & RETAINED) || de.id >= d.NCH) return;  // not in the prefix
+        const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
+        d.fring[pos >= d.NCH ? pos - d.NCH : pos] = de.id;
+    };
     for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
@@ -686,7 +683,11 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
     if ((c1 - c0) * CH <= (uint64_t)GREG * K1_T) {
         // the workgroup's chunks fit in registers: load once, count, reserve, scatter
         const uint32_t nb = (uint32_t)(c1 - c0), tot = nb * CH;
-        if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[c0 + threadIdx.x];
+        if (threadIdx.x < nb) {
+            const DueEnt de = d.due[c0 + threadIdx.x];
+            s_de[threadIdx.x] = de;
+            free_chunk(de, c0 + threadIdx.x);
+        }
         __syncthreads();
         const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
         Rec r[GREG];
@@ -748,7 +749,11 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
             const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
             __syncthreads();
-            if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+            if (threadIdx.x < nb) {
+                const DueEnt de = d.due[cb + threadIdx.x];
+                s_de[threadIdx.x] = de;
+                free_chunk(de, cb + threadIdx.x);
+            }
             __syncthreads();
             gather_pass<true>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
         }
