@@ -169,6 +169,7 @@ struct Dev {
     const uint16_t* vtab16;   // [N] attachment vertex only, when dst_exact
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
     uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
+    uint32_t gather_t;        // k_gather workgroup size (256 or 1024)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
     const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
@@ -591,20 +592,19 @@ __global__ void k_boot(Dev d) {
 // pass is independent of the others.
 constexpr uint32_t GDMAX = 32;   // due entries staged per batch
 constexpr int GUNR = 4;          // events in flight per thread (two-pass path)
-constexpr int GREG = 16;         // events per thread kept in registers (one-pass path: 4 chunks)
 
-template <bool SCATTER>
+template <bool SCATTER, int GT>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
                                             uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
                                             uint64_t& cmin, uint64_t& ntomb) {
     const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
     const uint32_t tot = nb * CH;
-    for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += K1_T * GUNR) {
+    for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += GT * GUNR) {
         Rec r[GUNR];
         bool v[GUNR];
 #pragma unroll
         for (int q = 0; q < GUNR; ++q) {
-            const uint32_t e = e0 + q * K1_T;
+            const uint32_t e = e0 + q * GT;
             const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
             v[q] = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
             r[q] = v[q] ? d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))] : Rec{TOMB, 0};
@@ -612,7 +612,7 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
 #pragma unroll
         for (int q = 0; q < GUNR; ++q) {
             if (!v[q] || r[q].a == TOMB) continue;
-            const uint32_t e = e0 + q * K1_T;
+            const uint32_t e = e0 + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             const uint64_t t = de.base + (r[q].a & M40);
             const uint32_t dl = (uint32_t)(r[q].a >> 40);
@@ -640,7 +640,11 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
     }
 }
 
-__global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
+// GT threads per workgroup (SG_GATHER_T: 256 or 1024), GR events per thread
+// in registers on the one-pass path (4 chunks per workgroup either way).
+template <int GT>
+__global__ __launch_bounds__(GT) void k_gather(Dev d) {
+    constexpr int GR = 4 * (int)CH / GT;
     const RoundState* rs = d.rs;
     if (rs->done | rs->phase) return;
     __shared__ uint32_t s_cnt[PMAX];
@@ -665,13 +669,13 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
         d.fring[pos >= d.NCH ? pos - d.NCH : pos] = de.id;
     };
-    for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
+    for (uint32_t p = threadIdx.x; p < P; p += GT) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
     }
     uint64_t cmin = UINT64_MAX, ntomb = 0;
     auto reserve = [&]() {  // one reservation per partition this workgroup feeds
-        for (uint32_t p = threadIdx.x; p < P; p += K1_T) {
+        for (uint32_t p = threadIdx.x; p < P; p += GT) {
             const uint32_t c = s_cnt[p];
             if (c) {
                 const uint32_t base = atomicAdd(&d.pcnt[p], c);
@@ -680,7 +684,7 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
             }
         }
     };
-    if ((c1 - c0) * CH <= (uint64_t)GREG * K1_T) {
+    if ((c1 - c0) * CH <= (uint64_t)GR * GT) {
         // the workgroup's chunks fit in registers: load once, count, reserve, scatter
         const uint32_t nb = (uint32_t)(c1 - c0), tot = nb * CH;
         if (threadIdx.x < nb) {
@@ -690,21 +694,21 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         }
         __syncthreads();
         const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
-        Rec r[GREG];
-        uint32_t pp[GREG];  // partition of the event, UINT32_MAX: not gathered
+        Rec r[GR];
+        uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
 #pragma unroll
-        for (int q = 0; q < GREG; ++q) {  // every load unconditional (clamped address)
-            const uint32_t e = threadIdx.x + q * K1_T;
+        for (int q = 0; q < GR; ++q) {  // every load unconditional (clamped address)
+            const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
             const bool v = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
             r[q] = d.pool[v ? ((size_t)de.id << CH_SHIFT) + (e & (CH - 1)) : 0];
             if (!v) r[q].a = TOMB;
         }
 #pragma unroll
-        for (int q = 0; q < GREG; ++q) {
+        for (int q = 0; q < GR; ++q) {
             pp[q] = UINT32_MAX;
             if (r[q].a == TOMB) continue;
-            const uint32_t e = threadIdx.x + q * K1_T;
+            const uint32_t e = threadIdx.x + q * GT;
             const uint64_t t = s_de[e >> CH_SHIFT].base + (r[q].a & M40);
             const uint32_t dl = (uint32_t)(r[q].a >> 40);
             if (dl >= d.L) {
@@ -723,12 +727,12 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
         reserve();
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < GREG; ++q) {
+        for (int q = 0; q < GR; ++q) {
             if (pp[q] == UINT32_MAX) continue;
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             if (slot < d.CAPP) d.part[(size_t)p * d.CAPP + slot] = r[q];
-            const uint32_t e = threadIdx.x + q * K1_T;
+            const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
@@ -742,7 +746,7 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
             __syncthreads();
             if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
             __syncthreads();
-            gather_pass<false>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
         }
         __syncthreads();
         reserve();
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(K1_T) void k_gather(Dev d) {
                 free_chunk(de, cb + threadIdx.x);
             }
             __syncthreads();
-            gather_pass<true>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
         }
     }
     const uint64_t m = block_min(cmin, s16);
@@ -2369,6 +2373,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
+    d.gather_t = env_u32("SG_GATHER_T", 1024) == 1024 ? 1024 : K1_T;
     // host partitions: HP hosts per k_proc workgroup (power of two), about
     // one partition per CU
     const uint32_t hp_env = env_u32("SG_HP", 0);
@@ -2668,7 +2673,10 @@ int sg_engine_boot(sg_engine* e) {
 static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
     int rc = timed_launch(e, SG_K_GATHER, [&] {
-        hipLaunchKernelGGL(k_gather, dim3(d.G1), dim3(K1_T), 0, e->stream, d);
+        if (d.gather_t == 1024)
+            hipLaunchKernelGGL(k_gather<1024>, dim3(d.G1), dim3(1024), 0, e->stream, d);
+        else
+            hipLaunchKernelGGL(k_gather<K1_T>, dim3(d.G1), dim3(K1_T), 0, e->stream, d);
     });
     if (rc) return rc;
     return timed_launch(e, SG_K_PROCESS, [&] {

@@ -251,3 +251,12 @@ def test_long_paths_use_wide_records():
     eng, orc = _run_both(cfg, trace=200_000)
     gs = _assert_same(eng, orc)
     assert gs["pops"] > 0
+
+
+def test_gather_workgroup_256(monkeypatch):
+    """k_gather is built for 1024- and 256-lane workgroups (SG_GATHER_T); the
+    non-default one must give the same bits, boot round (two-pass path) included."""
+    monkeypatch.setenv("SG_GATHER_T", "256")
+    cfg = phold.c4_config(n_hosts=20_000)
+    eng, orc = _run_both(cfg, max_rounds=40)
+    _assert_same(eng, orc)
