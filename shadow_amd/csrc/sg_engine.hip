@@ -1728,19 +1728,27 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         if (!rs->ins_local) return;
         const uint32_t n = d.rcnt[blk];
         if (n == 0) return;
-        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
-        __syncthreads();
         const uint64_t S = rs->ins_S, W = d.W;
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
         // SU events per thread in flight: every load of a batch is issued
-        // before any is used (staged record, then chunk table + allocation)
+        // before any is used (staged record, then chunk table + allocation);
+        // the first batch's records are loaded together with the cursors
         constexpr int SU = 4;
-        for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
-            Rec r[SU];
+        Rec r[SU];
 #pragma unroll
-            for (int q = 0; q < SU; ++q) {
-                const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                r[q] = src[i < n ? i : 0];
+        for (int q = 0; q < SU; ++q) {
+            const uint32_t i = threadIdx.x + q * K3_T;
+            r[q] = src[i < n ? i : 0];
+        }
+        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+            if (i0) {
+#pragma unroll
+                for (int q = 0; q < SU; ++q) {
+                    const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                    r[q] = src[i < n ? i : 0];
+                }
             }
             uint32_t rb[SU], pos[SU];
 #pragma unroll
