@@ -78,12 +78,13 @@ static void sheap_pop(sheap* h) {
 
 /* ---------------------------------------------------------------- state -- */
 typedef struct host_rt {
+    uint32_t run_pos;         /* next event of this round's extracted run ... */
+    uint32_t run_gen;         /* ... valid while equal to sg_policy.run_gen */
+    sheap selfq;
     uint32_t id;              /* GQuark */
     uint32_t thread;          /* owning thread slot */
-    uint32_t run_off, run_len, run_pos;
-    pthread_mutex_t lock;
-    sheap selfq;
     int in_self_list;
+    pthread_mutex_t lock;
 } host_rt;
 
 typedef struct thread_rt {
@@ -118,11 +119,15 @@ struct sg_policy {
     sg_simtime next_min;
     int error;
     const sgp_rec* runs;
+    const uint32_t *run_off, *run_len; /* per host index, from the last extract */
+    uint32_t run_gen;         /* bumped per extract: host run_pos values reset lazily */
     uint32_t* self_list;      /* hosts whose CPU heap may hold events */
     uint32_t n_self;
     pthread_mutex_t self_lock;
     /* SG_POLICY_PROF=1: seconds in the serial sections, printed at destroy */
     int prof;
+    int pinned;               /* worker arenas in pinned memory (SG_POLICY_PINNED=1; measured
+                               * no faster than pageable ones, so off by default) */
     double t_gather, t_insert, t_min, t_extract, t_runs;
 };
 
@@ -189,6 +194,8 @@ int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
     p->prepared = SG_SIMTIME_INVALID;
     const char* pe = getenv("SG_POLICY_PROF");
     p->prof = pe && *pe == '1';
+    const char* pp = getenv("SG_POLICY_PINNED");
+    p->pinned = pp && *pp == '1';
     *out = p;
     return SG_OK;
 }
@@ -208,7 +215,8 @@ int sg_policy_destroy(sg_policy* p) {
     if (p->threads)
         for (uint32_t i = 0; i < p->n_threads; i++) {
             free(p->threads[i].hosts);
-            free(p->threads[i].arena);
+            if (p->pinned) sgp_host_free(p->threads[i].arena);
+            else free(p->threads[i].arena);
         }
     free(p->hosts);
     free(p->map_key);
@@ -275,6 +283,21 @@ static int arena_push(sgp_rec** a, uint64_t* n, uint64_t* c, const sgp_rec* r) {
     return 0;
 }
 
+/* A worker's arena lives in pinned memory: the flush DMAs it in place. */
+static int arena_push_pinned(sgp_rec** a, uint64_t* n, uint64_t* c, const sgp_rec* r) {
+    if (*n == *c) {
+        uint64_t nc = *c ? 2 * *c : 65536;
+        sgp_rec* na = (sgp_rec*)sgp_host_alloc(nc * sizeof(sgp_rec));
+        if (!na) return -1;
+        if (*n) memcpy(na, *a, *n * sizeof(sgp_rec));
+        sgp_host_free(*a);
+        *a = na;
+        *c = nc;
+    }
+    (*a)[(*n)++] = *r;
+    return 0;
+}
+
 int sg_policy_push(sg_policy* p, uint64_t token, uint64_t handle, sg_simtime time, uint32_t src_id,
                    uint32_t dst_id, uint64_t src_event_id, sg_simtime barrier, sg_simtime* time_out) {
     int64_t di = host_index(p, dst_id);
@@ -302,13 +325,23 @@ int sg_policy_push(sg_policy* p, uint64_t token, uint64_t handle, sg_simtime tim
     thread_rt* t = thread_of(p, token);
     int rc;
     if (t) {
-        rc = arena_push(&t->arena, &t->na, &t->ca, &r);
+        rc = p->pinned ? arena_push_pinned(&t->arena, &t->na, &t->ca, &r)
+                       : arena_push(&t->arena, &t->na, &t->ca, &r);
     } else {
         pthread_mutex_lock(&p->foreign_lock);
         rc = arena_push(&p->foreign, &p->nf, &p->cf, &r);
         pthread_mutex_unlock(&p->foreign_lock);
     }
     return rc ? SG_ERR_NOMEM : SG_OK;
+}
+
+/* This round's run of host idx: its length, and run_pos reset on first use. */
+static uint32_t run_len(const sg_policy* p, uint32_t idx) { return p->run_len ? p->run_len[idx] : 0; }
+static void run_touch(sg_policy* p, host_rt* h) {
+    if (h->run_gen != p->run_gen) {
+        h->run_gen = p->run_gen;
+        h->run_pos = 0;
+    }
 }
 
 /* Extract the runs for `barrier` once; other threads wait for the leader. */
@@ -324,13 +357,11 @@ static int prepare(sg_policy* p, sg_simtime barrier) {
         double t0 = p->prof ? now_s() : 0;
         int rc = sgp_dev_extract(p->dev, barrier, &runs, &off, &cnt, &total);
         double t1 = p->prof ? now_s() : 0;
-        if (rc == 0) {
+        if (rc == 0) {  /* no per-host pass: pop reads off / cnt and resets run_pos lazily */
             p->runs = runs;
-            for (uint32_t i = 0; i < p->n_hosts; i++) {
-                p->hosts[i].run_off = off[i];
-                p->hosts[i].run_len = cnt[i];
-                p->hosts[i].run_pos = 0;
-            }
+            p->run_off = off;
+            p->run_len = cnt;
+            p->run_gen++;
         }
         if (p->prof) {
             p->t_extract += t1 - t0;
@@ -360,9 +391,16 @@ int sg_policy_pop(sg_policy* p, uint64_t token, sg_simtime barrier, uint64_t* ha
         t->cursor = 0;
     }
     while (t->cursor < t->n) {
-        host_rt* h = &p->hosts[t->hosts[t->cursor]];
+        const uint32_t idx = t->hosts[t->cursor];
+        host_rt* h = &p->hosts[idx];
+        const uint32_t len = run_len(p, idx);
+        run_touch(p, h);  /* only this thread pops, or pushes self events for, its hosts */
+        if (h->run_pos >= len && h->selfq.n == 0) {
+            t->cursor++; /* nothing left this round */
+            continue;
+        }
         pthread_mutex_lock(&h->lock);
-        const sgp_rec* a = h->run_pos < h->run_len ? &p->runs[h->run_off + h->run_pos] : NULL;
+        const sgp_rec* a = h->run_pos < len ? &p->runs[p->run_off[idx] + h->run_pos] : NULL;
         const sgp_rec* b = (h->selfq.n && h->selfq.a[0].time < barrier) ? &h->selfq.a[0] : NULL;
         uint64_t handle = 0;
         if (a && (!b || rec_less(a, b))) {
@@ -386,32 +424,43 @@ int sg_policy_pop(sg_policy* p, uint64_t token, sg_simtime barrier, uint64_t* ha
  * HBM, then reduce the MIN. */
 static int flush(sg_policy* p) {
     double t0 = p->prof ? now_s() : 0;
-    uint64_t total = p->nf;
-    for (uint32_t i = 0; i < p->n_threads; i++) total += p->threads[i].na;
-    for (uint32_t k = 0; k < p->n_self; k++) total += p->hosts[p->self_list[k]].selfq.n;
-    sgp_rec* all = (sgp_rec*)malloc((total ? total : 1) * sizeof(sgp_rec));
-    if (!all) return SG_ERR_NOMEM;
-    uint64_t n = 0;
-    for (uint32_t i = 0; i < p->n_threads; i++) {
-        thread_rt* t = &p->threads[i];
-        memcpy(all + n, t->arena, t->na * sizeof(sgp_rec));
-        n += t->na;
-        t->na = 0;
+    /* the workers' pinned arenas go to the device in place; foreign pushes
+     * and left-over CPU heap entries (few) are gathered into one more segment */
+    uint64_t extra = p->nf;
+    for (uint32_t k = 0; k < p->n_self; k++) extra += p->hosts[p->self_list[k]].selfq.n;
+    sgp_rec* ex = (sgp_rec*)malloc((extra ? extra : 1) * sizeof(sgp_rec));
+    const sgp_rec** segs = (const sgp_rec**)malloc((p->n_threads + 1) * sizeof *segs);
+    uint64_t* lens = (uint64_t*)malloc((p->n_threads + 1) * sizeof *lens);
+    if (!ex || !segs || !lens) {
+        free(ex);
+        free(segs);
+        free(lens);
+        return SG_ERR_NOMEM;
     }
-    memcpy(all + n, p->foreign, p->nf * sizeof(sgp_rec));
+    for (uint32_t i = 0; i < p->n_threads; i++) {
+        segs[i] = p->threads[i].arena;
+        lens[i] = p->threads[i].na;
+    }
+    uint64_t n = 0;
+    memcpy(ex, p->foreign, p->nf * sizeof(sgp_rec));
     n += p->nf;
     p->nf = 0;
     for (uint32_t k = 0; k < p->n_self; k++) {
         host_rt* h = &p->hosts[p->self_list[k]];
-        memcpy(all + n, h->selfq.a, h->selfq.n * sizeof(sgp_rec));
+        memcpy(ex + n, h->selfq.a, h->selfq.n * sizeof(sgp_rec));
         n += h->selfq.n;
         h->selfq.n = 0;
         h->in_self_list = 0;
     }
     p->n_self = 0;
+    segs[p->n_threads] = ex;
+    lens[p->n_threads] = n;
     double t1 = p->prof ? now_s() : 0;
-    int rc = sgp_dev_insert(p->dev, all, n);
-    free(all);
+    int rc = sgp_dev_insert_segs(p->dev, segs, lens, p->n_threads + 1);  /* synchronises */
+    for (uint32_t i = 0; i < p->n_threads; i++) p->threads[i].na = 0;   /* arenas reusable */
+    free(ex);
+    free(segs);
+    free(lens);
     if (rc) return rc;
     double t2 = p->prof ? now_s() : 0;
     rc = sgp_dev_min(p->dev, &p->next_min);
@@ -455,8 +504,9 @@ int sg_policy_remaining(sg_policy* p, uint64_t* handles, uint64_t cap, uint64_t*
         host_rt* h = &p->hosts[i];
         for (uint32_t k = 0; k < h->selfq.n; k++, n++)
             if (n < cap) handles[n] = h->selfq.a[k].handle;
-        for (uint32_t k = h->run_pos; k < h->run_len; k++, n++)
-            if (n < cap) handles[n] = p->runs[h->run_off + k].handle;
+        run_touch(p, h);
+        for (uint32_t k = h->run_pos; k < run_len(p, i); k++, n++)
+            if (n < cap) handles[n] = p->runs[p->run_off[i] + k].handle;
     }
     uint64_t nd = 0;
     sgp_rec* tmp = NULL;

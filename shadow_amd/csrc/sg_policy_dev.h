@@ -24,6 +24,12 @@ int sgp_dev_create(int device, uint32_t n_hosts, uint32_t cap, sgp_dev** out);
 int sgp_dev_destroy(sgp_dev* d);
 /* Deliver n records into the per-host HBM queues (grows them on demand). */
 int sgp_dev_insert(sgp_dev* d, const sgp_rec* recs, uint64_t n);
+/* The same for nseg host segments copied back to back (pinned segments DMA
+ * straight from where the workers staged them). */
+int sgp_dev_insert_segs(sgp_dev* d, const sgp_rec* const* segs, const uint64_t* lens, uint32_t nseg);
+/* Pinned host memory for the workers' staging arenas (NULL on failure). */
+void* sgp_host_alloc(uint64_t bytes);
+void sgp_host_free(void* p);
 /* MIN over every queued event time (SIMTIME_MAX if none). */
 int sgp_dev_min(sgp_dev* d, uint64_t* min_out);
 /* Remove every queued event with time < barrier; returns them in `runs`

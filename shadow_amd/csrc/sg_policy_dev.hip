@@ -333,12 +333,32 @@ int sgp_dev_destroy(sgp_dev* d) {
     return 0;
 }
 
+void* sgp_host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    return hipHostMalloc(&p, bytes ? bytes : 8, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void sgp_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int sgp_dev_insert(sgp_dev* d, const sgp_rec* recs, uint64_t n) {
+    return sgp_dev_insert_segs(d, &recs, &n, 1);
+}
+
+int sgp_dev_insert_segs(sgp_dev* d, const sgp_rec* const* segs, const uint64_t* lens, uint32_t nseg) {
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < nseg; ++i) n += lens[i];
     if (n == 0) return 0;
     PCHK(hipSetDevice(d->device));
     int rc = grow_in(d, n);
     if (rc) return rc;
-    PCHK(hipMemcpyAsync(d->d_in, recs, n * sizeof(sgp_rec), hipMemcpyHostToDevice, d->s));
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < nseg; ++i) {
+        if (lens[i])
+            PCHK(hipMemcpyAsync(d->d_in + o, segs[i], lens[i] * sizeof(sgp_rec), hipMemcpyHostToDevice, d->s));
+        o += lens[i];
+    }
     const sgp_rec* src = d->d_in;
     uint64_t m = n;
     for (int attempt = 0; attempt < 32; ++attempt) {

@@ -11,7 +11,7 @@ from oracle import oracle as O  # noqa: E402
 n = int(os.environ.get("HOSTS", "1000000"))
 cfg = phold.c4_config(n_hosts=n)
 for w in [int(x) for x in os.environ.get("WORKERS", "1,4,16").split(",")]:
-    for kind in ("gpu", "steal"):
+    for kind in os.environ.get("KINDS", "gpu,steal").split(","):
         ops = policy.gpu_ops(w, n) if kind == "gpu" else O.cpu_policy_ops(True, w, n)
         t = time.perf_counter()
         r = policy.run_phold(cfg, w, ops, max_rounds=24, mark_round=12)
