@@ -76,6 +76,13 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 constexpr int CH_SHIFT = 10;
 constexpr uint32_t CH = 1u << CH_SHIFT;  // events per chunk (16 KB)
 constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
+// Reservation shards: a workgroup reserves bucket slots in the counter of its
+// shard (workgroup index mod XS, which follows the XCD round-robin), so about
+// P / XS workgroups contend per counter instead of P; k_plan folds them.
+#ifndef SG_XS
+#define SG_XS 2
+#endif
+constexpr uint32_t XS = SG_XS;
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
@@ -189,7 +196,10 @@ struct Dev {
     uint32_t* fring;          // [NCH] free chunk ring
     uint32_t* nal;            // [R] chunks allocated to each bucket
     uint32_t* wbase;          // [P + G3][R] reserved base per (source, bucket): rows < P
-                              // partitions (k_proc), then k_count's received-block split
+                              // partitions (k_proc), then k_count's received-block split;
+                              // relative to the source's shard range in bxoff
+    uint32_t* bdel;           // [XS][R] this step's reservations, per reserving shard
+    uint32_t* bxoff;          // [XS][R] first slot of each shard's reservations (k_plan)
     DueEnt* due;              // [NCH]
     uint32_t* dueb;           // [R] ring slots of the listed non-retained buckets
     // partitions
@@ -536,6 +546,7 @@ __global__ void k_boot(Dev d) {
         d.hs[i] = s;
     }
     if (i < d.NCH) d.fring[i] = i;
+    for (uint32_t j = i; j < XS * d.R; j += gridDim.x * blockDim.x) d.bdel[j] = 0;
     if (i < nb0) d.btab[i] = i;  // bucket 0 is ring slot 0
     if (i < d.R) {
         d.nal[i] = i == 0 ? nb0 : 0;
@@ -1537,11 +1548,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     uint32_t* wb = d.wbase + (size_t)p * R;
+    uint32_t* xd = d.bdel + (size_t)(p % XS) * R;
     for (uint32_t rb = tid; rb < R; rb += K2_T) {
         const uint32_t c = s_bc[rb];
         if (!c) continue;
         const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
-        wb[rb] = atomicAdd(&d.bcnt[rb], c);
+        wb[rb] = atomicAdd(&xd[rb], c);
         atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
     }
     if (stamp && tid == 0) stamp[15] = wait_stamp();
@@ -1674,11 +1686,12 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     }
     __syncthreads();
     uint32_t* wb = d.wbase + (size_t)(d.P + blockIdx.x) * R;
+    uint32_t* xd = d.bdel + (size_t)(blockIdx.x % XS) * R;
     for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) {
         const uint32_t c = s_bc[rb];
         if (!c) continue;
         const uint64_t b = bS + ((rb + R - (uint32_t)(bS % R)) % R);  // absolute bucket of slot rb
-        wb[rb] = atomicAdd(&d.bcnt[rb], c);
+        wb[rb] = atomicAdd(&xd[rb], c);
         atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
     }
 }
@@ -1740,7 +1753,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
             const uint32_t i = threadIdx.x + q * K3_T;
             r[q] = src[i < n ? i : 0];
         }
-        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+        const uint32_t* xo = d.bxoff + (size_t)(blk % XS) * R;
+        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
         __syncthreads();
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
             if (i0) {
@@ -1777,9 +1791,10 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         }
         return;
     }
-    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
-    const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
     const uint32_t g3 = gridDim.x - 1 - d.P, w = blk - d.P;
+    const uint32_t* xo = d.bxoff + (size_t)(w % XS) * R;
+    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
+    const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
     for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
         uint64_t t, k;
@@ -1880,6 +1895,15 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             rm[q] = d.bmin[rb];
         }
     }
+    // this step's shard reservations, loaded unconditionally (clamped) so all
+    // PER * XS loads are in flight together; folded below
+    uint32_t v[PER][XS];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * PL_T < R ? tid + q * PL_T : R - 1;
+#pragma unroll
+        for (uint32_t x = 0; x < XS; ++x) v[q][x] = d.bdel[(size_t)x * R + rb];
+    }
     // the free ring from the head, for the allocation below (nothing writes
     // the ring in this launch before the allocation reads it)
     uint32_t fr0;
@@ -1915,6 +1939,24 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             s_m = m;
             s_j = j;
             s_ovf = ovf;
+        }
+    }
+    // fold: each shard's range starts where the previous one's ends (k_scatter
+    // adds it to the workgroup's own base)
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * PL_T;
+        if (rb < R) {
+            uint32_t base = rc[q];
+#pragma unroll
+            for (uint32_t x = 0; x < XS; ++x) {
+                if (v[q][x]) {
+                    d.bxoff[(size_t)x * R + rb] = base;
+                    d.bdel[(size_t)x * R + rb] = 0;
+                }
+                base += v[q][x];
+            }
+            rc[q] = base;
         }
     }
     uint64_t m = 0, j = 0, ovf = 0;
@@ -2520,6 +2562,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.fring, D.NCH);
     ALLOC(D.nal, D.R);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
+    ALLOC(D.bdel, (size_t)XS * D.R);
+    ALLOC(D.bxoff, (size_t)XS * D.R);
     ALLOC(D.due, D.NCH);
     ALLOC(D.dueb, D.R);
     ALLOC(D.pcnt, P);
