@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SG_ABI_VERSION 3
+#define SG_ABI_VERSION 4
 
 typedef uint64_t sg_simtime;                /* SimulationTime, core/support/definitions.h:18 */
 #define SG_SIMTIME_INVALID UINT64_MAX       /* definitions.h:28 */
@@ -209,6 +209,16 @@ enum sg_window_rule {
     SG_WINDOW_FIXED = 0,      /* every window is [min, min + fixed_jump) */
     SG_WINDOW_DISCOVERED = 1  /* master.c: runahead = truncated min discovered latency */
 };
+/* The event body the device executes per committed event. */
+enum sg_workload {
+    SG_WORKLOAD_PHOLD = 0,    /* test_phold.c: boot sends `load` messages, each receipt sends one */
+    SG_WORKLOAD_GOSSIP = 1    /* configs[4] flooding: message m originates at host
+                                 floor(m*N/M) at gossip_start + m*gossip_interval (a
+                                 self event its boot schedules); a host's first receipt
+                                 of m forwards it to `load` (= fan-out) drawn peers
+                                 through worker_sendPacket, later receipts are dropped
+                                 by a per-host seen set */
+};
 
 typedef struct sg_phold_params {
     uint32_t n_hosts;        /* N, global (all shards) */
@@ -229,6 +239,10 @@ typedef struct sg_phold_params {
     uint64_t exchange_cap;   /* per-peer outbox slots of the step API (multi-shard;
                                 a single shard with exchange_cap != 0 runs the
                                 step API too, one rank of a world-1 job) */
+    uint32_t workload;       /* enum sg_workload */
+    uint32_t gossip_msgs;    /* SG_WORKLOAD_GOSSIP: M messages, 1 <= M <= min(N, 65536) */
+    sg_simtime gossip_start; /* origin time of message 0 */
+    sg_simtime gossip_interval; /* origin spacing */
 } sg_phold_params;
 
 typedef struct sg_phold_tables {        /* host pointers, copied to HBM at create */
@@ -359,6 +373,10 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
  * resources only with its graph.  Errors of the
  * collective are SG_ERR_HIP with the RCCL message in sg_last_error. */
 typedef struct sg_comm sg_comm;
+/* SG_OK when RCCL can be opened in this process (no collective, no GPU work):
+ * every rank probes before the collective sg_comm_create, so a job falls back
+ * to another step loop on all ranks or none. */
+int sg_comm_available(void);
 int sg_comm_unique_id(uint8_t id_out[128]);
 int sg_comm_create(const uint8_t id[128], int rank, int world, int device, sg_comm** out);
 int sg_comm_destroy(sg_comm* c);
@@ -372,10 +390,16 @@ enum sg_kernel_class {
     SG_K_INSERT = 1,   /* k_ins: new / received events into time buckets */
     SG_K_PLAN = 2,     /* k_plan (+ k_fill when sharded) */
     SG_K_GATHER = 3,   /* k_gather: due chunks → host partitions */
-    SG_KCLASSES = 4
+    SG_K_EXCHANGE = 4, /* the step's RCCL all-to-all (sg_engine_run_steps): this shard's
+                          wait for the slowest shard plus the transfer — the barrier
+                          idle time of scheduler.c:380-389 */
+    SG_KCLASSES = 5
 };
 int sg_engine_kernel_times(sg_engine* e, double* ms, uint64_t* launches);
+/* enabled != 0 times every class; sg_engine_set_timing_mask times only the
+ * classes in mask (bit 1 << class): fewer events, less inflation of the rest. */
 int sg_engine_set_timing(sg_engine* e, int enabled);
+int sg_engine_set_timing_mask(sg_engine* e, uint32_t mask);
 
 /* Path packet counters (topology_incrementPathPacketCounter, topology.c:2053-2063,
  * counted where worker_sendPacket calls it: every send that passes the

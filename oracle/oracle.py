@@ -30,7 +30,9 @@ class OrcParams(C.Structure):
                 ("n_hosts", "n_vertices", "load", "dst_rule", "window_rule", "mode",
                  "first_host", "n_local")] + \
                [(n, C.c_uint64) for n in
-                ("end_time", "bootstrap_end", "fixed_jump", "runahead_min", "trace_capacity")]
+                ("end_time", "bootstrap_end", "fixed_jump", "runahead_min", "trace_capacity")] + \
+               [("workload", C.c_uint32), ("gossip_msgs", C.c_uint32),
+                ("gossip_start", C.c_uint64), ("gossip_interval", C.c_uint64)]
 
 
 class OrcStats(C.Structure):
@@ -43,7 +45,8 @@ class OrcStats(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
-EVENT_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("dst", "<u4"), ("src", "<u4")])
+EVENT_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("dst", "<u4"), ("src", "<u4"),
+                        ("msg", "<u4"), ("pad", "<u4")])
 TRACE_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"),
                         ("pos", "<u8")])
 
@@ -165,6 +168,10 @@ class Sim:
         p.fixed_jump = cfg.get("fixed_jump", 0)
         p.runahead_min = cfg.get("runahead_min", 0)
         p.trace_capacity = trace_capacity
+        p.workload = cfg.get("workload", 0)
+        p.gossip_msgs = cfg.get("gossip_msgs", 0)
+        p.gossip_start = cfg.get("gossip_start", 0)
+        p.gossip_interval = cfg.get("gossip_interval", 0)
         self.p = p
         self._keep = [np.ascontiguousarray(cfg[k]) for k in
                       ("host_vertex", "host_rng", "delay_ns", "keep_max", "jump_ms")]

@@ -16,6 +16,8 @@
  *   event ids        core/work/event.c:28-43, host/host.c:397-400
  *   RNG              utility/random.c:32-51 over glibc rand_r (glibc 2.35)
  *   PHOLD            src/test/phold/test_phold.c:160-178, 234-239, 310-312
+ *   gossip           configs[4]'s body (defined here): PHOLD's
+ *                    destination draw and worker_sendPacket per forward
  *   serial policy    scheduler_policy_global_single.c (no bump, one global queue)
  *
  * Per-host independence inside a round (inter-host events are bumped to >= the
@@ -134,6 +136,8 @@ struct orc_sim {
     uint64_t* win;
     size_t n_win, cap_win;
     uint64_t* pcount; /* [V*V] path packet counters (topology.c:2053-2063) */
+    uint32_t* seen;   /* gossip: [n_local][mw] message bitsets */
+    uint32_t mw;
 };
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
@@ -177,6 +181,20 @@ orc_sim* orc_create(const orc_params* p, const uint32_t* host_vertex, const uint
     s->rng_state = (uint32_t*)malloc(L * 4);
     s->pcount = (uint64_t*)calloc(VV, 8);
     if (p->trace_capacity) s->trace = (orc_trace_rec*)malloc(p->trace_capacity * sizeof(orc_trace_rec));
+    if (p->workload == ORC_WORKLOAD_GOSSIP) {
+        if (p->gossip_msgs == 0 || p->gossip_msgs > p->n_hosts || p->gossip_msgs > 65536) {
+            orc_destroy(s);
+            snprintf(orc_err, sizeof orc_err, "orc_create: gossip needs 1 <= messages <= min(hosts, 65536)");
+            return NULL;
+        }
+        s->mw = (p->gossip_msgs + 31) / 32;
+        s->seen = (uint32_t*)calloc(L * s->mw, 4);
+        if (!s->seen) {
+            orc_destroy(s);
+            snprintf(orc_err, sizeof orc_err, "orc_create: out of memory");
+            return NULL;
+        }
+    }
     if (!s->vertex || !s->rng || !s->delay || !s->keep || !s->jump || !s->wthresh || !s->q || !s->ev ||
         !s->pops || !s->digest || !s->rng_state || !s->pcount || (p->trace_capacity && !s->trace)) {
         orc_destroy(s);
@@ -215,6 +233,7 @@ void orc_destroy(orc_sim* s) {
     free(s->trace);
     free(s->win);
     free(s->pcount);
+    free(s->seen);
     free(s);
 }
 
@@ -276,7 +295,7 @@ static int choose_dst(orc_sim* s, uint32_t* rng, uint32_t* dst) {
 }
 
 /* One PHOLD send from host h at time now (worker_sendPacket, worker.c:243-304). */
-static int send_one(orc_sim* s, uint32_t h, uint32_t* rng, uint64_t now, uint64_t* evc) {
+static int send_one(orc_sim* s, uint32_t h, uint32_t* rng, uint64_t now, uint64_t* evc, uint32_t msg) {
     uint32_t d;
     if (!choose_dst(s, rng, &d)) { /* no host chosen: the plugin sends nothing */
         s->st.null_dst++;
@@ -298,7 +317,44 @@ static int send_one(orc_sim* s, uint32_t h, uint32_t* rng, uint64_t now, uint64_
     e.dst = d;
     e.src = h;
     e.seq = (*evc)++; /* event_new_ → host_getNewEventID */
+    e.msg = msg;
+    e.pad = 0;
     return sched_push(s, &e, h);
+}
+
+/* Gossip body (configs[4]).  The reference ships no gossip plugin, so the body
+ * is defined here on the reference's own send path:
+ *   message m in [0, M) originates at host o(m) = floor(m*N/M) at time
+ *   T_m = gossip_start + m*gossip_interval: o(m)'s boot event schedules a self
+ *   event carrying m (worker_scheduleTask, worker.c:218-234: src = dst, no
+ *   path, no draw; scheduler_push's endTime drop applies);
+ *   an event carrying m at host h: if h has seen m, nothing happens (the pop
+ *   still commits); otherwise h marks m seen and forwards it to k = load peers,
+ *   each one destination draw (test_phold.c:160-178) and one worker_sendPacket
+ *   (reliability draw before the drop test, worker.c:267-279). */
+static int execute_gossip(orc_sim* s, const orc_event* e, uint32_t li, int boot) {
+    const uint32_t h = e->dst;
+    if (boot) {
+        const uint64_t N = s->p.n_hosts, M = s->p.gossip_msgs;
+        const uint64_t m = ((uint64_t)h * M + N - 1) / N; /* smallest m with m*N/M >= h */
+        if (m < M && (m * N) / M == h) {
+            orc_event o;
+            o.time = s->p.gossip_start + m * s->p.gossip_interval;
+            o.seq = s->ev[li]++;
+            o.dst = o.src = h;
+            o.msg = (uint32_t)m;
+            o.pad = 0;
+            return sched_push(s, &o, h);
+        }
+        return 0;
+    }
+    uint32_t* w = &s->seen[(size_t)li * s->mw + (e->msg >> 5)];
+    const uint32_t bit = 1u << (e->msg & 31);
+    if (*w & bit) return 0; /* duplicate */
+    *w |= bit;
+    for (uint32_t k = 0; k < s->p.load; k++)
+        if (send_one(s, h, &s->rng_state[li], e->time, &s->ev[li], e->msg)) return -1;
+    return 0;
 }
 
 static int execute(orc_sim* s, const orc_event* e) {
@@ -315,10 +371,11 @@ static int execute(orc_sim* s, const orc_event* e) {
         r->pos = pos;
     }
     int boot = (e->src == h && e->seq == 0);
-    uint32_t nsend = boot ? s->p.load : 1; /* test_phold.c:234-239 / 310-312 */
     if (boot) s->st.boots++;
+    if (s->p.workload == ORC_WORKLOAD_GOSSIP) return execute_gossip(s, e, li, boot);
+    uint32_t nsend = boot ? s->p.load : 1; /* test_phold.c:234-239 / 310-312 */
     for (uint32_t k = 0; k < nsend; k++)
-        if (send_one(s, h, &s->rng_state[li], e->time, &s->ev[li])) return -1;
+        if (send_one(s, h, &s->rng_state[li], e->time, &s->ev[li], 0)) return -1;
     return 0;
 }
 
@@ -328,7 +385,7 @@ int orc_boot(orc_sim* s) {
      * Pushed before the first round, when currentRound.endTime == endTime. */
     s->E = s->p.end_time;
     for (uint32_t i = 0; i < s->p.n_local; i++) {
-        orc_event e = {0, s->ev[i]++, s->p.first_host + i, s->p.first_host + i};
+        orc_event e = {0, s->ev[i]++, s->p.first_host + i, s->p.first_host + i, 0, 0};
         if (sched_push(s, &e, e.src)) return -1;
     }
     s->S = 0; /* slave.c:431 */

@@ -21,9 +21,12 @@ typedef struct orc_event {
     uint64_t seq;   /* srcHostEventID */
     uint32_t dst;   /* destination host index (registration order) */
     uint32_t src;   /* source host index */
+    uint32_t msg;   /* gossip: message id carried by the packet (0 for PHOLD) */
+    uint32_t pad;
 } orc_event;
 
 enum { ORC_MODE_HOST = 0, ORC_MODE_SERIAL = 1 };
+enum { ORC_WORKLOAD_PHOLD = 0, ORC_WORKLOAD_GOSSIP = 1 };
 enum { ORC_DST_UNIFORM_FLOOR = 0, ORC_DST_WEIGHTS = 1 };
 enum { ORC_WINDOW_FIXED = 0, ORC_WINDOW_DISCOVERED = 1 };
 
@@ -32,6 +35,9 @@ typedef struct orc_params {
     uint32_t first_host, n_local; /* shard: hosts [first_host, first_host+n_local) */
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min;
     uint64_t trace_capacity;      /* 0 = no per-pop records */
+    /* gossip workload (configs[4]); see orc.c execute_gossip */
+    uint32_t workload, gossip_msgs;
+    uint64_t gossip_start, gossip_interval;
 } orc_params;
 
 typedef struct orc_stats {

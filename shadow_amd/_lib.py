@@ -17,6 +17,7 @@ SG_OK, SG_ERR_INVAL, SG_ERR_NOMEM, SG_ERR_HIP, SG_ERR_OVERFLOW, SG_ERR_STATE, SG
 SG_ATTACH_MODULO, SG_ATTACH_RANDOM = 0, 1
 SG_DST_UNIFORM_FLOOR, SG_DST_WEIGHTS = 0, 1
 SG_WINDOW_FIXED, SG_WINDOW_DISCOVERED = 0, 1
+SG_WORKLOAD_PHOLD, SG_WORKLOAD_GOSSIP = 0, 1
 ONE_MS = 1_000_000
 SIMTIME_MAX = (1 << 64) - 2
 RAND_MAX = 2147483647
@@ -39,7 +40,15 @@ class PholdParams(C.Structure):
                  "shard_index", "shard_count")] + \
                [(n, C.c_uint64) for n in
                 ("end_time", "bootstrap_end", "fixed_jump", "runahead_min", "trace_capacity",
-                 "exchange_cap")]
+                 "exchange_cap")] + \
+               [("workload", C.c_uint32), ("gossip_msgs", C.c_uint32),
+                ("gossip_start", C.c_uint64), ("gossip_interval", C.c_uint64)]
+
+    def set_workload(self, cfg: dict):
+        self.workload = cfg.get("workload", SG_WORKLOAD_PHOLD)
+        self.gossip_msgs = cfg.get("gossip_msgs", 0)
+        self.gossip_start = cfg.get("gossip_start", 0)
+        self.gossip_interval = cfg.get("gossip_interval", 0)
 
 
 class PholdTables(C.Structure):
@@ -67,7 +76,7 @@ class EngineGeom(C.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
-KERNEL_CLASSES = ("process", "insert", "plan", "gather")  # enum sg_kernel_class
+KERNEL_CLASSES = ("process", "insert", "plan", "gather", "exchange")  # enum sg_kernel_class
 
 
 class WindowState(C.Structure):
@@ -91,7 +100,7 @@ EXPORTS = [
     "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv",
     "sg_engine_enqueue_rounds", "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy",
     "sg_engine_run_steps", "sg_engine_set_graph", "sg_engine_kernel_times",
-    "sg_engine_set_timing", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
+    "sg_engine_set_timing", "sg_engine_set_timing_mask", "sg_comm_available", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
 ]
@@ -146,6 +155,8 @@ def lib():
     L.sg_engine_step_recv.argtypes = [C.c_void_p, C.c_void_p]
     L.sg_engine_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sg_engine_set_timing.argtypes = [C.c_void_p, C.c_int]
+    L.sg_engine_set_timing_mask.argtypes = [C.c_void_p, C.c_uint32]
+    L.sg_comm_available.argtypes = []
     L.sg_engine_geometry.argtypes = [C.c_void_p, C.POINTER(EngineGeom)]
     L.sg_engine_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_path_counters.argtypes = [C.c_void_p, C.c_int]

@@ -166,6 +166,12 @@ struct RoundState {
 
 struct Dev {
     uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
+    // gossip workload (SG_WORKLOAD_GOSSIP): keys carry the message id in their
+    // low msg_shift bits (key = src << 40 | srcHostEventID << msg_shift | msg,
+    // the same event_compare order since (src, srcHostEventID) is unique)
+    uint32_t workload, msg_shift, gossip_msgs, mw;
+    uint64_t gossip_start, gossip_interval;
+    uint32_t* seen;           // [L][mw] per-host message bitsets
     uint32_t R, NCH, HP, hp_shift, P, CAPP, ECAP, G1, G3;
     uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
                                               // events at, dynamic bytes
@@ -177,6 +183,7 @@ struct Dev {
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
     uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
     uint32_t gather_t;        // k_gather workgroup size (256 or 1024)
+    uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
     const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
@@ -547,6 +554,8 @@ __global__ void k_boot(Dev d) {
     }
     if (i < d.NCH) d.fring[i] = i;
     for (uint32_t j = i; j < XS * d.R; j += gridDim.x * blockDim.x) d.bdel[j] = 0;
+    if (d.seen)
+        for (size_t j = i; j < (size_t)d.L * d.mw; j += (size_t)gridDim.x * blockDim.x) d.seen[j] = 0;
     if (i < nb0) d.btab[i] = i;  // bucket 0 is ring slot 0
     if (i < d.R) {
         d.nal[i] = i == 0 ? nb0 : 0;
@@ -839,7 +848,8 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
                                               HostCtx& c, Acc& a, uint64_t bt, uint64_t bk,
                                               ProcShared& sh, Append append, Count count) {
     const uint32_t bsrc = (uint32_t)(bk >> SRC_SHIFT);
-    const uint64_t bseq = bk & SEQ_MASK;
+    const uint64_t bseq = (bk & SEQ_MASK) >> d.msg_shift;
+    const uint32_t msg = (uint32_t)(bk & ((1ULL << d.msg_shift) - 1));
     c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
     if (d.trace) {
         const uint64_t ts = atomicAdd((unsigned long long*)&d.rs->trace_len, 1ULL);
@@ -859,7 +869,40 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
     ++a.ctr[C_POPS];
     const bool boot = (bsrc == c.h && bseq == 0);
     a.ctr[C_BOOTS] += boot;
-    const uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+    uint32_t nsend = boot ? d.load : 1u;  // test_phold.c:234-239 / 310-312
+    if (d.workload == SG_WORKLOAD_GOSSIP) {
+        // configs[4] body (oracle/orc.c execute_gossip): the boot event schedules
+        // the host's origin self event (worker_scheduleTask, worker.c:218-234); a
+        // message's first receipt forwards it to `load` peers, later ones are
+        // dropped by the seen set
+        nsend = 0;
+        const uint32_t lh = c.h - d.lo;
+        if (boot) {
+            const uint64_t N = d.N, M = d.gossip_msgs;
+            const uint64_t m = ((uint64_t)c.h * M + N - 1) / N;
+            if (m < M && (m * N) / M == c.h) {
+                const uint64_t tn = d.gossip_start + m * d.gossip_interval;
+                const uint64_t sq = c.s.evc++;
+                if (sq >> (SRC_SHIFT - d.msg_shift)) a.overflow = true;
+                const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | (sq << d.msg_shift) | m;
+                if (tn >= d.end_time) {
+                    ++a.ctr[C_DROPEND];
+                } else if (tn < E) {
+                    ++a.ctr[C_SAME];
+                    if (!append(tn - S, key)) a.overflow = true;
+                } else if (stage_event(d, S, part, sh, a, c.h, tn, key)) {
+                    count(tn);
+                }
+            }
+        } else {
+            uint32_t* w = d.seen + (size_t)lh * d.mw + (msg >> 5);
+            const uint32_t bit = 1u << (msg & 31), wv = *w;
+            if (!(wv & bit)) {
+                *w = wv | bit;
+                nsend = d.load;
+            }
+        }
+    }
     for (uint32_t m = 0; m < nsend; ++m) {
         const int32_t x = dev_rand_r(c.s.rng);
         HostInfo di;
@@ -879,11 +922,12 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
         if (d.pcount) atomicAdd(&d.pcount[(size_t)c.vh * d.V + di.vertex], 1u);  // worker.c:279
         uint64_t tn = bt + pr.delay;        // worker.c:275-277
         const uint64_t sq = c.s.evc++;      // event.c:38
+        if (sq >> (SRC_SHIFT - d.msg_shift)) a.overflow = true;
         if (tn >= d.end_time) {             // scheduler.c:343-346
             ++a.ctr[C_DROPEND];
             continue;
         }
-        const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | sq;
+        const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | (sq << d.msg_shift) | msg;
         if (dst == c.h && tn < E) {
             ++a.ctr[C_SAME];
             if (!append(tn - S, key)) a.overflow = true;
@@ -1295,7 +1339,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     if (st0) stamp[8] = wait_stamp();
                     sort_segment(seg, cnt);  // pop order
                     if (st0) stamp[9] = wait_stamp();
-                    if (S + (seg[0].a & M52) + self_delay < E) {
+                    if (d.workload != SG_WORKLOAD_PHOLD || S + (seg[0].a & M52) + self_delay < E) {
                         // sequential body: a self event may land inside this window
                         uint32_t nx = 0;
                         auto append = [&](uint64_t trel, uint64_t key) -> bool {
@@ -1911,6 +1955,17 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         const uint64_t h0 = rs->fl_head;
         fr0 = d.fring[(h0 + tid) % NCH];  // NCH may be below PL_T (small engines)
     }
+    if (mode == 1 && d.check) {
+        // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in this
+        // shard's headers, from device-scope atomics it read without a fence,
+        // must equal the same terms re-derived here from the workgroups' plain
+        // partials (visible after the kernel boundary); the own block comes back
+        // in recv.  On a drain step fill_blocks wrote them from the partials.
+        uint64_t lm, lj;
+        reduce_local(d, s16, lm, lj);  // barriers inside
+        const int64_t* own = recv + (size_t)d.g * d.xrows * 3;
+        if (tid == 0 && ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj)) flag(d, OV_BUG);
+    }
     if (tid == 0) {
         s_head = rs->fl_head;
         s_tail = rs->fl_tail;
@@ -2213,6 +2268,7 @@ struct sg_engine {
     RoundState* h_rs;  // pinned
     unsigned long long* d_pend;
     bool timing;
+    uint32_t timing_mask;  // kernel classes timed while timing is on
     bool debug_sync;  // SG_DEBUG_SYNC=1: synchronise after every launch, name the faulting class
     struct Pair { hipEvent_t a, b; int cls; };
     std::vector<Pair> pending_ev;
@@ -2272,7 +2328,8 @@ static hipEvent_t get_event(sg_engine* e) {
 template <typename F>
 static int timed_launch(sg_engine* e, int cls, F&& launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (e->timing) {
+    const bool timed = e->timing && (e->timing_mask >> cls & 1u);
+    if (timed) {
         a = get_event(e);
         b = get_event(e);
         if (a && b) HIPCHK(hipEventRecord(a, e->stream));
@@ -2282,13 +2339,13 @@ static int timed_launch(sg_engine* e, int cls, F&& launch) {
     if (e->debug_sync) {
         const hipError_t err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) {
-            static const char* names[SG_KCLASSES] = {"process", "insert", "plan", "gather"};
+            static const char* names[SG_KCLASSES] = {"process", "insert", "plan", "gather", "exchange"};
             sg_set_error("kernel class %s (launch %llu) failed: %s", names[cls],
                          (unsigned long long)e->launches[cls], hipGetErrorString(err));
             return SG_ERR_HIP;
         }
     }
-    if (e->timing && a && b) {
+    if (timed && a && b) {
         HIPCHK(hipEventRecord(b, e->stream));
         e->pending_ev.push_back({a, b, cls});
     }
@@ -2340,8 +2397,13 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     if (p.n_hosts == 0 || p.n_hosts > (1u << (64 - SRC_SHIFT)) || p.n_vertices == 0 || p.n_vertices > 0xFFFFu || G > MAXG ||
         p.shard_index >= G || G > p.n_hosts || !t->host_vertex || !t->host_rng || !t->delay_ns ||
         !t->keep_max || !t->jump_ms || (p.dst_rule == SG_DST_WEIGHTS && !t->weight_thresh) ||
-        p.dst_rule > 1 || p.window_rule > 1 || p.load == 0) {
+        p.dst_rule > 1 || p.window_rule > 1 || p.load == 0 || p.workload > SG_WORKLOAD_GOSSIP) {
         sg_set_error("sg_engine_create: invalid parameters (n_hosts must be in [1, 2^24], n_vertices in [1, 65535])");
+        return SG_ERR_INVAL;
+    }
+    if (p.workload == SG_WORKLOAD_GOSSIP &&
+        (p.gossip_msgs == 0 || p.gossip_msgs > p.n_hosts || p.gossip_msgs > 65536)) {
+        sg_set_error("sg_engine_create: gossip needs 1 <= gossip_msgs <= min(n_hosts, 65536)");
         return SG_ERR_INVAL;
     }
     int ndev = 0;
@@ -2371,6 +2433,14 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         return SG_ERR_INVAL;
     }
     d.load = p.load;
+    d.workload = p.workload;
+    if (p.workload == SG_WORKLOAD_GOSSIP) {
+        d.msg_shift = 16;  // srcHostEventID keeps 24 bits: 16M sends per host
+        d.gossip_msgs = p.gossip_msgs;
+        d.mw = (p.gossip_msgs + 31) / 32;
+        d.gossip_start = p.gossip_start;
+        d.gossip_interval = p.gossip_interval;
+    }
     d.dst_rule = p.dst_rule;
     d.window_rule = p.window_rule;
     d.end_time = p.end_time;
@@ -2398,7 +2468,11 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         max_jump = std::max<uint64_t>(std::max<uint64_t>(10 * SG_ONE_MS, p.runahead_min),
                                       max_jump_ms * SG_ONE_MS);
     }
-    const uint64_t span = max_jump + max_delay + 2;
+    uint64_t span = max_jump + max_delay + 2;
+    if (p.workload == SG_WORKLOAD_GOSSIP) {  // origin self events are scheduled at boot
+        const uint64_t last = p.gossip_start + (uint64_t)(p.gossip_msgs - 1) * p.gossip_interval;
+        span = std::max<uint64_t>(span, std::min<uint64_t>(last, p.end_time) + 2);
+    }
     if (span >= (1ULL << 39)) {
         sg_set_error("sg_engine_create: window + delay span %llu ns exceeds 2^39 ns",
                      (unsigned long long)span);
@@ -2412,7 +2486,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.W = W;
     d.R = (uint32_t)(span / W + 3);
     d.G3 = env_u32("SG_INS_GRID", 128);
-    const uint64_t qc = p.queue_cap ? p.queue_cap : 64;
+    // default event slots per host: PHOLD keeps `load` events per host in flight;
+    // gossip floods keep about ten fan-outs' worth (configs[4]: 82 per host at peak)
+    const uint64_t qc = p.queue_cap ? p.queue_cap
+                                    : p.workload == SG_WORKLOAD_GOSSIP ? std::max<uint64_t>(64, 24ull * p.load) : 64;
     const uint64_t base_ch = ((uint64_t)d.L * qc + CH - 1) / CH;
     // every live bucket may hold one partly filled chunk
     const uint64_t nch = base_ch + d.R + 64;
@@ -2424,6 +2501,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
     d.gather_t = env_u32("SG_GATHER_T", 1024) == 1024 ? 1024 : K1_T;
+    d.check = env_u32("SG_CHECK", 0) != 0;
     // host partitions: HP hosts per k_proc workgroup (power of two), about
     // one partition per CU
     const uint32_t hp_env = env_u32("SG_HP", 0);
@@ -2554,6 +2632,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.pairs = pairs;
     D.vself = vself;
     ALLOC(D.hs, L);
+    if (D.workload == SG_WORKLOAD_GOSSIP) ALLOC(D.seen, L * D.mw);
     ALLOC(D.pool, (size_t)D.NCH * CH);
     ALLOC(D.btab, (size_t)D.R * D.NCH);
     ALLOC(D.bcnt, D.R);
@@ -3066,8 +3145,17 @@ int sg_engine_path_counts(sg_engine* e, uint64_t* out, uint64_t capacity, uint64
 }
 
 int sg_engine_set_timing(sg_engine* e, int enabled) {
+    return sg_engine_set_timing_mask(e, enabled ? (1u << SG_KCLASSES) - 1 : 0u);
+}
+
+int sg_engine_set_timing_mask(sg_engine* e, uint32_t mask) {
     if (!e) return SG_ERR_INVAL;
-    e->timing = enabled != 0;
+    if (e->timing) {  // events of the previous setting are harvested first
+        const int rc = sg_engine_sync(e);
+        if (rc) return rc;
+    }
+    e->timing = mask != 0;
+    e->timing_mask = mask;
     for (int i = 0; i < SG_KCLASSES; ++i) {
         e->ms[i] = 0;
         e->launches[i] = 0;
@@ -3142,6 +3230,8 @@ struct sg_comm {
 
 extern "C" {
 
+int sg_comm_available(void) { return rccl_open(); }
+
 int sg_comm_unique_id(uint8_t id_out[128]) {
     if (!id_out) return SG_ERR_INVAL;
     int rc = rccl_open();
@@ -3205,7 +3295,10 @@ int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, 
     auto step = [&]() -> int {
         int r = sg_engine_step_send(e, send);
         if (r) return r;
-        RCCLCHK(g_rccl.allToAll(send, recv, per_peer, ncclInt64, c->comm, e->stream));
+        ncclResult_t nr = ncclSuccess;
+        r = timed_launch(e, SG_K_EXCHANGE, [&] { nr = g_rccl.allToAll(send, recv, per_peer, ncclInt64, c->comm, e->stream); });
+        if (r) return r;
+        RCCLCHK(nr);
         return sg_engine_step_recv(e, recv);
     };
     const uint32_t b = e->graph_batch ? e->graph_batch : 32;

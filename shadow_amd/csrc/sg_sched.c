@@ -174,8 +174,8 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
                        sg_sched_result* res, uint64_t* digest, uint64_t* pops, uint32_t* rng,
                        uint64_t* event_counter) {
     if (!P || !T || !ops || n_workers == 0 || P->n_hosts == 0 ||
-        (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh)) {
-        sg_set_error("sg_sched_run_phold: bad arguments");
+        (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh) || P->workload != SG_WORKLOAD_PHOLD) {
+        sg_set_error("sg_sched_run_phold: bad arguments (the CPU-worker driver runs the PHOLD body only)");
         return SG_ERR_INVAL;
     }
     drv D;

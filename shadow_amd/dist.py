@@ -71,11 +71,28 @@ class EngineShard:
         self.send = torch.zeros((self.world, rows, 3), dtype=torch.int64, device=self.dev)
         self.recv = torch.zeros_like(self.send)
 
+    def _all_ok(self, ok: bool) -> bool:
+        """Every rank's flag, AND-reduced over the default group."""
+        t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        if _backend() == "nccl":
+            t = t.to(self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(int(t.item()))
+
     def enable_native(self, graph_batch: int = 0):
         """Issue whole steps from C (sg_engine_run_steps) over a communicator of
         libshadowgpu's own, made from a unique id rank 0 broadcasts over the
-        default process group; graph_batch > 0 replays captured hipGraphs."""
+        default process group; graph_batch > 0 replays captured hipGraphs.
+
+        Every decision is collective, so all ranks take the native loop or none:
+        each rank probes RCCL first (no collective), the flags are AND-reduced,
+        rank 0's id is broadcast with its own flag, and after the collective
+        ncclCommInitRank a second AND-reduce confirms every rank got a
+        communicator (a rank that did not releases nothing, the others close
+        theirs).  Raises on every rank when the native loop is unavailable."""
         from .engine import Comm
+        if not self._all_ok(Comm.available()):
+            raise RuntimeError("RCCL cannot be opened on every rank")
         uid = torch.zeros(129, dtype=torch.uint8)  # [0]: rank 0 made an id; [1:]: the id
         if self.rank == 0:
             try:
@@ -92,7 +109,16 @@ class EngineShard:
         if not int(uid[0]):
             raise RuntimeError("rank 0 could not create an RCCL unique id")
         uid = uid[1:]
-        self.comm = Comm(bytes(uid.tolist()), self.rank, self.world, self.dev.index)
+        comm, err = None, None
+        try:
+            comm = Comm(bytes(uid.tolist()), self.rank, self.world, self.dev.index)
+        except Exception as exc:  # noqa: BLE001 — reported after the agreement below
+            err = exc
+        if not self._all_ok(comm is not None):
+            if comm is not None:
+                comm.close()
+            raise RuntimeError(f"RCCL communicator creation failed on some rank ({err})")
+        self.comm = comm
         self.eng.set_graph(graph_batch)
 
     def close_native(self):
@@ -131,6 +157,12 @@ class EngineShard:
 
     def done(self) -> bool:
         return bool(self.eng.stats()["done"])
+
+    def fingerprint(self) -> int:
+        """This shard's term of the host-state fingerprint (sums to the unsharded one)."""
+        from .trace import state_fingerprint
+        hs = self.eng.host_state()
+        return state_fingerprint(self.eng.first_host, hs["digest"], hs["pops"], hs["rng"], hs["ev"])
 
     def stats(self):
         return self.eng.stats()
@@ -207,11 +239,20 @@ def _env_rank():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def _gather_rows(vals, dev):
+    """All ranks' float rows, to every rank (list of lists)."""
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
 def bench(args):
     """bench.py --gpus N under torch.distributed.run: the 1M-host PHOLD over N
     GPUs (strong scaling: the host count stays 1M).  Returns the JSON dict on
     rank 0, None elsewhere."""
     from . import phold
+    from ._lib import KERNEL_CLASSES
     rank, world, local = _env_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with "
@@ -227,11 +268,12 @@ def bench(args):
     if args.dist_backend == "nccl" and not args.py_steps:
         try:
             shard.enable_native(args.graph)
-        except Exception as exc:  # same on every rank (e.g. no RCCL symbols): Python steps
+        except Exception as exc:  # the same on every rank (enable_native decides collectively)
             import sys
             print(f"native step loop unavailable ({exc}); driving steps from Python",
                   file=sys.stderr, flush=True)
             shard.comm = None
+    native = shard.comm is not None
     shard.boot()
     # warmup: the boot round (its outbox drains over several steps), then size
     # the exchange blocks from the steady-state per-peer peak, the same on every rank
@@ -257,21 +299,40 @@ def bench(args):
     s1 = shard.stats()
     t = torch.tensor([dt], dtype=torch.float64, device=shard.dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    fp = shard.fingerprint()  # this shard's term of the end-of-region state fingerprint
     tot = torch.tensor([s1["pops"] - s0["pops"], s1["rounds"] - s0["rounds"],
-                        s1["exchange_steps"] - s0["exchange_steps"], s1["overflow"]],
+                        s1["exchange_steps"] - s0["exchange_steps"], s1["overflow"],
+                        int(s1["done"]), fp - (1 << 64 if fp >= 1 << 63 else 0)],
                        dtype=torch.int64, device=shard.dev)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     tmax = float(t.item())
-    total, rounds_sum, steps_sum, ovf = (int(x) for x in tot.tolist())
+    total, rounds_sum, steps_sum, ovf, done_sum, fp = (int(x) for x in tot.tolist())
+    fp &= (1 << 64) - 1
+    end_round = s1["rounds"]
+    # per-rank kernel times over the next steps (HIP events on the engine stream;
+    # the exchange class is this rank's RCCL all-to-all: its wait for the slowest
+    # rank plus the transfer, the barrier idle time of scheduler.c:380-389)
+    kr = max(1, min(args.steps, args.kernel_rounds))
+    if native:
+        shard.eng.set_timing(True)
+        run(shard, world, kr, check_every=1 << 30)
+        kt = shard.eng.kernel_times()
+        shard.eng.set_timing(False)
+        rows = _gather_rows([kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES], shard.dev)
+    else:
+        rows = None
     shard.close_native()
     dist.destroy_process_group()
     global _BACKEND
     _BACKEND = None
     if ovf:
         raise SystemExit(f"queue/outbox overflow during bench ({ovf:#x})")
+    if rounds_sum == 0 or done_sum:
+        raise SystemExit(f"simulation ended early: {rounds_sum // world} rounds timed, done on "
+                         f"{done_sum} of {world} ranks")
     if rank != 0:
         return None
-    return {
+    res = {
         "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
         "value": total / tmax,
         "unit": "events/s",
@@ -293,6 +354,15 @@ def bench(args):
                    "parallelism": f"hosts block-sharded {world} ways, one "
                                   f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
                                   "all-to-all per step",
-                   "step_loop": "python" if getattr(shard, "comm", None) is None else
-                                f"native (sg_engine_run_steps, hipGraph batch {args.graph})"},
+                   "step_loop": f"native (sg_engine_run_steps, hipGraph batch {args.graph})" if native
+                                else "python"},
+        # bench.py checks these against the oracle fixture and drops them
+        "_end_round": end_round, "_fingerprint": fp,
     }
+    if rows is not None:
+        res["per_rank_us_per_step"] = {
+            "classes": list(KERNEL_CLASSES), "steps": kr, "rows": rows,
+            "note": "HIP events around every launch on each rank's engine stream (they inflate "
+                    "each kernel by a few us); 'exchange' is the RCCL all-to-all: wait for the "
+                    "slowest rank + transfer (barrier idle, scheduler.c:380-389)"}
+    return res

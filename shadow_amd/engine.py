@@ -34,6 +34,7 @@ class Engine:
         p.runahead_min = cfg.get("runahead_min", 0)
         p.trace_capacity = trace_capacity
         p.exchange_cap = exchange_cap
+        p.set_workload(cfg)
         self.params = p
         self._arrays = [np.ascontiguousarray(cfg["host_vertex"], np.uint32),
                         np.ascontiguousarray(cfg["host_rng"], np.uint32),
@@ -123,6 +124,19 @@ class Engine:
         """Count kept sends per (src vertex, dst vertex) from now on (zeroed)."""
         L.check(L.lib().sg_engine_path_counters(self.h, int(enable)))
 
+    def object_counts(self) -> dict:
+        """Event objects created and freed so far (object_counter.c:90-230 for
+        the Event type): created = boot events + every event a send or a
+        schedule made (staged, same-round or dropped at endTime); freed = every
+        executed pop + every endTime drop (scheduler.c:343-346).  The
+        difference is the events still queued."""
+        a, e = C.c_uint64(), C.c_uint64()
+        L.check(L.lib().sg_engine_active_hosts(self.h, C.byref(a), C.byref(e)))
+        st = self.stats()
+        new = st["boots"] + e.value + st["same_round"] + st["drop_endtime"]
+        return {"event_new": new, "event_free": st["pops"] + st["drop_endtime"],
+                "event_live": st["pending"]}
+
     def path_counts(self) -> np.ndarray:
         n = C.c_uint64()
         L.check(L.lib().sg_engine_path_counts(self.h, None, 0, C.byref(n)))
@@ -131,8 +145,14 @@ class Engine:
             L.check(L.lib().sg_engine_path_counts(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out
 
-    def set_timing(self, on: bool):
-        L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
+    def set_timing(self, on: bool, classes=None):
+        """Per-kernel HIP-event timing: every class, or only `classes` (names of
+        _lib.KERNEL_CLASSES) — fewer events inflate the timed kernels less."""
+        if classes is None:
+            L.check(L.lib().sg_engine_set_timing(self.h, int(on)))
+        else:
+            mask = sum(1 << L.KERNEL_CLASSES.index(c) for c in classes) if on else 0
+            L.check(L.lib().sg_engine_set_timing_mask(self.h, mask))
 
     def kernel_times(self):
         """{class: (total ms, launches)} since set_timing(True), per sg_kernel_class."""
@@ -185,6 +205,11 @@ class Engine:
 class Comm:
     """An RCCL communicator owned by libshadowgpu (sg_comm_create): rank 0 makes
     the 128-byte unique id, the caller broadcasts it."""
+
+    @staticmethod
+    def available() -> bool:
+        """RCCL can be opened in this process (no collective is made)."""
+        return L.lib().sg_comm_available() == L.SG_OK
 
     @staticmethod
     def unique_id() -> bytes:

@@ -137,16 +137,39 @@ def c4_config(n_hosts=1_000_000, V=1024, end_time_s=10.0, load=16, seed_topology
                        end_time_s=end_time_s, runahead_ms=1, name=f"phold-c4-{n_hosts}")
 
 
-def c5_config(n_hosts=100_000, V=256, end_time_s=10.0, load=8, loss=(0.005, 0.05),
-              seed_topology=5):
-    """BASELINE configs[4] shape: 100k hosts on lossy links (edge loss uniform in
-    [0.005, 0.05]); every send draws the host's reliability chance."""
+def _lossy_mesh(V, seed_topology, loss):
     lat, _ = lognormal_topology(V, seed_topology, median_ms=40.0, sigma=0.7, min_ms=2.0)
     rs = np.random.default_rng(seed_topology)  # input generation only
     el = rs.uniform(loss[0], loss[1], size=(V, V))
     el = np.triu(el) + np.triu(el, 1).T
-    return make_config(n_hosts=n_hosts, latency_ms=lat, edge_loss=el.ravel(), load=load,
-                       end_time_s=end_time_s, name=f"lossy-c5-{n_hosts}")
+    return lat, el.ravel()
+
+
+def lossy_config(n_hosts=100_000, V=256, end_time_s=10.0, load=8, loss=(0.005, 0.05),
+                 seed_topology=5):
+    """PHOLD on configs[4]'s lossy links (edge loss uniform in [0.005, 0.05]);
+    every send draws the host's reliability chance."""
+    lat, el = _lossy_mesh(V, seed_topology, loss)
+    return make_config(n_hosts=n_hosts, latency_ms=lat, edge_loss=el, load=load,
+                       end_time_s=end_time_s, name=f"lossy-phold-{n_hosts}")
+
+
+def c5_config(n_hosts=100_000, V=256, fanout=8, msgs=64, start_ms=1.0, interval_ms=5.0,
+              end_time_s=10.0, loss=(0.005, 0.05), seed_topology=5, seed=1):
+    """BASELINE configs[4]: Bitcoin-style gossip over lossy links.  Message m of
+    `msgs` originates at host floor(m*N/msgs) at start + m*interval; a host's
+    first receipt of a message forwards it to `fanout` drawn peers (each send
+    through worker_sendPacket: reliability draw, then the drop test,
+    worker.c:267-279); later receipts are dropped by the host's seen set.
+    Links: log-normal latency (median 40 ms, min 2 ms) over V vertices, edge
+    loss uniform in [0.005, 0.05]."""
+    lat, el = _lossy_mesh(V, seed_topology, loss)
+    cfg = make_config(n_hosts=n_hosts, latency_ms=lat, edge_loss=el, load=fanout, seed=seed,
+                      end_time_s=end_time_s, name=f"gossip-c5-{n_hosts}")
+    cfg.update(workload=L.SG_WORKLOAD_GOSSIP, gossip_msgs=msgs,
+               gossip_start=int(round(start_ms * L.ONE_MS)),
+               gossip_interval=int(round(interval_ms * L.ONE_MS)))
+    return cfg
 
 
 def topology_config(graph, n_hosts, *, load=16, seed=1, end_time_s=10.0, hints=None,
@@ -173,6 +196,17 @@ def topology_config(graph, n_hosts, *, load=16, seed=1, end_time_s=10.0, hints=N
         bootstrap_end=int(bootstrap_end), fixed_jump=int(fixed_jump_ms * L.ONE_MS),
         runahead_min=int(runahead_ms * L.ONE_MS), host_vertex=vertex, host_rng=rng,
         delay_ns=delay, keep_max=keep, jump_ms=jump, weight_thresh=wt)
+
+
+def c1_config(end_time_s=3600.0, load=16, seed=1):
+    """BASELINE configs[0] shape without tgen (the plugin is not available
+    offline): the example config's two hosts ("server", "client") on its
+    embedded one-vertex topology (50 ms self-loop, loss 0.01), stoptime 3600 s,
+    PHOLD traffic between them."""
+    from . import topology as T
+    g = T.Graph.from_file(T.C1_EMBEDDED)
+    return topology_config(g, 2, load=load, seed=seed, end_time_s=end_time_s,
+                           name="c1-example-2")
 
 
 def c3_config(n_relays=2000, n_clients=8000, end_time_s=10.0, load=4, seed=1):

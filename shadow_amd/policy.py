@@ -83,6 +83,7 @@ def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 
     p.bootstrap_end = cfg.get("bootstrap_end", 0)
     p.fixed_jump = cfg.get("fixed_jump", 0)
     p.runahead_min = cfg.get("runahead_min", 0)
+    p.set_workload(cfg)
     arrs = [np.ascontiguousarray(cfg["host_vertex"], np.uint32),
             np.ascontiguousarray(cfg["host_rng"], np.uint32),
             np.ascontiguousarray(cfg["delay_ns"], np.uint64),

@@ -169,5 +169,9 @@ def path_tables(latency_ms, reliability, discovered_ms=None):
     return d, k, j
 
 
-GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
-BUNDLED = os.path.join(GOLDEN, "topology.graphml.xml.xz")
+# the reference's bundled topology (resource/topology.graphml.xml.xz, data file
+# copied byte for byte): workload input for the configs on it
+BUNDLED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "topology.graphml.xml.xz")
+# the one-vertex topology embedded in configs[0]'s example config
+# (resource/examples/shadow.config.xml:2-23: 50 ms self-loop, packet loss 0.01)
+C1_EMBEDDED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "c1_topology.graphml")

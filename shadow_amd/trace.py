@@ -31,6 +31,31 @@ from ._lib import TRACE_DTYPE
 HEADER = "# shadow-amd pop trace v1: host pos time_ns src_host src_event_id"
 
 
+def _fmix64(z: np.ndarray) -> np.ndarray:
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xFF51AFD7ED558CCD)
+    z = z ^ (z >> np.uint64(33))
+    z = z * np.uint64(0xC4CEB9FE1A85EC53)
+    return z ^ (z >> np.uint64(33))
+
+
+def state_fingerprint(first_host: int, digest, pops, rng, ev) -> int:
+    """Order-independent 64-bit fingerprint of per-host end state (trace digest,
+    pop count, rand_r state, srcHostEventID counter) — a checksum of checksums.
+    Additive over hosts (mod 2^64), so shards' fingerprints sum to the
+    unsharded one; position-sensitive through the host index."""
+    n = len(digest)
+    if n == 0:
+        return 0
+    with np.errstate(over="ignore"):
+        h = np.arange(first_host, first_host + n, dtype=np.uint64)
+        z = _fmix64(np.asarray(digest, np.uint64) + (h + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15))
+        z = _fmix64(z ^ np.asarray(pops, np.uint64))
+        z = _fmix64(z ^ np.asarray(rng, np.uint64))
+        z = _fmix64(z ^ np.asarray(ev, np.uint64))
+        return int(z.sum(dtype=np.uint64))
+
+
 def canonical(trace: np.ndarray) -> np.ndarray:
     """Hosts in index order, each host's pops in pop order."""
     t = np.asarray(trace)

@@ -26,6 +26,8 @@ class OracleShard:
         self.world = world
         self.rank = rank
         self.sim = O.Sim(cfg, first_host=b[rank], n_local=b[rank + 1] - b[rank])
+        # the engine's key layout: src << 40 | srcHostEventID << msg_shift | msg
+        self.msg_shift = np.uint64(16 if cfg.get("workload", 0) == 1 else 0)
         self.xcap = exchange_cap
         self.rows = HDR + exchange_cap
         self.recv = torch.zeros((world, self.rows, 3), dtype=torch.int64)
@@ -54,7 +56,8 @@ class OracleShard:
                 ev = out[owner == p] if p != self.rank else out[:0]
                 self.outq[p] = np.stack([ev["time"].astype(np.int64),
                                          ((ev["src"].astype(np.uint64) << np.uint64(40)) |
-                                          ev["seq"].astype(np.uint64)).astype(np.int64),
+                                          (ev["seq"].astype(np.uint64) << self.msg_shift) |
+                                          ev["msg"].astype(np.uint64)).astype(np.int64),
                                          ev["dst"].astype(np.int64)], 1) if len(ev) else \
                     np.zeros((0, 3), np.int64)
             self.sent = [0] * self.world
@@ -90,7 +93,9 @@ class OracleShard:
             tri = r[p, HDR:HDR + n].astype(np.uint64)
             ev = np.zeros(n, O.EVENT_DTYPE)
             ev["time"] = tri[:, 0]
-            ev["seq"] = tri[:, 1] & np.uint64((1 << 40) - 1)
+            low = tri[:, 1] & np.uint64((1 << 40) - 1)
+            ev["seq"] = low >> self.msg_shift
+            ev["msg"] = low & ((np.uint64(1) << self.msg_shift) - np.uint64(1))
             ev["src"] = (tri[:, 1] >> np.uint64(40)).astype(np.uint32)
             ev["dst"] = tri[:, 2].astype(np.uint32)
             self.sim.ingest(ev)

@@ -1,4 +1,4 @@
-"""CPU, world size 2 and 3 over gloo: the distributed step protocol of
+"""CPU, world size 2, 3, 4 and 8 over gloo (PHOLD and the gossip body): the distributed step protocol of
 shadow_amd.dist (one all-to-all of fixed-size blocks per step, the window from
 the block headers, drain steps when an outbox exceeds the block) reproduces
 the unsharded simulation exactly (per-host digests, pops, RNG states, event
@@ -53,12 +53,14 @@ def _run(cfg, world, xcap):
 
 
 @pytest.mark.parametrize("world,kind,xcap", [(2, "tiny", 64), (3, "lossy", 16), (2, "probe10", 4096),
-                                             (2, "tiny", 3)])
+                                             (2, "tiny", 3), (8, "tiny", 8), (4, "gossip", 16),
+                                             (8, "gossip", 64)])
 def test_sharded_protocol_matches_unsharded(world, kind, xcap):
     from oracle import oracle as O
     cfg = {"tiny": lambda: phold.tiny_config(n_hosts=200, V=6, load=4, end_time_s=0.4),
            "lossy": lambda: phold.tiny_config(n_hosts=151, V=5, load=3, loss=0.3, end_time_s=0.3),
-           "probe10": lambda: phold.probe_config(n_hosts=120, jump_ms=10, end_time_s=0.3)}[kind]()
+           "probe10": lambda: phold.probe_config(n_hosts=120, jump_ms=10, end_time_s=0.3),
+           "gossip": lambda: phold.c5_config(n_hosts=400, V=6, msgs=12, fanout=4, end_time_s=1.0)}[kind]()
     res = _run(cfg, world, xcap)
     ref = O.Sim(cfg)
     ref.boot()

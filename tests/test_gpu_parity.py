@@ -106,8 +106,8 @@ def test_c4_shape_prefix_parity():
     _assert_same(eng, orc)
 
 
-def test_lossy_c5_shape_prefix_parity():
-    cfg = phold.c5_config(n_hosts=20_000)
+def test_lossy_phold_prefix_parity():
+    cfg = phold.lossy_config(n_hosts=20_000)
     eng, orc = _run_both(cfg, max_rounds=60)
     gs = _assert_same(eng, orc)
     assert gs["drop_reliability"] > 0

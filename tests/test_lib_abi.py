@@ -36,7 +36,9 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert L.lib().sg_abi_version() == 3
+    import re
+    hdr = open(os.path.join(ROOT, "include", "shadowgpu.h")).read()
+    assert L.lib().sg_abi_version() == int(re.search(r"SG_ABI_VERSION (\d+)", hdr).group(1))
 
 
 def test_engine_without_gpu_fails_loudly():

@@ -66,7 +66,7 @@ def test_known_delay_values():
 
 
 def test_c1_embedded_topology():
-    g = T.Graph(open(os.path.join(GOLDEN, "c1_topology.graphml")).read())
+    g = T.Graph.from_file(T.C1_EMBEDDED)
     assert (g.n_vertices, g.n_edges, g.complete) == (1, 1, True)
     lat, rel, disc, kind = g.paths()
     assert lat[0] == 50.0 and rel[0] == 1.0 * (1.0 - 0.0) * (1.0 - 0.0) * (1.0 - 0.01)

@@ -26,9 +26,13 @@ for r in range(3):
         v = ph[:, i]
         print(f"   {nm:<12} median {np.median(v):6.2f} us  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
     print("   due/active/sends per WG median", np.median(st[:, 5:8], axis=0), "max", st[:, 5:8].max(axis=0))
-    a = np.diff(st[:, [1, 8, 9, 10, 11, 12]], axis=1) / 100
+    a = np.diff(st[:, [1, 8, 9, 10, 11]], axis=1) / 100
+    # stamp 12 is written only when that lane's first host recorded its sends
+    # (phase B/C path); a light host commits inline and leaves it unset
+    rec = st[:, 12] >= st[:, 11]
+    r_s = "%.2f" % np.median((st[rec, 12] - st[rec, 11]) / 100) if rec.any() else "n/a"
     print("   phase A, lane 0 of wave 0, first host (median us): state loads %.2f  sort %.2f  count draws %.2f  "
-          "reserve %.2f  record+store %.2f" % tuple(np.median(a, axis=0)))
+          "reserve %.2f" % tuple(np.median(a, axis=0)) + f"  record+store {r_s} ({int(rec.sum())} WGs)")
     t = np.diff(st[:, [3, 13, 14, 15, 4]], axis=1) / 100
     print("   after phase B (median us): phase C %.2f  partials %.2f  reservations %.2f  tail %.2f"
           % tuple(np.median(t, axis=0)))
