@@ -161,24 +161,20 @@ def run_single(args):
     hs = eng.host_state()  # the state at the end of the timed region, for the parity check
     fp = state_fingerprint(0, hs["digest"], hs["pops"], hs["rng"], hs["ev"])
     del hs
-    # k_proc's launch duration: the next rounds of the same run with HIP events
-    # around k_proc only, on the engine stream (events add a gap before and
-    # after the kernel they bracket, so they stay out of the headline region)
+    # kernel durations: the next rounds of the same run, every launch carrying
+    # HIP events as its dispatch packet's start / stop timestamps
+    # (hipExtLaunchKernelGGL) on the engine stream — kept out of the headline
+    # region all the same
     a1, _ = eng.active_hosts()
     kr = max(1, min(args.steps, args.kernel_rounds))
-    eng.set_timing(True, classes=["process"])
-    eng.run(kr, batch=args.batch)
-    proc_ms, proc_n = eng.kernel_times()["process"]
-    eng.set_timing(False)
-    s2 = eng.stats()
-    a2, _ = eng.active_hosts()
-    kpops = s2["pops"] - s1["pops"]
-    # every kernel class, events around every launch (each class inflated by
-    # its events; the sum exceeds ms_per_step by the event overhead)
     eng.set_timing(True)
     eng.run(kr, batch=args.batch)
     kt = eng.kernel_times()
     eng.set_timing(False)
+    proc_ms, proc_n = kt["process"]
+    s2 = eng.stats()
+    a2, _ = eng.active_hosts()
+    kpops = s2["pops"] - s1["pops"]
     alg_bytes = ALG_BYTES_PER_EVENT * kpops + ALG_BYTES_PER_ACTIVE_HOST * (a2 - a1)
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
@@ -211,12 +207,10 @@ def run_single(args):
                      "kernel": DOMINANT, "avg_launch_us": avg_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "timing_rounds": kr,
-                     "event_timed_us_per_round": {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]},
-                     "event_timed_note": "k_proc alone is bracketed by events for avg_launch_us; "
-                                         "event_timed_us_per_round brackets every launch, so each "
-                                         "class carries its events' overhead and the sum exceeds "
-                                         "ms_per_step; rocprofv3 kernel-trace durations are in "
-                                         "profiles/ (see DESIGN.md section 5)"},
+                     "kernel_us_per_round": {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]},
+                     "timing_method": "HIP events as each launch's dispatch-packet timestamps "
+                                      "(hipExtLaunchKernelGGL), rounds after the timed region; "
+                                      "the rest of ms_per_step is launch gaps"},
         "_end_round": s1["rounds"], "_fingerprint": fp,
     }
     if not args.no_cpu_baseline:

@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libshadowgpu.so")
+# SG_LIB (A/B experiments only): another in-tree build of the same library,
+# e.g. shadow_amd/libshadowgpu_v.so from `python -m shadow_amd.build --variant v -DX=1`
+LIB_PATH = os.path.join(_PKG, os.environ.get("SG_LIB", "libshadowgpu.so"))
 
 SG_OK, SG_ERR_INVAL, SG_ERR_NOMEM, SG_ERR_HIP, SG_ERR_OVERFLOW, SG_ERR_STATE, SG_ERR_NODEV = range(7)
 SG_ATTACH_MODULO, SG_ATTACH_RANDOM = 0, 1

@@ -45,7 +45,13 @@ def _stale(out, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, variant: str = "", defines=()) -> str:
+    """variant / defines: an A/B build (libshadowgpu_<variant>.so, objects in
+    build/<variant>/) with extra -D flags; the default build has neither."""
+    global BUILD, LIB
+    if variant:
+        BUILD = os.path.join(ROOT, "build", variant)
+        LIB = os.path.join(PKG, f"libshadowgpu_{variant}.so")
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(INC, f) for f in os.listdir(INC) if f.endswith(".h")]
     hdrs += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
@@ -64,7 +70,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
             continue
         obj = os.path.join(BUILD, src + ".o")
         if force or _stale(obj, [path] + hdrs):
-            _run([HIPCC] + HIP_FLAGS + ["-c", path, "-o", obj], verbose)
+            _run([HIPCC] + HIP_FLAGS + list(defines) + ["-c", path, "-o", obj], verbose)
         objs.append(obj)
     if force or _stale(LIB, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-lpthread"],
@@ -73,4 +79,6 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    a = sys.argv[1:]
+    v = a[a.index("--variant") + 1] if "--variant" in a else ""
+    print(build(verbose=True, force="--force" in a, variant=v, defines=[x for x in a if x.startswith("-D")]))
