@@ -119,7 +119,7 @@ struct sg_policy {
     sg_simtime next_min;
     int error;
     const sgp_rec* runs;
-    const uint32_t *run_off, *run_len; /* per host index, from the last extract */
+    const uint32_t* run_off;  /* [n + 1] per host index, host-ordered runs of the last extract */
     uint32_t run_gen;         /* bumped per extract: host run_pos values reset lazily */
     uint32_t* self_list;      /* hosts whose CPU heap may hold events */
     uint32_t n_self;
@@ -336,7 +336,9 @@ int sg_policy_push(sg_policy* p, uint64_t token, uint64_t handle, sg_simtime tim
 }
 
 /* This round's run of host idx: its length, and run_pos reset on first use. */
-static uint32_t run_len(const sg_policy* p, uint32_t idx) { return p->run_len ? p->run_len[idx] : 0; }
+static uint32_t run_len(const sg_policy* p, uint32_t idx) {
+    return p->run_off ? p->run_off[idx + 1] - p->run_off[idx] : 0;
+}
 static void run_touch(sg_policy* p, host_rt* h) {
     if (h->run_gen != p->run_gen) {
         h->run_gen = p->run_gen;
@@ -352,15 +354,14 @@ static int prepare(sg_policy* p, sg_simtime barrier) {
         p->preparing = 1;
         pthread_mutex_unlock(&p->m);
         const sgp_rec* runs;
-        const uint32_t *off, *cnt;
+        const uint32_t* off;
         uint64_t total;
         double t0 = p->prof ? now_s() : 0;
-        int rc = sgp_dev_extract(p->dev, barrier, &runs, &off, &cnt, &total);
+        int rc = sgp_dev_extract(p->dev, barrier, &runs, &off, &total);
         double t1 = p->prof ? now_s() : 0;
         if (rc == 0) {  /* no per-host pass: pop reads off / cnt and resets run_pos lazily */
             p->runs = runs;
             p->run_off = off;
-            p->run_len = cnt;
             p->run_gen++;
         }
         if (p->prof) {

@@ -34,9 +34,10 @@ void sgp_host_free(void* p);
 int sgp_dev_min(sgp_dev* d, uint64_t* min_out);
 /* Remove every queued event with time < barrier; returns them in `runs`
  * (pinned host memory owned by d), grouped per host in event_compare order,
- * host h's run at [off[h], off[h] + cnt[h]). */
+ * runs in host order: host h's run is [off[h], off[h + 1]) (off has N + 1
+ * entries). */
 int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const uint32_t** off,
-                    const uint32_t** cnt, uint64_t* total);
+                    uint64_t* total);
 /* Copy out every queued record (teardown). */
 int sgp_dev_all(sgp_dev* d, sgp_rec* out, uint64_t capacity, uint64_t* n_out);
 

@@ -5,9 +5,16 @@
 // key (time, src host id, srcHostEventID; the destination is the queue).
 //   k_pins      staged events → destination queues; overflowing records are
 //               listed so the host can grow the queues and re-deliver them
-//   k_pextract  per host: every event before the barrier, ranked in
-//               event_compare order (event.c:110-153) and written as one
-//               contiguous run per host; the rest is compacted in place
+//   extraction  three passes over the hosts whose earliest event is before
+//               the barrier (every other host is one 8-byte read):
+//     k_pcount    due events per host, block sums
+//     k_pscan     exclusive scan of the block sums (one workgroup)
+//     k_pwrite    per host: its due events' slots gathered in registers,
+//                 ranked among themselves in event_compare order
+//                 (event.c:110-153), written as one contiguous run at the
+//                 host-ordered offset; the rest compacted in place
+//     The runs are in host order, so off[h + 1] - off[h] is host h's count:
+//     one N + 1 offset array crosses PCIe, no count array.
 //   k_pmin      MIN over the hosts' earliest times (host_single.c:273-305)
 #include <hip/hip_runtime.h>
 
@@ -84,59 +91,138 @@ __device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uin
     return (t < bt) | ((t == bt) & ((s < bs) | ((s == bs) & (q < bq))));
 }
 
-__global__ __launch_bounds__(BLOCK) void k_pextract(Q q, uint64_t barrier, sgp_rec* out, uint32_t* off,
-                                                    uint32_t* cnt_out, unsigned long long* total) {
-    __shared__ uint32_t s_cnt[BLOCK];
-    __shared__ uint32_t s_base;
+// Due events of host h (time < barrier) and the earliest time after it.
+__global__ __launch_bounds__(BLOCK) void k_pcount(Q q, uint64_t barrier, uint32_t* kcnt, uint32_t* bsum) {
+    __shared__ uint32_t s_w[BLOCK / 64];
+    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t k = 0;
+    if (h < q.n && q.hmin[h] < barrier) {
+        const uint32_t c = q.cnt[h];
+        for (uint32_t j = 0; j < c; ++j) k += q.time[(size_t)j * q.n + h] < barrier;
+    }
+    if (h < q.n) kcnt[h] = k;
+    uint32_t w = k;
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < BLOCK / 64; ++i) t += s_w[i];
+        bsum[blockIdx.x] = t;
+    }
+}
+
+// Exclusive scan of nb block sums in place (one workgroup of 1024), total out.
+__global__ __launch_bounds__(1024) void k_pscan(uint32_t* bsum, uint32_t nb, unsigned long long* total) {
+    __shared__ uint32_t s[1024];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < nb ? bsum[i] : 0;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t u = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
+            __syncthreads();
+            s[threadIdx.x] += u;
+            __syncthreads();
+        }
+        if (i < nb) bsum[i] = carry + s[threadIdx.x] - v;
+        carry += s[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+constexpr uint32_t KREG = 8;  // due events a lane ranks in registers; more take the slow path
+
+__global__ __launch_bounds__(BLOCK) void k_pwrite(Q q, uint64_t barrier, const uint32_t* kcnt,
+                                                  const uint32_t* boff, sgp_rec* out, uint32_t* off) {
+    __shared__ uint32_t s[BLOCK];
     const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
     const size_t N = q.n;
-    uint32_t k = 0, c = 0;
-    uint64_t rest = SIMTIME_MAX;
-    const bool active = h < q.n && q.hmin[h] < barrier;
-    if (active) {
-        c = q.cnt[h];
-        for (uint32_t j = 0; j < c; ++j) {
-            const uint64_t t = q.time[(size_t)j * N + h];
-            if (t < barrier) ++k; else if (t < rest) rest = t;
-        }
-    }
-    // workgroup exclusive scan of k, one global allocation per workgroup
-    s_cnt[threadIdx.x] = k;
+    const uint32_t k = h < q.n ? kcnt[h] : 0;
+    s[threadIdx.x] = k;
     __syncthreads();
     for (int o = 1; o < BLOCK; o <<= 1) {
-        const uint32_t v = threadIdx.x >= (unsigned)o ? s_cnt[threadIdx.x - o] : 0;
+        const uint32_t u = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
         __syncthreads();
-        s_cnt[threadIdx.x] += v;
+        s[threadIdx.x] += u;
         __syncthreads();
     }
-    if (threadIdx.x == BLOCK - 1) s_base = (uint32_t)atomicAdd(total, (unsigned long long)s_cnt[BLOCK - 1]);
-    __syncthreads();
-    const uint32_t base = s_base + s_cnt[threadIdx.x] - k;
-    if (h < q.n) {
-        off[h] = base;
-        cnt_out[h] = k;
-    }
-    if (!active || k == 0) return;
-    // rank every due event among the due ones: its position in the host's run
-    for (uint32_t i = 0; i < c; ++i) {
-        const size_t ki = (size_t)i * N + h;
-        const uint64_t ti = q.time[ki];
-        if (ti >= barrier) continue;
-        const uint32_t si = q.src[ki];
-        const uint64_t qi = q.seq[ki];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < c; ++j) {
-            const size_t kj = (size_t)j * N + h;
-            const uint64_t tj = q.time[kj];
-            if (tj < barrier && key_less(tj, q.src[kj], q.seq[kj], ti, si, qi)) ++rank;
+    const uint32_t base = boff[blockIdx.x] + s[threadIdx.x] - k;
+    if (h < q.n) off[h] = base;
+    if (h + 1 == q.n) off[q.n] = base + k;
+    if (k == 0) return;
+    const uint32_t c = q.cnt[h];
+    // the due slots, in registers (the host's times are read once)
+    uint32_t idx[KREG] = {};
+    uint64_t tt[KREG] = {};
+    uint32_t nd = 0;
+    uint64_t rest = SIMTIME_MAX;
+    for (uint32_t j = 0; j < c; ++j) {
+        const uint64_t t = q.time[(size_t)j * N + h];
+        if (t < barrier) {
+#pragma unroll
+            for (uint32_t a = 0; a < KREG; ++a) {  // selects, so the arrays stay in registers
+                const bool w = a == nd;
+                idx[a] = w ? j : idx[a];
+                tt[a] = w ? t : tt[a];
+            }
+            ++nd;
+        } else if (t < rest) {
+            rest = t;
         }
-        sgp_rec r;
-        r.time = ti;
-        r.seq = qi;
-        r.handle = q.handle[ki];
-        r.src_id = si;
-        r.dst = h;
-        out[base + rank] = r;
+    }
+    if (nd <= KREG) {
+        uint32_t ss[KREG];
+        uint64_t sq[KREG];
+#pragma unroll
+        for (uint32_t a = 0; a < KREG; ++a) {
+            if (a >= nd) break;
+            const size_t ka = (size_t)idx[a] * N + h;
+            ss[a] = q.src[ka];
+            sq[a] = q.seq[ka];
+        }
+#pragma unroll
+        for (uint32_t a = 0; a < KREG; ++a) {
+            if (a >= nd) break;
+            uint32_t rank = 0;
+#pragma unroll
+            for (uint32_t b = 0; b < KREG; ++b) {
+                if (b >= nd) break;
+                rank += key_less(tt[b], ss[b], sq[b], tt[a], ss[a], sq[a]);
+            }
+            sgp_rec r;
+            r.time = tt[a];
+            r.seq = sq[a];
+            r.handle = q.handle[(size_t)idx[a] * N + h];
+            r.src_id = ss[a];
+            r.dst = h;
+            out[base + rank] = r;
+        }
+    } else {
+        // many due events at one host: rank each among the due ones from memory
+        for (uint32_t i = 0; i < c; ++i) {
+            const size_t ki = (size_t)i * N + h;
+            const uint64_t ti = q.time[ki];
+            if (ti >= barrier) continue;
+            const uint32_t si = q.src[ki];
+            const uint64_t qi = q.seq[ki];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < c; ++j) {
+                const size_t kj = (size_t)j * N + h;
+                const uint64_t tj = q.time[kj];
+                if (tj < barrier && key_less(tj, q.src[kj], q.seq[kj], ti, si, qi)) ++rank;
+            }
+            sgp_rec r;
+            r.time = ti;
+            r.seq = qi;
+            r.handle = q.handle[ki];
+            r.src_id = si;
+            r.dst = h;
+            out[base + rank] = r;
+        }
     }
     // compact the events after the barrier to the front
     uint32_t w = 0;
@@ -202,13 +288,13 @@ struct sgp_dev {
     uint32_t* d_nfail;
     sgp_rec* d_out;     // extracted runs
     uint64_t out_cap;
-    uint32_t* d_off;
-    uint32_t* d_cnt;
+    uint32_t* d_off;     // [N + 1] host-ordered run offsets
+    uint32_t* d_cnt;     // [N] due events per host
+    uint32_t* d_bsum;    // [N / BLOCK] block sums, scanned in place
     unsigned long long* d_scalar;
     sgp_rec* h_runs;    // pinned
     uint64_t h_runs_cap;
     uint32_t* h_off;
-    uint32_t* h_cnt;
     uint64_t queued;    // events in HBM
 };
 
@@ -299,11 +385,11 @@ int sgp_dev_create(int device, uint32_t n_hosts, uint32_t cap, sgp_dev** out) {
         return rc;
     }
     if (hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->d_off, (size_t)n_hosts * 4) != hipSuccess ||
+        hipMalloc(&d->d_off, ((size_t)n_hosts + 1) * 4) != hipSuccess ||
         hipMalloc(&d->d_cnt, (size_t)n_hosts * 4) != hipSuccess ||
+        hipMalloc(&d->d_bsum, ((size_t)n_hosts + BLOCK - 1) / BLOCK * 4) != hipSuccess ||
         hipMalloc(&d->d_nfail, 4) != hipSuccess || hipMalloc(&d->d_scalar, 16) != hipSuccess ||
-        hipHostMalloc((void**)&d->h_off, (size_t)n_hosts * 4, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&d->h_cnt, (size_t)n_hosts * 4, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&d->h_off, ((size_t)n_hosts + 1) * 4, hipHostMallocDefault) != hipSuccess) {
         sg_set_error("sgp_dev_create: allocation failed");
         sgp_dev_destroy(d);
         return 2;
@@ -322,12 +408,11 @@ int sgp_dev_destroy(sgp_dev* d) {
     if (!d) return 0;
     if (d->s) (void)hipStreamSynchronize(d->s);
     for (void* p : d->qallocs) (void)hipFree(p);
-    void* dp[] = {d->d_in, d->d_fail, d->d_out, d->d_off, d->d_cnt, d->d_nfail, d->d_scalar};
+    void* dp[] = {d->d_in, d->d_fail, d->d_out, d->d_off, d->d_cnt, d->d_bsum, d->d_nfail, d->d_scalar};
     for (void* p : dp)
         if (p) (void)hipFree(p);
     if (d->h_runs) (void)hipHostFree(d->h_runs);
     if (d->h_off) (void)hipHostFree(d->h_off);
-    if (d->h_cnt) (void)hipHostFree(d->h_cnt);
     if (d->s) (void)hipStreamDestroy(d->s);
     delete d;
     return 0;
@@ -415,25 +500,24 @@ int sgp_dev_min(sgp_dev* d, uint64_t* min_out) {
 }
 
 int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const uint32_t** off,
-                    const uint32_t** cnt, uint64_t* total) {
+                    uint64_t* total) {
     PCHK(hipSetDevice(d->device));
     int rc = grow_out(d, d->queued ? d->queued : 1);
     if (rc) return rc;
-    PCHK(hipMemsetAsync(d->d_scalar, 0, 8, d->s));
-    const uint32_t n = d->q.n;
-    hipLaunchKernelGGL(k_pextract, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, d->q, barrier,
-                       d->d_out, d->d_off, d->d_cnt, d->d_scalar);
+    const uint32_t n = d->q.n, nb = (n + BLOCK - 1) / BLOCK;
+    hipLaunchKernelGGL(k_pcount, dim3(nb), dim3(BLOCK), 0, d->s, d->q, barrier, d->d_cnt, d->d_bsum);
+    hipLaunchKernelGGL(k_pscan, dim3(1), dim3(1024), 0, d->s, d->d_bsum, nb, d->d_scalar);
+    hipLaunchKernelGGL(k_pwrite, dim3(nb), dim3(BLOCK), 0, d->s, d->q, barrier, d->d_cnt, d->d_bsum,
+                       d->d_out, d->d_off);
     PCHK(hipGetLastError());
     unsigned long long t = 0;
     PCHK(hipMemcpyAsync(&t, d->d_scalar, 8, hipMemcpyDeviceToHost, d->s));
-    PCHK(hipMemcpyAsync(d->h_off, d->d_off, (size_t)n * 4, hipMemcpyDeviceToHost, d->s));
-    PCHK(hipMemcpyAsync(d->h_cnt, d->d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost, d->s));
+    PCHK(hipMemcpyAsync(d->h_off, d->d_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, d->s));
     PCHK(hipStreamSynchronize(d->s));
     if (t) PCHK(hipMemcpy(d->h_runs, d->d_out, t * sizeof(sgp_rec), hipMemcpyDeviceToHost));
     d->queued -= t;
     *runs = d->h_runs;
     *off = d->h_off;
-    *cnt = d->h_cnt;
     *total = t;
     return 0;
 }
