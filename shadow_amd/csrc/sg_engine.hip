@@ -198,6 +198,7 @@ struct RoundState {
     uint64_t nfree;          // due chunks outside the retained bucket (a prefix of the list):
                              // k_gather returns them to the free ring behind fl_tail
     uint64_t rmin_todo;      // k_plan listed a window: k_scatter's last workgroup computes rmin
+    uint64_t listed;         // k_plan listed a new window: k_scatter gathers and routes for it
     uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
     uint64_t fl_head, fl_tail;
     uint64_t ins_local;      // k_count took the staged local events (process step)
@@ -208,7 +209,9 @@ struct RoundState {
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
     uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
     uint64_t xacc[2];    // emitted min, discovery min of this launch's workgroups (atomics)
-    uint64_t xcarry;     // carry min of k_gather's workgroups (atomics; read by k_plan mode 0)
+    uint64_t xcarry;     // carry min: what stays in the straddling bucket after k_scatter's gather
+                         // and inserts (atomics; read by k_plan mode 0 and the step headers,
+                         // reset by k_plan when a round completes)
 };
 
 struct Dev {
@@ -229,7 +232,6 @@ struct Dev {
     const uint16_t* vtab16;   // [N] attachment vertex only, when dst_exact
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
     uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
-    uint32_t gather_t;        // k_gather workgroup size (256 or 1024)
     uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
@@ -265,7 +267,6 @@ struct Dev {
     Rec* loc;                 // [P][ECAP]
     Rec* sends;               // [P][ECAP] k_proc's per-send records (phases A-C)
     // per-workgroup partials
-    uint64_t* c1min;          // [G1] carry min
     uint64_t* p2min;          // [2][P] emitted min, discovery min
     uint64_t* pcum;           // [NCTR][P] cumulative counters
     // multi-shard
@@ -633,6 +634,7 @@ __global__ void k_boot(Dev d) {
         rs->rmin = SIMTIME_MAX;
         rs->ndue = 0;
         rs->ndueb = 0;
+        rs->listed = 0;
         rs->ret_b = UINT64_MAX;
         rs->fl_head = nb0;
         rs->fl_tail = d.NCH;
@@ -707,25 +709,25 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
     }
 }
 
-// GT threads per workgroup (SG_GATHER_T: 256 or 1024), GR events per thread
-// in registers on the one-pass path (4 chunks per workgroup either way).
+// Gather role of k_scatter's workgroups [g0, g0 + nw): the due chunks k_plan
+// listed for the new window [S, E) into the host partitions.  GR events per
+// thread in registers on the one-pass path (4 chunks per workgroup).  The
+// listed counts cover only the slots filled before this launch ("old"
+// slots); the same launch's insert workgroups route the new due events
+// themselves, so the two never touch the same slot.
+constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8;
 template <int GT>
-__global__ __launch_bounds__(GT) void k_gather(Dev d) {
+__device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char* lds) {
     constexpr int GR = 4 * (int)CH / GT;
     const RoundState* rs = d.rs;
-    if (rs->done | rs->phase) return;
-    __shared__ uint32_t s_cnt[PMAX];
-    __shared__ uint32_t s_cur[PMAX];
-    __shared__ DueEnt s_de[GDMAX];
-    __shared__ uint64_t s16[16];
+    uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
+    uint32_t* s_cur = s_cnt + PMAX;                        // [PMAX]
+    DueEnt* s_de = (DueEnt*)(s_cur + PMAX);                // [GDMAX]
+    uint64_t* s16 = (uint64_t*)(s_de + GDMAX);             // [16]
     const uint64_t S = rs->S, E = rs->E;
     const uint64_t nd = rs->ndue;
-    const uint64_t c0 = nd * blockIdx.x / gridDim.x, c1 = nd * (blockIdx.x + 1) / gridDim.x;
+    const uint64_t c0 = nd * w / nw, c1 = nd * (w + 1) / nw;
     const uint32_t P = d.P;
-    if (d.outn && blockIdx.x == 0 && threadIdx.x < d.G) {  // a process step refills the outboxes
-        d.outn[threadIdx.x] = 0;
-        d.sent[threadIdx.x] = 0;
-    }
     // The window's chunks outside the retained bucket go back to the free ring
     // behind fl_tail, from the due entries as they are staged below (k_plan
     // advances the tail once the round is done; nothing allocates before it).
@@ -832,7 +834,6 @@ __global__ __launch_bounds__(GT) void k_gather(Dev d) {
     const uint64_t m = block_min(cmin, s16);
     const uint64_t nt = block_sum(ntomb, s16);
     if (threadIdx.x == 0) {
-        d.c1min[blockIdx.x] = m;
         if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry, (unsigned long long)m);
         if (rs->ret_b != UINT64_MAX) {
             const uint32_t rb = (uint32_t)(rs->ret_b % d.R);
@@ -1677,9 +1678,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
         __syncthreads();
         if (s_lastwg) {
-            uint64_t m = UINT64_MAX;
-            for (uint32_t i = tid; i < d.G1; i += K2_T) m = d.c1min[i] < m ? d.c1min[i] : m;
-            m = block_min(m, s16);  // barriers inside
+            uint64_t m = rs->xcarry;  // carry min (k_scatter's atomics, a kernel ago)
             const uint64_t em = atomic_read(&rs->xacc[0]), jm = atomic_read(&rs->xacc[1]);
             m = em < m ? em : m;
             m = rs->rmin < m ? rs->rmin : m;
@@ -1787,28 +1786,128 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     }
 }
 
-// One event into its reserved slot of bucket t / W.
-__device__ __forceinline__ void place_event(const Dev& d, uint32_t* s_cur, uint64_t t, uint64_t k, uint32_t dl) {
-    const uint64_t b = t / d.W;
-    const uint32_t rb = (uint32_t)(b % d.R);
-    const uint32_t pos = atomicAdd(&s_cur[rb], 1u);
-    if ((pos >> CH_SHIFT) >= d.nal[rb]) return;  // beyond the pool (flagged by k_plan)
-    const uint32_t id = d.btab[(size_t)rb * d.NCH + (pos >> CH_SHIFT)];
-    if (id >= d.NCH) return;
-    d.pool[((size_t)id << CH_SHIFT) + (pos & (CH - 1))] = Rec{((uint64_t)dl << 40) | (t - b * d.W), k};
+// k_scatter: new (and received) events into the calendar, fused with the
+// gather of the window k_plan just listed.  Workgroup roles:
+//   [0, P)          partition blk's staged local events (process step)
+//   [P, P + G3)     the received blocks' events (multi-shard), split evenly
+//   [g0, g0 + G1)   gather: the listed due chunks into the host partitions
+//   last            rmin: first live bucket beyond the new window, its min
+// An inserted event due in the new window (t < E) is routed straight to its
+// host partition instead: its slot stays empty in a fully due bucket (whose
+// chunks k_plan did not grow and k_scatter's gather returns to the ring) or
+// becomes a tombstone in the straddling bucket.  Events that stay in the
+// straddling bucket add to the carry min (the next MIN term), as the
+// gather's leftovers do.
+constexpr int SU = 4;  // events per thread in flight
+constexpr size_t INS_LDS = (RMAX + 2 * PMAX) * 4 + 16 * 8 + MAXG * 4;
+constexpr size_t SCAT_LDS = INS_LDS > GATHER_LDS ? INS_LDS : GATHER_LDS;
+
+struct Route {
+    bool listed;
+    uint64_t S, E, ret;   // the new window, its straddling bucket (UINT64_MAX: none)
+};
+
+// One batch of up to SU events per thread (every thread of the workgroup
+// calls it): slot from the (partition, bucket) reservation cursor, chunk
+// from k_plan's allocation; due events routed.  Returns nothing; carry min
+// and tombstones accumulate in smin / ntomb.
+__device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t* s_cur, uint32_t* s_pc,
+                                             uint32_t* s_pk, const bool (&v)[SU], const uint64_t (&t)[SU],
+                                             const uint64_t (&k)[SU], const uint32_t (&dl)[SU], uint64_t& smin,
+                                             uint64_t& ntomb) {
+    const uint64_t W = d.W;
+    const uint32_t R = d.R;
+    uint32_t rb[SU], pos[SU];
+    bool due[SU], write[SU];
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+        const uint64_t b = t[q] / W;
+        rb[q] = v[q] ? (uint32_t)(b % R) : 0u;
+        pos[q] = v[q] ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
+        due[q] = v[q] && ro.listed && t[q] < ro.E;
+        const bool in_ret = ro.listed && b == ro.ret;
+        write[q] = v[q] && (!due[q] || in_ret);  // fully due buckets: the slot stays empty
+        if (v[q] && !due[q] && in_ret) smin = t[q] < smin ? t[q] : smin;
+        if (due[q]) atomicAdd(&s_pc[dl[q] >> d.hp_shift], 1u);
+    }
+    uint32_t na[SU], id[SU];
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+        const uint32_t ci = pos[q] >> CH_SHIFT;
+        na[q] = d.nal[rb[q]];
+        id[q] = d.btab[(size_t)rb[q] * d.NCH + (ci < d.NCH ? ci : d.NCH - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+        // beyond the allocation only when the pool ran out (k_plan flagged it)
+        if (!write[q] || (pos[q] >> CH_SHIFT) >= na[q] || id[q] >= d.NCH) continue;
+        const uint64_t b = t[q] / W;
+        Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | (t[q] - b * W)), k[q]};
+        ntomb += due[q];
+        d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r;
+    }
+    if (!ro.listed) return;  // launch-uniform
+    // due events: one reservation per (workgroup, partition), then the copies
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) {
+        const uint32_t c = s_pc[p];
+        s_pk[p] = 0;
+        if (c) {
+            const uint32_t base = atomicAdd(&d.pcnt[p], c);
+            if (base + c > d.CAPP) flag(d, OV_PART);
+            s_pc[p] = base;
+        }
+    }
+    __syncthreads();
+    const uint32_t hmask = d.HP - 1;
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+        if (!due[q]) continue;
+        const uint32_t p = dl[q] >> d.hp_shift;
+        const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
+        if (slot < d.CAPP)
+            d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl[q] & hmask) << 52) | (t[q] - ro.S), k[q]};
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uint64_t smin, uint64_t ntomb,
+                                              uint64_t* s16) {
+    if (!ro.listed || ro.ret == UINT64_MAX) return;  // launch-uniform
+    const uint64_t m = block_min(smin, s16);
+    const uint64_t nt = block_sum(ntomb, s16);
+    if (threadIdx.x == 0) {
+        const uint32_t rb = (uint32_t)(ro.ret % d.R);
+        if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
+        if (m != UINT64_MAX) {
+            atomicMin((unsigned long long*)&d.rs->xcarry, (unsigned long long)m);
+            atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)m);
+        }
+    }
 }
 
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     RoundState* rs = d.rs;
     if (rs->done) return;
-    __shared__ uint32_t s_off[MAXG];
-    __shared__ uint32_t s_cur[RMAX];
-    __shared__ uint64_t s16[16];
+    __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     const uint32_t R = d.R, blk = blockIdx.x;
+    const uint32_t g0 = d.P + (recv ? d.G3 : 0);
+    Route ro;
+    ro.listed = rs->listed != 0;
+    ro.S = rs->S;
+    ro.E = rs->E;
+    ro.ret = rs->ret_b;
     if (blk == gridDim.x - 1) {
+        uint64_t* s16 = (uint64_t*)lds;
+        if (ro.listed && d.outn && threadIdx.x < d.G) {  // the next step processes: outboxes refill
+            d.outn[threadIdx.x] = 0;
+            d.sent[threadIdx.x] = 0;
+        }
         // rmin for the window k_plan just listed: the first non-empty bucket in
         // (bL, bS + R) and its min time.  k_plan wrote the metadata back; this
-        // launch only writes pool slots, so the counts it reads are final.
+        // launch changes only the straddling bucket's, so the counts read are final.
         if (!rs->rmin_todo) return;
         const uint64_t bS = rs->bS, bL = rs->bL;
         const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
@@ -1827,71 +1926,66 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         }
         return;
     }
+    if (blk >= g0) {
+        if (ro.listed) gather_role<K3_T>(d, blk - g0, gridDim.x - 1 - g0, lds);
+        return;
+    }
+    uint32_t* s_cur = (uint32_t*)lds;    // [RMAX] slot cursor per bucket
+    uint32_t* s_pc = s_cur + RMAX;       // [PMAX] routed events per partition, then their base
+    uint32_t* s_pk = s_pc + PMAX;        // [PMAX] cursor within it
+    uint64_t* s16 = (uint64_t*)(s_pk + PMAX);
+    uint32_t* s_off = (uint32_t*)(s16 + 16);  // [MAXG] received blocks' offsets
     const uint32_t* wb = d.wbase + (size_t)blk * R;
+    uint64_t smin = UINT64_MAX, ntomb = 0;
     if (blk < d.P) {  // partition blk's staged local events
         if (!rs->ins_local) return;
         const uint32_t n = d.rcnt[blk];
-        if (n == 0) return;
-        const uint64_t S = rs->ins_S, W = d.W;
+        if (n == 0) return;  // uniform: nothing routed, nothing to finish
+        const uint64_t S = rs->ins_S;
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
-        // SU events per thread in flight: every load of a batch is issued
-        // before any is used (staged record, then chunk table + allocation);
-        // the first batch's records are loaded together with the cursors
-        constexpr int SU = 4;
-        Rec r[SU];
-#pragma unroll
-        for (int q = 0; q < SU; ++q) {
-            const uint32_t i = threadIdx.x + q * K3_T;
-            r[q] = ld_stream(&src[i < n ? i : 0]);
-        }
         const uint32_t* xo = d.bxoff + (size_t)(blk % XS) * R;
         for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
+        for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
         __syncthreads();
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
-            if (i0) {
-#pragma unroll
-                for (int q = 0; q < SU; ++q) {
-                    const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                    r[q] = ld_stream(&src[i < n ? i : 0]);
-                }
-            }
-            uint32_t rb[SU], pos[SU];
+            bool v[SU];
+            uint64_t t[SU], k[SU];
+            uint32_t dl[SU];
 #pragma unroll
             for (int q = 0; q < SU; ++q) {
                 const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                const uint64_t t = S + (r[q].a & M40);
-                const uint64_t b = t / W;
-                rb[q] = i < n ? (uint32_t)(b % R) : 0u;
-                pos[q] = i < n ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
-                r[q].a = (r[q].a & ~M40) | (t - b * W);  // {dst_local << 40 | offset in bucket}
+                const Rec r = ld_stream(&src[i < n ? i : 0]);
+                v[q] = i < n;
+                t[q] = S + (r.a & M40);
+                k[q] = r.k;
+                dl[q] = (uint32_t)(r.a >> 40);
             }
-            uint32_t na[SU], id[SU];
-#pragma unroll
-            for (int q = 0; q < SU; ++q) {
-                const uint32_t ci = pos[q] >> CH_SHIFT;
-                na[q] = d.nal[rb[q]];
-                id[q] = d.btab[(size_t)rb[q] * d.NCH + (ci < d.NCH ? ci : d.NCH - 1)];
-            }
-#pragma unroll
-            for (int q = 0; q < SU; ++q) {
-                const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                // beyond the allocation only when the pool ran out (k_plan flagged it)
-                if (i < n && (pos[q] >> CH_SHIFT) < na[q] && id[q] < d.NCH)
-                    st_stream(&d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))], r[q]);
-            }
+            insert_batch(d, ro, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
+        insert_finish(d, ro, smin, ntomb, s16);
         return;
     }
-    const uint32_t g3 = gridDim.x - 1 - d.P, w = blk - d.P;
+    // the received blocks' events, split evenly over G3 workgroups
+    const uint32_t g3 = d.G3, w = blk - d.P;
     const uint32_t* xo = d.bxoff + (size_t)(w % XS) * R;
     for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
+    for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
     const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
-    for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
-        uint64_t t, k;
-        uint32_t dl;
-        if (recv_event(d, recv, s_off, (uint32_t)idx, t, k, dl)) place_event(d, s_cur, t, k, dl);
+    for (uint64_t i0 = lo; i0 < hi; i0 += K3_T * SU) {
+        bool v[SU];
+        uint64_t t[SU], k[SU];
+        uint32_t dl[SU];
+#pragma unroll
+        for (int q = 0; q < SU; ++q) {
+            const uint64_t idx = i0 + threadIdx.x + q * K3_T;
+            t[q] = k[q] = 0;
+            dl[q] = 0;
+            v[q] = idx < hi && recv_event(d, recv, s_off, (uint32_t)idx, t[q], k[q], dl[q]);
+        }
+        insert_batch(d, ro, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
     }
+    insert_finish(d, ro, smin, ntomb, s16);
 }
 
 // ----------------------------------------------------------------- plan ----
@@ -1932,8 +2026,7 @@ __device__ __forceinline__ void reset_bucket(const Dev& d, uint32_t rb) {
 // The local MIN terms of a round: carry min (k_gather), emitted min and
 // discovery min (k_proc), and the buckets beyond the window (rmin).
 __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
-    uint64_t mm = UINT64_MAX, jj = UINT64_MAX;
-    for (uint32_t i = threadIdx.x; i < d.G1; i += blockDim.x) mm = d.c1min[i] < mm ? d.c1min[i] : mm;
+    uint64_t mm = d.rs->xcarry, jj = UINT64_MAX;
     for (uint32_t i = threadIdx.x; i < d.P; i += blockDim.x) {
         const uint64_t x = d.p2min[i], y = d.p2min[d.P + i];
         mm = x < mm ? x : mm;
@@ -1951,6 +2044,7 @@ __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t&
 // coalesced load, scans and updates in LDS, one write-back.
 struct PlanLds {
     uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
+    uint32_t old[RMAX];  // count before this step's reservations: the slots already written
     uint32_t off[RMAX];  // allocation: first new chunk of each bucket in this launch's run
     uint64_t mn[RMAX];
     uint32_t fr[PL_T];   // the free ring's first PL_T entries from the head, read at launch
@@ -1974,13 +2068,14 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     if (pst) pst[k] = __builtin_amdgcn_s_memrealtime()
     PSTAMP(0);
     // bucket metadata: loads issued together with reduce_local's, LDS stores after
-    uint32_t rc[PER], rt[PER], rn[PER];
+    uint32_t rc[PER], rt[PER], rn[PER], ro[PER];
     uint64_t rm[PER];
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t rb = tid + q * PL_T;
         if (rb < R) {
             rc[q] = d.bcnt[rb];
+            ro[q] = rc[q];
             rt[q] = d.btomb[rb];
             rn[q] = d.nal[rb];
             rm[q] = d.bmin[rb];
@@ -2084,6 +2179,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         const uint32_t rb = tid + q * PL_T;
         if (rb < R) {
             B.cnt[rb] = rc[q];
+            B.old[rb] = ro[q];
             B.tomb[rb] = rt[q];
             B.nal[rb] = rn[q];
             B.mn[rb] = rm[q];
@@ -2097,6 +2193,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         ovf = s_ovf;
     }
     const bool round_done = mode == 0 || (mode == 1 && !s_more);
+    if (mode == 1 && round_done && tid == 0) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
     if (round_done) {
         // k_gather returned the window's chunks (not the retained bucket's) to
         // the ring behind the tail: take them, and reset the consumed buckets
@@ -2112,13 +2209,40 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         __syncthreads();
     }
     PSTAMP(2);
+    bool list = true;
+    if (mode == 1 && s_more) {  // drain step: same window, more exchange
+        list = false;
+        if (tid == 0) {
+            rs->phase = 1;
+            rs->overflow |= ovf;
+        }
+    } else if (round_done) {
+        if (tid == 0) {
+            rs->phase = 0;
+            rs->jmin = j;
+            apply_window(d, m, j, ~ovf);
+            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
+            s_S = rs->S;
+            s_E = rs->E;
+            s_done = rs->done;
+        }
+        __syncthreads();
+        list = !s_done;
+    }
+    PSTAMP(4);
+    // the new window's buckets (when listed): [nbS, nbL], nbL straddling E or not
+    const uint64_t nbS = s_S / W, nbL = (s_E - 1) / W;
+    const bool nstraddle = s_E < (nbL + 1) * W;
     if (mode != 2) {
         // every bucket gets the chunks its count needs (k_proc / k_count
         // reserved the slots), from the ring: per-bucket offsets into the run
         // of new chunks, then one cooperative pass over the run (a bucket
-        // search in LDS per chunk) so every ring load is independent
+        // search in LDS per chunk) so every ring load is independent.  A
+        // bucket the new window takes whole gets none: k_scatter routes its
+        // new events straight to the host partitions and never writes them.
         uint32_t need[PER];
         uint64_t mine = 0;
+        const uint32_t nbSr = (uint32_t)(nbS % R);
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;
@@ -2127,6 +2251,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
                 const uint64_t want = ((uint64_t)B.cnt[rb] + CH - 1) >> CH_SHIFT;
                 const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
                 need[q] = w > B.nal[rb] ? w - B.nal[rb] : 0;
+                const uint64_t o = rb >= nbSr ? rb - nbSr : rb + R - nbSr;  // bucket nbS + o
+                if (list && o <= nbL - nbS && !(nstraddle && o == nbL - nbS)) need[q] = 0;
             }
             mine += need[q];
         }
@@ -2169,29 +2295,10 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         __syncthreads();
     }
     PSTAMP(3);
-    bool list = true;
-    if (mode == 1 && s_more) {  // drain step: same window, more exchange
-        list = false;
-        if (tid == 0) {
-            rs->phase = 1;
-            rs->overflow |= ovf;
-        }
-    } else if (round_done) {
-        if (tid == 0) {
-            rs->phase = 0;
-            rs->jmin = j;
-            apply_window(d, m, j, ~ovf);
-            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
-            s_S = rs->S;
-            s_E = rs->E;
-            s_done = rs->done;
-        }
-        __syncthreads();
-        list = !s_done;
-    }
     PSTAMP(4);
     if (list) {
-        // list the due chunks of the new window [S, E)
+        // list the due chunks of the new window [S, E): the slots written
+        // before this launch (old); k_scatter routes the new ones itself
         const uint64_t S = s_S, E = s_E;
         const uint64_t bS = S / W, bL = (E - 1) / W;
         const uint64_t pr = rs->ret_b;
@@ -2221,11 +2328,14 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         uint64_t nd = 0, ndb = 0, nf = 0;
         for (uint64_t b = bS; b <= bL; ++b) {
             const uint32_t rb = (uint32_t)(b % R);
-            const uint32_t c = B.cnt[rb], nc = B.nal[rb];
+            const uint32_t c = B.cnt[rb], co = B.old[rb];
             const bool ret = straddle && b == bL;
+            // a retained bucket lists the chunks holding old slots; a bucket
+            // taken whole lists every chunk, all of them go back to the ring
+            const uint32_t nc = ret ? std::min<uint32_t>(B.nal[rb], (co + CH - 1) >> CH_SHIFT) : B.nal[rb];
             const uint32_t* tab = d.btab + (size_t)rb * NCH;
             for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-                const uint32_t left = c - (ci << CH_SHIFT);
+                const uint32_t left = co > (ci << CH_SHIFT) ? co - (ci << CH_SHIFT) : 0u;
                 const uint32_t n = left < CH ? left : CH;
                 d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
             }
@@ -2265,6 +2375,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             rs->ret_b = straddle ? bL : UINT64_MAX;
         }
     }
+    if (tid == 0) rs->listed = list ? 1 : 0;  // k_scatter gathers and routes for the new window
     __syncthreads();
     PSTAMP(6);
     for (uint32_t rb = tid; rb < R; rb += PL_T) {
@@ -2288,8 +2399,22 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
     for (int i = 0; i < NCTR; ++i) c[i] = 0;
     for (uint32_t b = threadIdx.x; b < d.P; b += 1024)
         for (int i = 0; i < NCTR; ++i) c[i] += d.pcum[(size_t)i * d.P + b];
+    // pending: live calendar events outside the listed window's buckets (the
+    // straddling one's stay), plus the window's events already in the host
+    // partitions (gathered or routed by k_scatter, not yet popped)
+    const RoundState* rs = d.rs;
+    const bool listed = rs->listed != 0;
+    const uint64_t bS = rs->bS, span = rs->bL - rs->bS;
+    const uint32_t bSr = (uint32_t)(bS % d.R);
+    const uint32_t retr = rs->ret_b != UINT64_MAX ? (uint32_t)(rs->ret_b % d.R) : UINT32_MAX;
     uint64_t pend = 0;
-    for (uint32_t rb = threadIdx.x; rb < d.R; rb += 1024) pend += d.bcnt[rb] - d.btomb[rb];
+    for (uint32_t rb = threadIdx.x; rb < d.R; rb += 1024) {
+        const uint64_t o = rb >= bSr ? rb - bSr : rb + d.R - bSr;
+        if (listed && o <= span && rb != retr) continue;
+        pend += d.bcnt[rb] - d.btomb[rb];
+    }
+    if (listed)
+        for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += d.pcnt[p];
     for (int i = 0; i < NCTR; ++i) {
         const uint64_t t = block_sum(c[i], s16);
         if (threadIdx.x == 0) d.rs->ctr[i] = t;
@@ -2555,7 +2680,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
-    d.gather_t = env_u32("SG_GATHER_T", 1024) == 1024 ? 1024 : K1_T;
     d.check = env_u32("SG_CHECK", 0) != 0;
     // host partitions: HP hosts per k_proc workgroup (power of two), about
     // one partition per CU
@@ -2707,7 +2831,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rcnt, P);
     ALLOC(D.loc, P * D.ECAP);
     ALLOC(D.sends, P * D.ECAP);
-    ALLOC(D.c1min, D.G1);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
     if (G > 1 || p.exchange_cap) {  // step API (a single shard may use it too: exchange_cap != 0)
@@ -2852,19 +2975,15 @@ int sg_engine_boot(sg_engine* e) {
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, (const int64_t*)nullptr, 2);
     HIPCHK(hipGetLastError());
+    // the first window's gather (k_scatter's gather role; nothing is staged yet)
+    hipLaunchKernelGGL(k_scatter, dim3(d.P + d.G1 + 1), dim3(K3_T), 0, e->stream, d, (const int64_t*)nullptr);
+    HIPCHK(hipGetLastError());
     e->booted = true;
     return SG_OK;
 }
 
 static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
-    int rc = timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {
-        if (d.gather_t == 1024)
-            SG_LAUNCH(k_gather<1024>, dim3(d.G1), dim3(1024), 0, e->stream, a, b, d);
-        else
-            SG_LAUNCH(k_gather<K1_T>, dim3(d.G1), dim3(K1_T), 0, e->stream, a, b, d);
-    });
-    if (rc) return rc;
     return timed_launch(e, SG_K_PROCESS, [&](hipEvent_t a, hipEvent_t b) {
         SG_LAUNCH(k_proc, dim3(d.P), dim3(K2_T), d.proc_lds, e->stream, a, b, d);
     });
@@ -2887,7 +3006,7 @@ static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
     });
     if (rc) return rc;
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + 1), dim3(K3_T), 0, e->stream, a, b, d, recv);
+        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 1), dim3(K3_T), 0, e->stream, a, b, d, recv);
     });
 }
 

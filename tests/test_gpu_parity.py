@@ -140,7 +140,12 @@ def test_queue_capacity_paths(cap):
     one chunk per ring bucket).  A pool far below the live event count must fail
     loudly (SG_ERR_OVERFLOW), never silently; a large one stays bit-exact."""
     if cap == 1:
-        cfg = phold.c2_config(n_hosts=20_000, end_time_s=0.3)
+        # log-normal delays keep events in many future buckets (with C2's one
+        # 50 ms path every new event is due in the next window and k_scatter
+        # routes it past the calendar, so that config needs no chunks at all)
+        # (the pool also holds one chunk per ring bucket: 200k hosts' 3.2M live
+        # events need far more than that headroom)
+        cfg = phold.c4_config(n_hosts=200_000, V=64, end_time_s=0.3)
         eng = Engine(cfg, queue_cap=cap)
         eng.boot()
         with pytest.raises(L.SgError) as ei:
@@ -253,10 +258,12 @@ def test_long_paths_use_wide_records():
     assert gs["pops"] > 0
 
 
-def test_gather_workgroup_256(monkeypatch):
-    """k_gather is built for 1024- and 256-lane workgroups (SG_GATHER_T); the
-    non-default one must give the same bits, boot round (two-pass path) included."""
-    monkeypatch.setenv("SG_GATHER_T", "256")
+@pytest.mark.parametrize("grid", [1, 37, 512])
+def test_gather_grid(grid, monkeypatch):
+    """k_scatter's gather role over SG_GATHER_GRID workgroups: one (every due
+    chunk in one workgroup: the two-pass path every round), an odd count, and
+    more workgroups than due chunks must all give the same bits."""
+    monkeypatch.setenv("SG_GATHER_GRID", str(grid))
     cfg = phold.c4_config(n_hosts=20_000)
     eng, orc = _run_both(cfg, max_rounds=40)
     _assert_same(eng, orc)
