@@ -89,6 +89,7 @@ constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
 constexpr uint32_t RETAINED = 1u << 31;
+constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record {evc, HDR_REC | host}
 // exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
 constexpr int HDR = 2;
 enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND };
@@ -165,6 +166,17 @@ struct DueEnt {
 struct HostInfo {
     int32_t wt;       // PHOLD weight threshold (test_phold.c:160-178)
     uint32_t vertex;  // attachment vertex
+    uint32_t slot;    // global slot: owner shard's first host + the host's place in its
+                      // shard's vertex-sorted order
+    uint32_t pad;
+};
+// Per local slot: the host's registration index (its id in event keys and
+// traces) and its attachment vertex.  A shard's hosts occupy slots in
+// (vertex, index) order, so a partition's hosts share a few vertices and their
+// path rows fit in LDS.
+struct SlotInfo {
+    uint32_t h;
+    uint32_t v;
 };
 struct PairRec {
     uint64_t delay;   // ceil(latency_ms * 1e6)   (worker.c:275-277)
@@ -229,7 +241,12 @@ struct Dev {
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
-    const uint16_t* vtab16;   // [N] attachment vertex only, when dst_exact
+    const uint32_t* vs32;     // [N] vertex << slot_bits | global slot, when dst_exact
+    uint32_t slot_bits;
+    const SlotInfo* sinfo;    // [L] per local slot
+    uint32_t lds_rows;        // k_proc stages its partition's path rows in LDS
+    const void* prow;         // [V][V] full row-major records (4 or 8 B) the rows are staged from
+    uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
     uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
     uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
@@ -347,8 +364,8 @@ __device__ __forceinline__ uint64_t digest_mix(uint64_t pos, uint64_t t, uint32_
     return fmix64(z ^ seq);
 }
 
-// Destination draw; returns N when no host is selected (test_phold.c:176-177)
-// and the chosen host's info record.  Weights rule: the first i with
+// Destination draw; returns the chosen host's global slot, or N when no host
+// is selected (test_phold.c:176-177), and its vertex.  Weights rule: the first i with
 // x <= wt[i] (non-decreasing thresholds); the uniform-position guess and its
 // two neighbours are loaded together, which settles near-uniform weights in
 // one round trip, and anything else is bisected.  Split in three steps
@@ -389,7 +406,7 @@ __device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_
                                                 uint32_t& vert) {
     if (d.dst_rule == SG_DST_UNIFORM_FLOOR) {
         vert = pb.cur.vertex;
-        return g;
+        return pb.cur.slot;
     }
     const uint32_t N = d.N;
     const HostInfo* w = d.hinfo;
@@ -397,14 +414,14 @@ __device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_
     if (x <= pb.cur.wt) {
         if (g == 0 || x > pb.prev.wt) {
             vert = opaque(pb.cur.vertex);
-            return g;
+            return opaque(pb.cur.slot);
         }
         lo = 0;
         hi = g - 1;  // x <= wt[g-1]: the answer is in [0, g-1]
     } else {
         if (g + 1 < N && x <= pb.next.wt) {
             vert = opaque(pb.next.vertex);
-            return g + 1;
+            return opaque(pb.next.slot);
         }
         if (g + 1 >= N || x > w[N - 1].wt) return N;
         lo = g + 2;
@@ -415,7 +432,7 @@ __device__ __forceinline__ uint32_t dst_resolve(const Dev& d, int32_t x, uint32_
         if (x <= w[mid].wt) hi = mid; else lo = mid + 1;
     }
     vert = opaque(w[lo].vertex);
-    return lo;
+    return opaque(w[lo].slot);
 }
 __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo& info) {
     const uint32_t g = dst_guess(d, x);
@@ -592,7 +609,7 @@ __global__ void k_boot(Dev d) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nb0 = (d.L + CH - 1) >> CH_SHIFT;
     if (i < d.L) {
-        const uint32_t h = d.lo + i;
+        const uint32_t h = d.sinfo[i].h;  // slot i's host
         d.pool[i] = Rec{(uint64_t)i << 40, (uint64_t)h << SRC_SHIFT};
         HostState s = d.hs[i];
         s.evc = 1;
@@ -852,7 +869,8 @@ struct Acc {
 };
 
 struct HostCtx {
-    uint32_t h, vh;
+    uint32_t h, vh;   // registration index, vertex
+    uint32_t sg;      // global slot (destinations are slots)
     HostState s;
 };
 
@@ -924,7 +942,7 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
         // message's first receipt forwards it to `load` peers, later ones are
         // dropped by the seen set
         nsend = 0;
-        const uint32_t lh = c.h - d.lo;
+        const uint32_t lh = c.sg - d.lo;
         if (boot) {
             const uint64_t N = d.N, M = d.gossip_msgs;
             const uint64_t m = ((uint64_t)c.h * M + N - 1) / N;
@@ -938,7 +956,7 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
                 } else if (tn < E) {
                     ++a.ctr[C_SAME];
                     if (!append(tn - S, key)) a.overflow = true;
-                } else if (stage_event(d, S, part, sh, a, c.h, tn, key)) {
+                } else if (stage_event(d, S, part, sh, a, c.sg, tn, key)) {
                     count(tn);
                 }
             }
@@ -976,12 +994,12 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
             continue;
         }
         const uint64_t key = ((uint64_t)c.h << SRC_SHIFT) | (sq << d.msg_shift) | msg;
-        if (dst == c.h && tn < E) {
+        if (dst == c.sg && tn < E) {
             ++a.ctr[C_SAME];
             if (!append(tn - S, key)) a.overflow = true;
             continue;
         }
-        if (dst != c.h && tn < E) {  // host_single.c:180-184
+        if (dst != c.sg && tn < E) {  // host_single.c:180-184
             tn = E;
             ++a.ctr[C_BUMPED];
         }
@@ -1009,8 +1027,8 @@ __device__ __forceinline__ void commit_send(const Dev& d, uint64_t S, uint64_t E
         ++a.ctr[C_DROPEND];
         return;
     }
-    if (dst == c.h && tn < E) a.overflow = true;  // excluded by the caller's self-path test
-    if (dst != c.h && tn < E) {
+    if (dst == c.sg && tn < E) a.overflow = true;  // excluded by the caller's self-path test
+    if (dst != c.sg && tn < E) {
         tn = E;
         ++a.ctr[C_BUMPED];
     }
@@ -1169,6 +1187,28 @@ __device__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t nblk, uint64_t*
     }
 }
 
+// The path record of (sv, dv) from the partition's LDS rows (sv in
+// [vlo, vlo + rows)); the discovered-ms field from HBM while it can matter.
+__device__ __forceinline__ PairRec lds_pair(const Dev& d, const unsigned char* rows, uint32_t vlo, uint32_t sv,
+                                            uint32_t dv, bool want_jump) {
+    const size_t i = (size_t)(sv - vlo) * d.V + dv;
+    PairRec pr;
+    if (d.pair_fmt == PAIR_NARROW) {
+        const uint2 v = reinterpret_cast<const uint2*>(rows)[i];
+        pr.delay = v.x;
+        pr.keep = (int32_t)v.y;
+    } else {
+        pr.delay = reinterpret_cast<const uint32_t*>(rows)[i];
+        pr.keep = SG_RAND_MAX;
+    }
+    pr.jump = want_jump ? d.pjump[pair_index(d, sv, dv)] : UINT32_MAX;
+    return pr;
+}
+
+// EXACT: d.dst_exact (a destination's vertex and slot are one 4-byte read per
+// send); the other instantiation resolves destinations through the weight
+// probes.  ROWS: d.lds_rows (path records from the partition's LDS rows).
+template <bool EXACT, bool ROWS>
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
     if (rs->done) return;
@@ -1187,6 +1227,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint32_t* s_bc = (uint32_t*)(dyn + d.bin_off);  // [R] staged local events per bucket
     uint32_t* s_bm = s_bc + R;                      // [R] their min time offset in the bucket
     Rec* s_ev = (Rec*)(dyn + d.ev_off);             // [EVL] due events grouped by host
+    const unsigned char* s_rows = dyn + d.row_off;  // [rows][V] path records of the partition's vertices
     __shared__ uint32_t s_nsend;
     __shared__ int32_t s_last;         // last weight threshold: x above it selects no host
     __shared__ ProcShared sh;
@@ -1228,6 +1269,27 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             rr[q] = i < n ? ld_stream(&part[i]) : Rec{0, 0};
         }
     }
+    // the partition's hosts share a few vertices (slots are vertex-sorted):
+    // their path rows into LDS, one coalesced pass
+    uint32_t vlo = 0;
+    if constexpr (ROWS) {
+        const uint32_t s0 = p * HP, s1 = (p + 1) * HP < d.L ? (p + 1) * HP : d.L;
+        vlo = d.sinfo[s0].v;
+        const uint32_t nrow = d.sinfo[s1 - 1].v - vlo + 1;
+        const uint32_t nent = (nrow < d.rows_max ? nrow : d.rows_max) * d.V;
+        const size_t r0 = (size_t)vlo * d.V;  // the rows are contiguous in the full table
+        for (uint32_t i = tid; i < nent; i += K2_T) {
+            if (d.pair_fmt == PAIR_NARROW)
+                reinterpret_cast<uint2*>(dyn + d.row_off)[i] = reinterpret_cast<const uint2*>(d.prow)[r0 + i];
+            else
+                reinterpret_cast<uint32_t*>(dyn + d.row_off)[i] = reinterpret_cast<const uint32_t*>(d.prow)[r0 + i];
+        }
+        if (nrow > d.rows_max && tid == 0) flag(d, OV_BUG);  // the host sized rows_max
+    }
+    auto pair_of = [&](uint32_t sv, uint32_t dv, bool wj) __attribute__((always_inline)) {
+        if constexpr (ROWS) return lds_pair(d, s_rows, vlo, sv, dv, wj);
+        else return load_pair(d, sv, dv, wj);
+    };
     if (stamp && tid == 0) stamp[20] = wait_stamp();
     __syncthreads();
     if (in_lds) {
@@ -1279,27 +1341,28 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint32_t nact = (uint32_t)tot;
     __syncthreads();
     if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
-    const uint32_t hbase = d.lo + p * HP;
+    const uint32_t sbase = p * HP;  // the partition's first local slot
     // phase A's first NPRE hosts of every lane: state loads issued now, under
     // the LDS scatter below
     constexpr uint32_t NPRE = 2;
     // HostState as two 16-B words per host, kept in plain scalars
     ulonglong2 pre_a0 = make_ulonglong2(0, 0), pre_b0 = pre_a0, pre_a1 = pre_a0, pre_b1 = pre_a0;
-    uint32_t pre_v0 = 0, pre_v1 = 0;
+    uint2 pre_s0 = make_uint2(0, 0), pre_s1 = pre_s0;  // SlotInfo {h, v}
     {
         const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
-        const uint32_t h0 = hbase + (tid < nact ? s_act[tid] : 0u);
-        if (tid < nact && h0 - d.lo < d.L) {
-            pre_a0 = ld_stream2(&hsw[2 * (size_t)(h0 - d.lo)]);
-            pre_b0 = ld_stream2(&hsw[2 * (size_t)(h0 - d.lo) + 1]);
-            pre_v0 = d.hinfo[h0].vertex;
+        const uint2* siw = reinterpret_cast<const uint2*>(d.sinfo);
+        const uint32_t l0 = sbase + (tid < nact ? s_act[tid] : 0u);
+        if (tid < nact && l0 < d.L) {
+            pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
+            pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
+            pre_s0 = siw[l0];
         }
         const uint32_t j1 = tid + K2_T;
-        const uint32_t h1 = hbase + (j1 < nact ? s_act[j1] : 0u);
-        if (j1 < nact && h1 - d.lo < d.L) {
-            pre_a1 = ld_stream2(&hsw[2 * (size_t)(h1 - d.lo)]);
-            pre_b1 = ld_stream2(&hsw[2 * (size_t)(h1 - d.lo) + 1]);
-            pre_v1 = d.hinfo[h1].vertex;
+        const uint32_t l1 = sbase + (j1 < nact ? s_act[j1] : 0u);
+        if (j1 < nact && l1 < d.L) {
+            pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
+            pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
+            pre_s1 = siw[l1];
         }
     }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
@@ -1365,8 +1428,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 const uint32_t hl = s_act[j];
                 cnt = s_n[hl];
                 seg = segs + (s_c[hl] - cnt);
-                c.h = hbase + hl;
-                lh = c.h - d.lo;
+                lh = sbase + hl;  // local slot
+                c.sg = d.lo + lh;
                 if (lh >= d.L) {
                     a.overflow = true;
                 } else {
@@ -1376,10 +1439,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                         c.s.pops = opaque(q == 0 ? pre_a0.y : pre_a1.y);
                         c.s.digest = opaque(q == 0 ? pre_b0.x : pre_b1.x);
                         c.s.evc = opaque(q == 0 ? pre_b0.y : pre_b1.y);
-                        c.vh = opaque(q == 0 ? pre_v0 : pre_v1);
+                        c.h = opaque(q == 0 ? pre_s0.x : pre_s1.x);
+                        c.vh = opaque(q == 0 ? pre_s0.y : pre_s1.y);
                     } else {
                         c.s = d.hs[lh];
-                        c.vh = d.hinfo[c.h].vertex;
+                        const SlotInfo si = d.sinfo[lh];
+                        c.h = si.h;
+                        c.vh = si.v;
                     }
                     s_vh[j] = c.vh;
                     ++a.ctr[C_ACTIVE];
@@ -1456,11 +1522,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             // branch around it and wait for it before the next one
                             const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
                             uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
-                            if (d.dst_exact) {  // launch-uniform: one 2-byte read per send
-                                vd0 = d.vtab16[g0];
-                                vd1 = d.vtab16[g1];
-                                dst0 = g0;
-                                dst1 = g1;
+                            if constexpr (EXACT) {  // one 4-byte read per send: vertex and slot
+                                const uint32_t w0 = d.vs32[g0], w1 = d.vs32[g1];
+                                vd0 = w0 >> d.slot_bits;
+                                vd1 = w1 >> d.slot_bits;
+                                dst0 = w0 & ((1u << d.slot_bits) - 1);
+                                dst1 = w1 & ((1u << d.slot_bits) - 1);
                             } else {
                                 const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
                                 dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
@@ -1468,8 +1535,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             }
                             if (st0) stamp[17] = wait_stamp();
                             asm volatile("" ::: "memory");  // both pair loads after both resolves
-                            const PairRec pr0 = load_pair(d, c.vh, vd0, want_jump);
-                            const PairRec pr1 = load_pair(d, c.vh, vd1, want_jump);
+                            const PairRec pr0 = pair_of(c.vh, vd0, want_jump);
+                            const PairRec pr1 = pair_of(c.vh, vd1, want_jump);
                             if (st0) stamp[18] = wait_stamp();
                             if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, vd0, pr0, count_local);
                             if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, vd1, pr1, count_local);
@@ -1485,10 +1552,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 }
             }
             if (st0) stamp[10] = wait_stamp();
-            const uint32_t base = wave_reserve(&s_nsend, ns);  // wave converged here
+            // a header record {evc, HDR | host} then the sends: phase C needs no
+            // state load
+            const uint32_t base = wave_reserve(&s_nsend, go ? ns + 1 : 0u);  // wave converged here
             if (st0) stamp[11] = wait_stamp();
             if (!go) continue;
-            if (base + ns > d.ECAP) {
+            if (base + ns + 1 > d.ECAP) {
                 a.overflow = true;
                 continue;
             }
@@ -1498,7 +1567,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             s_sb[j] = base;
             s_vh[j] = c.vh | (ns << 16);
-            uint32_t k = base;
+            snd[base] = Rec{c.s.evc, HDR_REC | c.h};
+            uint32_t k = base + 1;
             pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
                 snd[k++] = Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
             });
@@ -1514,7 +1584,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- phase B: one lane per send, two in flight
+    // ---- phase B: one lane per send, two in flight (header records skipped)
     const uint32_t nsend = s_nsend < d.ECAP ? s_nsend : d.ECAP;
     for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
         const uint32_t i1 = i0 + K2_T;
@@ -1524,11 +1594,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
         uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
-        if (d.dst_exact) {
-            vd0 = d.vtab16[g0];
-            vd1 = d.vtab16[g1];
-            dst0 = g0;
-            dst1 = g1;
+        if constexpr (EXACT) {
+            const uint32_t w0 = d.vs32[g0], w1 = d.vs32[g1];
+            vd0 = w0 >> d.slot_bits;
+            vd1 = w1 >> d.slot_bits;
+            dst0 = w0 & ((1u << d.slot_bits) - 1);
+            dst1 = w1 & ((1u << d.slot_bits) - 1);
         } else {
             const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
             dst0 = dst_resolve(d, x0, g0, pb0, vd0);
@@ -1536,9 +1607,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
         const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
-        const PairRec pr0 = load_pair(d, s_vh[j0] & 0xFFFFu, vd0, want_jump);
-        const PairRec pr1 = load_pair(d, s_vh[j1] & 0xFFFFu, vd1, want_jump);
-        {
+        const PairRec pr0 = pair_of(s_vh[j0] & 0xFFFFu, vd0, want_jump);
+        const PairRec pr1 = pair_of(s_vh[j1] & 0xFFFFu, vd1, want_jump);
+        if (!(r0.k & HDR_REC)) {
             const uint64_t bt = S + (r0.a & M52);
             const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
             a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
@@ -1546,7 +1617,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
             snd[i0] = Rec{((uint64_t)keep << 63) | (bt + pr0.delay - S), dst0};  // worker.c:275-277
         }
-        if (v1) {
+        if (v1 && !(r1.k & HDR_REC)) {
             const uint64_t bt = S + (r1.a & M52);
             const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
             a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
@@ -1565,14 +1636,21 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if (j >= nact) break;
         const uint32_t sb = s_sb[j];
         if (sb == UINT32_MAX) continue;
-        const uint32_t h = hbase + s_act[j];
+        const uint32_t ls = sbase + s_act[j];  // local slot
+        const uint32_t sg = d.lo + ls;
         const uint32_t ns = s_vh[j] >> 16;
-        uint64_t evc = d.hs[h - d.lo].evc;  // untouched by phase A on this path
+        // the header and the first four sends in flight together (clamped
+        // addresses: with no send the header is read twice)
+        const uint32_t k0 = sb + 1, klast = sb + ns;
         Rec rq[4];
-        const uint32_t klast = sb + ns - 1;
-        for (uint32_t k = sb; k < sb + ns; ++k) {
-            const uint32_t u = (k - sb) & 3u;
-            if (u == 0) {  // the next four records in flight together (clamped addresses)
+        const Rec hd = snd[sb];
+#pragma unroll
+        for (uint32_t v = 0; v < 4; ++v) rq[v] = snd[k0 + v < klast ? k0 + v : klast];
+        uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
+        const uint32_t h = (uint32_t)hd.k;
+        for (uint32_t k = k0; k <= klast; ++k) {
+            const uint32_t u = (k - k0) & 3u;
+            if (u == 0 && k != k0) {  // the next four records in flight together
 #pragma unroll
                 for (uint32_t v = 0; v < 4; ++v) rq[v] = snd[k + v < klast ? k + v : klast];
             }
@@ -1588,14 +1666,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 continue;
             }
             const uint32_t dst = (uint32_t)r.k;
-            if (dst == h && tn < E) a.overflow = true;  // excluded by the phase A test
-            if (dst != h && tn < E) {               // host_single.c:180-184
+            if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
+            if (dst != sg && tn < E) {              // host_single.c:180-184
                 tn = E;
                 ++a.ctr[C_BUMPED];
             }
             if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
         }
-        d.hs[h - d.lo].evc = evc;
+        d.hs[ls].evc = evc;
     }
     __syncthreads();  // staging done: sh.nloc final, bins complete
     if (d.outn) {
@@ -2431,6 +2509,7 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
 struct sg_engine {
     sg_phold_params p;
     Dev d;
+    std::vector<uint32_t> host_of_slot;  // local slot -> registration index
     int device;
     hipStream_t stream;
     bool own_stream;
@@ -2692,11 +2771,59 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
         return SG_ERR_INVAL;
     }
+    // Slots: every shard's hosts in (vertex, index) order.  Every shard knows
+    // every host's global slot (the destination of a send is a slot).
+    for (size_t i = 0; i < p.n_hosts; ++i)
+        if (t->host_vertex[i] >= d.V) {
+            sg_set_error("sg_engine_create: host %zu attached to vertex %u >= %u", i, t->host_vertex[i], d.V);
+            return SG_ERR_INVAL;
+        }
+    std::vector<uint32_t> slot_of(p.n_hosts), host_of_slot(d.L);
+    {
+        std::vector<uint32_t> ord;
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t b0 = d.bounds[g], b1 = d.bounds[g + 1];
+            ord.resize(b1 - b0);
+            for (uint32_t i = 0; i < b1 - b0; ++i) ord[i] = b0 + i;
+            std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+                return t->host_vertex[x] < t->host_vertex[y];
+            });
+            for (uint32_t i = 0; i < b1 - b0; ++i) {
+                slot_of[ord[i]] = b0 + i;
+                if (g == d.g) host_of_slot[i] = ord[i];
+            }
+        }
+    }
+    // path-record format: delays below 2^32 ns fit the narrow records
+    uint64_t max_delay_all = 0, gjmin = UINT64_MAX;
+    bool all_keep = true;
+    for (size_t i = 0; i < VV; ++i) {
+        max_delay_all = std::max<uint64_t>(max_delay_all, t->delay_ns[i]);
+        gjmin = std::min<uint64_t>(gjmin, t->jump_ms[i]);
+        all_keep &= t->keep_max[i] >= SG_RAND_MAX;
+    }
+    d.pair_fmt = max_delay_all >> 32 ? PAIR_WIDE : all_keep ? PAIR_DELAY : PAIR_NARROW;
+    {
+        const uint32_t fmt_env = env_u32z("SG_PAIR_FMT", 99);  // debugging: force a wider format
+        if (fmt_env < d.pair_fmt) d.pair_fmt = fmt_env;
+    }
+    // a partition's path rows in LDS when they fit (vertex span x V records)
+    d.rows_max = 0;
+    for (uint32_t q = 0; q < d.P; ++q) {
+        const uint32_t s0 = q * d.HP, s1 = std::min<uint32_t>(d.L, s0 + d.HP);
+        const uint32_t nrow = t->host_vertex[host_of_slot[s1 - 1]] - t->host_vertex[host_of_slot[s0]] + 1;
+        d.rows_max = std::max(d.rows_max, nrow);
+    }
+    const uint32_t resz = d.pair_fmt == PAIR_NARROW ? 8 : 4;
+    const uint64_t row_bytes = (uint64_t)d.rows_max * d.V * resz;
+    d.lds_rows = d.pair_fmt != PAIR_WIDE && row_bytes <= (32u << 10) && env_u32("SG_NO_LDS_ROWS", 0) == 0;
     // k_proc dynamic LDS: per-host arrays (18 B per host), the bucket bins
-    // (2 x R u32), then the event image (EVL due events, 16 B each).  Two
-    // workgroups per CU when there are more partitions than CUs.
+    // (2 x R u32), the partition's path rows, then the event image (EVL due
+    // events, 16 B each).  Two workgroups per CU when there are more
+    // partitions than CUs.
     d.bin_off = (d.HP * 18 + 15) & ~15u;
-    d.ev_off = d.bin_off + ((8 * d.R + 15) & ~15u);
+    d.row_off = d.bin_off + ((8 * d.R + 15) & ~15u);
+    d.ev_off = d.row_off + (d.lds_rows ? (uint32_t)((row_bytes + 15) & ~15ull) : 0u);
     {
         uint32_t wgs = d.P > 256 ? 2 : 1, evl = 0;
         for (;;) {
@@ -2739,22 +2866,15 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }                                              \
     } while (0)
     HostInfo* hinfo;
-    uint16_t* vtab16 = nullptr;
+    uint32_t* vs32 = nullptr;
+    SlotInfo* sinfo;
     PairRec* pairs = nullptr;
     uint2* pairs8 = nullptr;
     uint32_t *pdelay = nullptr, *pjump = nullptr;
     ALLOC(hinfo, N);
-    // path-record format: delays below 2^32 ns fit the narrow records
-    uint64_t max_delay_all = 0, gjmin = UINT64_MAX;
-    bool all_keep = true;
-    for (size_t i = 0; i < VV; ++i) {
-        max_delay_all = std::max<uint64_t>(max_delay_all, t->delay_ns[i]);
-        gjmin = std::min<uint64_t>(gjmin, t->jump_ms[i]);
-        all_keep &= t->keep_max[i] >= SG_RAND_MAX;
-    }
-    D.pair_fmt = max_delay_all >> 32 ? PAIR_WIDE : all_keep ? PAIR_DELAY : PAIR_NARROW;
-    const uint32_t fmt_env = env_u32z("SG_PAIR_FMT", 99);  // debugging: force a wider format
-    if (fmt_env < D.pair_fmt) D.pair_fmt = fmt_env;
+    ALLOC(sinfo, L);
+    D.sinfo = sinfo;
+    e->host_of_slot = host_of_slot;
     D.gjmin = gjmin;
     bool sym = D.pair_fmt != PAIR_WIDE && env_u32("SG_NO_TRI", 0) == 0;
     for (size_t a = 0; sym && a < D.V; ++a)
@@ -2775,6 +2895,13 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.pairs8 = pairs8;
     D.pdelay = pdelay;
     D.pjump = pjump;
+    void* prow = nullptr;
+    if (D.lds_rows) {
+        unsigned char* pr_ = nullptr;
+        ALLOC(pr_, VV * resz);
+        prow = pr_;
+    }
+    D.prow = prow;
     uint64_t* vself;
     ALLOC(vself, D.V);
     D.hinfo = hinfo;
@@ -2806,8 +2933,16 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }
         D.dst_exact = ok ? 1 : 0;
     }
-    if (D.dst_exact) ALLOC(vtab16, N);
-    D.vtab16 = vtab16;
+    // vertex and global slot in one word
+    D.slot_bits = 1;
+    while (D.slot_bits < 32 && (1ull << D.slot_bits) < N) ++D.slot_bits;
+    {
+        uint32_t vbits = 1;
+        while ((1ull << vbits) < D.V) ++vbits;
+        if (D.slot_bits + vbits > 32) D.dst_exact = 0;  // the probe path carries slots instead
+    }
+    if (D.dst_exact) ALLOC(vs32, N);
+    D.vs32 = vs32;
     D.pairs = pairs;
     D.vself = vself;
     ALLOC(D.hs, L);
@@ -2872,11 +3007,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     for (size_t i = 0; i < N; ++i) {
         hi[i].vertex = t->host_vertex[i];
         hi[i].wt = t->weight_thresh ? t->weight_thresh[i] : 0;
-        if (hi[i].vertex >= D.V) {
-            sg_engine_destroy(e);
-            sg_set_error("sg_engine_create: host %zu attached to vertex %u >= %u", i, hi[i].vertex, D.V);
-            return SG_ERR_INVAL;
-        }
+        hi[i].slot = slot_of[i];
+        hi[i].pad = 0;
     }
     std::vector<PairRec> pr(D.pair_fmt == PAIR_WIDE ? VV : 0);
     std::vector<uint2> pr8(D.pair_fmt == PAIR_NARROW ? NT : 0);
@@ -2893,18 +3025,35 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     std::vector<uint64_t> vs(D.V);
     for (size_t v = 0; v < D.V; ++v) vs[v] = t->delay_ns[v * D.V + v];
     std::vector<HostState> hs(L);
-    for (size_t i = 0; i < L; ++i) hs[i] = HostState{t->host_rng[D.lo + i], 0, 0, 0, 0};  // evc 0 until boot
+    std::vector<SlotInfo> si(L);
+    for (size_t i = 0; i < L; ++i) {
+        const uint32_t h = host_of_slot[i];
+        hs[i] = HostState{t->host_rng[h], 0, 0, 0, 0};  // evc 0 until boot
+        si[i] = SlotInfo{h, t->host_vertex[h]};
+    }
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
-    if (vtab16) {
-        std::vector<uint16_t> vt(N);
-        for (size_t i = 0; i < N; ++i) vt[i] = (uint16_t)hi[i].vertex;
-        err = err != hipSuccess ? err : hipMemcpy(vtab16, vt.data(), N * 2, hipMemcpyHostToDevice);
+    err = err != hipSuccess ? err : hipMemcpy(sinfo, si.data(), L * sizeof(SlotInfo), hipMemcpyHostToDevice);
+    if (vs32) {
+        std::vector<uint32_t> vt(N);
+        for (size_t i = 0; i < N; ++i) vt[i] = (hi[i].vertex << D.slot_bits) | slot_of[i];
+        err = err != hipSuccess ? err : hipMemcpy(vs32, vt.data(), N * 4, hipMemcpyHostToDevice);
     }
     if (pairs) err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
     if (pairs8) err = err != hipSuccess ? err : hipMemcpy(pairs8, pr8.data(), NT * sizeof(uint2), hipMemcpyHostToDevice);
     if (pdelay) err = err != hipSuccess ? err : hipMemcpy(pdelay, pd.data(), NT * 4, hipMemcpyHostToDevice);
     if (pjump) err = err != hipSuccess ? err : hipMemcpy(pjump, pj.data(), NT * 4, hipMemcpyHostToDevice);
+    if (prow) {  // full row-major copy for k_proc's LDS rows
+        if (D.pair_fmt == PAIR_NARROW) {
+            std::vector<uint2> f(VV);
+            for (size_t i = 0; i < VV; ++i) f[i] = make_uint2((uint32_t)t->delay_ns[i], (uint32_t)t->keep_max[i]);
+            err = err != hipSuccess ? err : hipMemcpy(prow, f.data(), VV * 8, hipMemcpyHostToDevice);
+        } else {
+            std::vector<uint32_t> f(VV);
+            for (size_t i = 0; i < VV; ++i) f[i] = (uint32_t)t->delay_ns[i];
+            err = err != hipSuccess ? err : hipMemcpy(prow, f.data(), VV * 4, hipMemcpyHostToDevice);
+        }
+    }
     err = err != hipSuccess ? err : hipMemcpy(vself, vs.data(), D.V * sizeof(uint64_t), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(D.hs, hs.data(), L * sizeof(HostState), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemset(D.rs, 0, sizeof(RoundState));
@@ -2968,7 +3117,10 @@ int sg_engine_boot(sg_engine* e) {
     }
     HIPCHK(hipSetDevice(e->device));
     const Dev& d = e->d;
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)d.R * d.NCH * sizeof(uint32_t), e->stream));
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
@@ -2985,7 +3137,11 @@ int sg_engine_boot(sg_engine* e) {
 static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
     return timed_launch(e, SG_K_PROCESS, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_proc, dim3(d.P), dim3(K2_T), d.proc_lds, e->stream, a, b, d);
+        const dim3 g(d.P), t(K2_T);
+        if (d.dst_exact && d.lds_rows) SG_LAUNCH((k_proc<true, true>), g, t, d.proc_lds, e->stream, a, b, d);
+        else if (d.dst_exact) SG_LAUNCH((k_proc<true, false>), g, t, d.proc_lds, e->stream, a, b, d);
+        else if (d.lds_rows) SG_LAUNCH((k_proc<false, true>), g, t, d.proc_lds, e->stream, a, b, d);
+        else SG_LAUNCH((k_proc<false, false>), g, t, d.proc_lds, e->stream, a, b, d);
     });
 }
 
@@ -3177,11 +3333,12 @@ int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops, uint32_
     HIPCHK(hipMemcpyAsync(hs.data(), e->d.hs, L * sizeof(HostState), hipMemcpyDeviceToHost, e->stream));
     int rc = sg_engine_sync(e);
     if (rc) return rc;
-    for (size_t i = 0; i < L; ++i) {
-        if (digest) digest[i] = hs[i].digest;
-        if (pops) pops[i] = hs[i].pops;
-        if (rng) rng[i] = hs[i].rng;
-        if (event_counter) event_counter[i] = hs[i].evc;
+    for (size_t sl = 0; sl < L; ++sl) {  // slots back to registration order
+        const size_t i = e->host_of_slot[sl] - e->d.lo;
+        if (digest) digest[i] = hs[sl].digest;
+        if (pops) pops[i] = hs[sl].pops;
+        if (rng) rng[i] = hs[sl].rng;
+        if (event_counter) event_counter[i] = hs[sl].evc;
     }
     return SG_OK;
 }

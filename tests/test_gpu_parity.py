@@ -267,3 +267,17 @@ def test_gather_grid(grid, monkeypatch):
     cfg = phold.c4_config(n_hosts=20_000)
     eng, orc = _run_both(cfg, max_rounds=40)
     _assert_same(eng, orc)
+
+
+@pytest.mark.parametrize("no_rows", [0, 1])
+def test_lds_path_rows_switch(no_rows, monkeypatch):
+    """Hosts sit in vertex-sorted slots, so a k_proc partition's path records
+    are staged in LDS; SG_NO_LDS_ROWS=1 reads them from HBM instead.  Both,
+    on a lossy topology (8-byte records) and configs[3]'s (4-byte), must
+    give the same bits."""
+    if no_rows:
+        monkeypatch.setenv("SG_NO_LDS_ROWS", "1")
+    for cfg in (phold.lossy_config(n_hosts=30_000, V=64, end_time_s=0.3),
+                phold.c4_config(n_hosts=50_000, V=256, end_time_s=0.2)):
+        eng, orc = _run_both(cfg, max_rounds=60)
+        _assert_same(eng, orc)
