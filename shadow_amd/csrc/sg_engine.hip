@@ -2124,6 +2124,7 @@ struct PlanLds {
     uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
     uint32_t old[RMAX];  // count before this step's reservations: the slots already written
     uint32_t off[RMAX];  // allocation: first new chunk of each bucket in this launch's run
+    uint32_t own[RMAX];  // allocation: new chunk i's bucket | its index among the bucket's new ones << 12
     uint64_t mn[RMAX];
     uint32_t fr[PL_T];   // the free ring's first PL_T entries from the head, read at launch
 };
@@ -2214,6 +2215,33 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             s_m = m;
             s_j = j;
             s_ovf = ovf;
+        } else if (mode == 0) {
+            // the local MIN terms, accumulated by k_scatter's and k_proc's
+            // workgroups with device-scope atomics (reduce_local's terms);
+            // only this thread reads them, so it resets them too
+            const uint64_t cm = rs->xcarry, em = rs->xacc[0], jm = rs->xacc[1];
+            uint64_t m = cm < em ? cm : em;
+            m = rs->rmin < m ? rs->rmin : m;
+            s_m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+            s_j = rs->jmin < jm ? rs->jmin : jm;
+            s_ovf = rs->overflow;
+            rs->xcarry = UINT64_MAX;
+            rs->xacc[0] = UINT64_MAX;
+            rs->xacc[1] = UINT64_MAX;
+        }
+        // the next window (master.c:450-480), under the other threads' loads
+        if (mode == 1 && s_more) {  // drain step: same window, more exchange
+            rs->phase = 1;
+            rs->overflow |= s_ovf;
+        } else if (mode != 2) {
+            if (mode == 1) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
+            rs->phase = 0;
+            rs->jmin = s_j;
+            apply_window(d, s_m, s_j, ~s_ovf);
+            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
+            s_S = rs->S;
+            s_E = rs->E;
+            s_done = rs->done;
         }
     }
     // fold: each shard's range starts where the previous one's ends (k_scatter
@@ -2234,23 +2262,6 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             rc[q] = base;
         }
     }
-    uint64_t m = 0, j = 0, ovf = 0;
-    if (mode == 0) {
-        // the local MIN terms, accumulated by k_gather's and k_proc's
-        // workgroups with device-scope atomics (reduce_local's terms)
-        const uint64_t cm = rs->xcarry, em = rs->xacc[0], jm = rs->xacc[1];
-        m = cm < em ? cm : em;
-        m = rs->rmin < m ? rs->rmin : m;
-        m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
-        j = rs->jmin < jm ? rs->jmin : jm;
-        ovf = rs->overflow;
-        __syncthreads();  // every thread has read them before thread 0 resets them
-        if (tid == 0) {
-            rs->xcarry = UINT64_MAX;
-            rs->xacc[0] = UINT64_MAX;
-            rs->xacc[1] = UINT64_MAX;
-        }
-    }
     B.fr[tid] = fr0;
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
@@ -2265,13 +2276,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     }
     __syncthreads();
     PSTAMP(1);
-    if (mode == 1) {
-        m = s_m;
-        j = s_j;
-        ovf = s_ovf;
-    }
     const bool round_done = mode == 0 || (mode == 1 && !s_more);
-    if (mode == 1 && round_done && tid == 0) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
+    // listed: a new window (or the first one, at boot)
+    const bool list = mode == 2 || (round_done && !s_done);
     if (round_done) {
         // k_gather returned the window's chunks (not the retained bucket's) to
         // the ring behind the tail: take them, and reset the consumed buckets
@@ -2287,26 +2294,6 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         __syncthreads();
     }
     PSTAMP(2);
-    bool list = true;
-    if (mode == 1 && s_more) {  // drain step: same window, more exchange
-        list = false;
-        if (tid == 0) {
-            rs->phase = 1;
-            rs->overflow |= ovf;
-        }
-    } else if (round_done) {
-        if (tid == 0) {
-            rs->phase = 0;
-            rs->jmin = j;
-            apply_window(d, m, j, ~ovf);
-            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
-            s_S = rs->S;
-            s_E = rs->E;
-            s_done = rs->done;
-        }
-        __syncthreads();
-        list = !s_done;
-    }
     PSTAMP(4);
     // the new window's buckets (when listed): [nbS, nbL], nbL straddling E or not
     const uint64_t nbS = s_S / W, nbL = (s_E - 1) / W;
@@ -2336,10 +2323,15 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         }
         uint64_t total;
         uint64_t off = block_excl_scan(mine, s16, &total);
+        // new chunk i's owner: an LDS table when the run fits it (every steady
+        // round), else a bucket search per chunk (the boot round)
+        const bool table = total <= RMAX;
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;
             if (rb < R) B.off[rb] = (uint32_t)off;
+            if (table)
+                for (uint32_t k = 0; k < need[q]; ++k) B.own[off + k] = rb | (k << 12);
             off += need[q];
         }
         __syncthreads();
@@ -2347,14 +2339,23 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         const uint32_t give = (uint32_t)(total < avail ? total : avail);
         const uint32_t head_r = (uint32_t)(head % NCH);
         for (uint32_t i = tid; i < give; i += PL_T) {
-            uint32_t lo = 0, hi = R - 1;  // the last bucket whose run starts at or before i
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (B.off[mid] <= i) lo = mid; else hi = mid - 1;
+            uint32_t lo, k;
+            if (table) {
+                const uint32_t o = B.own[i];
+                lo = o & 0xFFFu;
+                k = o >> 12;
+            } else {
+                lo = 0;
+                uint32_t hi = R - 1;  // the last bucket whose run starts at or before i
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    if (B.off[mid] <= i) lo = mid; else hi = mid - 1;
+                }
+                k = i - B.off[lo];
             }
             const uint32_t pos = head_r + i;  // give <= NCH: one wrap at most
             const uint32_t id = i < PL_T ? B.fr[i] : d.fring[pos >= NCH ? pos - NCH : pos];
-            d.btab[(size_t)lo * NCH + B.nal[lo] + (i - B.off[lo])] = id;
+            d.btab[(size_t)lo * NCH + B.nal[lo] + k] = id;
         }
         __syncthreads();
 #pragma unroll
