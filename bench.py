@@ -35,14 +35,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = os.path.join(ROOT, "profiles", "r01", "bench_default", "pmc.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r02", "bench_default", "pmc.json")
 DOMINANT = "k_proc"
 
 
 def pmc_traffic(n_hosts):
+    """(corrected PMC bytes per launch of the dominant kernel, source) from the
+    committed profile of this workload, or (None, None)."""
     if n_hosts != 1_000_000 or not os.path.exists(PMC_JSON):
         return None, None
-    k = json.load(open(PMC_JSON))["kernels"].get(DOMINANT)
+    ks = json.load(open(PMC_JSON))["kernels"]
+    k = next((v for n, v in ks.items() if n == DOMINANT or n.startswith(DOMINANT + "<")), None)
     if not k:
         return None, None
     return k["traffic_bytes"], os.path.relpath(PMC_JSON, ROOT)

@@ -241,14 +241,15 @@ struct Dev {
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
-    const uint32_t* vs32;     // [N] vertex << slot_bits | global slot, when dst_exact
+    const uint2* nearw;       // [N + 1] {weight threshold, vertex << slot_bits | global slot}, when dst_near
     uint32_t slot_bits;
     const SlotInfo* sinfo;    // [L] per local slot
     uint32_t lds_rows;        // k_proc stages its partition's path rows in LDS
     const void* prow;         // [V][V] full row-major records (4 or 8 B) the rows are staged from
     uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
-    uint32_t dst_exact;       // the uniform-position guess is the drawn host for every x (host-checked)
+    uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
+                              // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
@@ -1205,9 +1206,18 @@ __device__ __forceinline__ PairRec lds_pair(const Dev& d, const unsigned char* r
     return pr;
 }
 
-// EXACT: d.dst_exact (a destination's vertex and slot are one 4-byte read per
-// send); the other instantiation resolves destinations through the weight
-// probes.  ROWS: d.lds_rows (path records from the partition's LDS rows).
+// A draw x whose host is its guess g or g + 1 (d.dst_near): a = record g,
+// b = record g + 1 (adjacent: one line); the first host with x <= threshold.
+__device__ __forceinline__ void near_resolve(const Dev& d, int32_t x, uint2 a, uint2 b, uint32_t& vd, uint32_t& dst) {
+    const bool first = d.dst_rule == SG_DST_UNIFORM_FLOOR || x <= (int32_t)a.x;
+    const uint32_t w = first ? a.y : b.y;
+    vd = w >> d.slot_bits;
+    dst = w & ((1u << d.slot_bits) - 1);
+}
+
+// EXACT: d.dst_near (a destination is two adjacent 8-byte records per send);
+// the other instantiation resolves destinations through the weight probes
+// (and bisection).  ROWS: d.lds_rows (path records from the partition's LDS rows).
 template <bool EXACT, bool ROWS>
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
@@ -1522,12 +1532,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             // branch around it and wait for it before the next one
                             const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
                             uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
-                            if constexpr (EXACT) {  // one 4-byte read per send: vertex and slot
-                                const uint32_t w0 = d.vs32[g0], w1 = d.vs32[g1];
-                                vd0 = w0 >> d.slot_bits;
-                                vd1 = w1 >> d.slot_bits;
-                                dst0 = w0 & ((1u << d.slot_bits) - 1);
-                                dst1 = w1 & ((1u << d.slot_bits) - 1);
+                            if constexpr (EXACT) {  // records g and g + 1: threshold, vertex, slot
+                                const uint2 a0 = d.nearw[g0], b0 = d.nearw[g0 + 1];
+                                const uint2 a1 = d.nearw[g1], b1 = d.nearw[g1 + 1];
+                                near_resolve(d, x0, a0, b0, vd0, dst0);
+                                near_resolve(d, x1, a1, b1, vd1, dst1);
                             } else {
                                 const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
                                 dst0 = nsd > 0 ? dst_resolve(d, x0, g0, pb0, vd0) : 0;
@@ -1595,11 +1604,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
         uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
         if constexpr (EXACT) {
-            const uint32_t w0 = d.vs32[g0], w1 = d.vs32[g1];
-            vd0 = w0 >> d.slot_bits;
-            vd1 = w1 >> d.slot_bits;
-            dst0 = w0 & ((1u << d.slot_bits) - 1);
-            dst1 = w1 & ((1u << d.slot_bits) - 1);
+            const uint2 a0 = d.nearw[g0], b0 = d.nearw[g0 + 1];
+            const uint2 a1 = d.nearw[g1], b1 = d.nearw[g1 + 1];
+            near_resolve(d, x0, a0, b0, vd0, dst0);
+            near_resolve(d, x1, a1, b1, vd1, dst1);
         } else {
             const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
             dst0 = dst_resolve(d, x0, g0, pb0, vd0);
@@ -2867,7 +2875,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }                                              \
     } while (0)
     HostInfo* hinfo;
-    uint32_t* vs32 = nullptr;
+    uint2* nearw = nullptr;
     SlotInfo* sinfo;
     PairRec* pairs = nullptr;
     uint2* pairs8 = nullptr;
@@ -2912,7 +2920,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // chains then overlap every other lane's instead of running after them
     D.light_q = env_u32z("SG_LIGHT_Q", 1);
     D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
-    D.dst_exact = 0;
+    // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
+    // must map to i - 1 or i under the (monotone) guess, so checking both ends
+    // suffices; the floor rule's guess is its answer
+    D.dst_near = 0;
     if (D.V <= 65536 && env_u32("SG_NO_EXACT_DST", 0) == 0) {
         bool ok = true;
         if (p.dst_rule == SG_DST_WEIGHTS) {
@@ -2920,19 +2931,20 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
                 const uint64_t g = ((uint64_t)x * N) >> 31;
                 return g >= N ? N - 1 : g;
             };
+            auto near = [&](uint64_t g, size_t i) { return g == i || g + 1 == i; };
             int64_t prev = -1;
             for (size_t i = 0; i < N && ok; ++i) {
                 const int64_t hi = t->weight_thresh ? t->weight_thresh[i] : 0;
                 if (hi > prev && hi >= 0) {
                     const int64_t lo = prev + 1 > 0 ? prev + 1 : 0;
                     const int64_t hc = hi < SG_RAND_MAX ? hi : SG_RAND_MAX;
-                    if (lo <= hc) ok = guess(lo) == i && guess(hc) == i;
+                    if (lo <= hc) ok = near(guess(lo), i) && near(guess(hc), i);
                 }
                 prev = hi > prev ? hi : prev;
             }
             ok = ok && t->weight_thresh != nullptr;
         }
-        D.dst_exact = ok ? 1 : 0;
+        D.dst_near = ok ? 1 : 0;
     }
     // vertex and global slot in one word
     D.slot_bits = 1;
@@ -2940,10 +2952,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     {
         uint32_t vbits = 1;
         while ((1ull << vbits) < D.V) ++vbits;
-        if (D.slot_bits + vbits > 32) D.dst_exact = 0;  // the probe path carries slots instead
+        if (D.slot_bits + vbits > 32) D.dst_near = 0;  // the probe path carries slots instead
     }
-    if (D.dst_exact) ALLOC(vs32, N);
-    D.vs32 = vs32;
+    if (D.dst_near) ALLOC(nearw, N + 1);
+    D.nearw = nearw;
     D.pairs = pairs;
     D.vself = vself;
     ALLOC(D.hs, L);
@@ -3035,10 +3047,12 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     hipError_t err = hipSuccess;
     err = err != hipSuccess ? err : hipMemcpy(hinfo, hi.data(), N * sizeof(HostInfo), hipMemcpyHostToDevice);
     err = err != hipSuccess ? err : hipMemcpy(sinfo, si.data(), L * sizeof(SlotInfo), hipMemcpyHostToDevice);
-    if (vs32) {
-        std::vector<uint32_t> vt(N);
-        for (size_t i = 0; i < N; ++i) vt[i] = (hi[i].vertex << D.slot_bits) | slot_of[i];
-        err = err != hipSuccess ? err : hipMemcpy(vs32, vt.data(), N * 4, hipMemcpyHostToDevice);
+    if (nearw) {
+        std::vector<uint2> vt(N + 1);
+        for (size_t i = 0; i < N; ++i)
+            vt[i] = make_uint2((uint32_t)hi[i].wt, (hi[i].vertex << D.slot_bits) | slot_of[i]);
+        vt[N] = vt[N - 1];  // read as record g + 1 of g = N - 1; never chosen (x > wt[N-1] has no host)
+        err = err != hipSuccess ? err : hipMemcpy(nearw, vt.data(), (N + 1) * sizeof(uint2), hipMemcpyHostToDevice);
     }
     if (pairs) err = err != hipSuccess ? err : hipMemcpy(pairs, pr.data(), VV * sizeof(PairRec), hipMemcpyHostToDevice);
     if (pairs8) err = err != hipSuccess ? err : hipMemcpy(pairs8, pr8.data(), NT * sizeof(uint2), hipMemcpyHostToDevice);
@@ -3139,8 +3153,8 @@ static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
     return timed_launch(e, SG_K_PROCESS, [&](hipEvent_t a, hipEvent_t b) {
         const dim3 g(d.P), t(K2_T);
-        if (d.dst_exact && d.lds_rows) SG_LAUNCH((k_proc<true, true>), g, t, d.proc_lds, e->stream, a, b, d);
-        else if (d.dst_exact) SG_LAUNCH((k_proc<true, false>), g, t, d.proc_lds, e->stream, a, b, d);
+        if (d.dst_near && d.lds_rows) SG_LAUNCH((k_proc<true, true>), g, t, d.proc_lds, e->stream, a, b, d);
+        else if (d.dst_near) SG_LAUNCH((k_proc<true, false>), g, t, d.proc_lds, e->stream, a, b, d);
         else if (d.lds_rows) SG_LAUNCH((k_proc<false, true>), g, t, d.proc_lds, e->stream, a, b, d);
         else SG_LAUNCH((k_proc<false, false>), g, t, d.proc_lds, e->stream, a, b, d);
     });
