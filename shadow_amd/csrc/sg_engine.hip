@@ -298,7 +298,8 @@ struct Dev {
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
-    uint64_t* stamps;         // [P][SG_STAMP_W] k_proc phase stamps + [SG_STAMP_W] k_plan's (SG_STAMPS=1), else null
+    uint64_t* stamps;         // [P][SG_STAMP_W] k_proc phase stamps + [SG_STAMP_W] k_plan's + one row
+                              // per k_scatter workgroup (SG_STAMPS=1), else null
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
@@ -735,7 +736,7 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
 // themselves, so the two never touch the same slot.
 constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8;
 template <int GT>
-__device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char* lds) {
+__device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char* lds, uint64_t* st) {
     constexpr int GR = 4 * (int)CH / GT;
     const RoundState* rs = d.rs;
     uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
@@ -780,6 +781,10 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
             free_chunk(de, c0 + threadIdx.x);
         }
         __syncthreads();
+        if (st) {
+            st[1] = __builtin_amdgcn_s_memrealtime();
+            st[5] = nb;
+        }
         const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
         Rec r[GR];
         uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
@@ -811,8 +816,10 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
             atomicAdd(&s_cnt[pp[q]], 1u);
         }
         __syncthreads();
+        if (st) st[2] = __builtin_amdgcn_s_memrealtime();
         reserve();
         __syncthreads();
+        if (st) st[6] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int q = 0; q < GR; ++q) {
             if (pp[q] == UINT32_MAX) continue;
@@ -1985,6 +1992,14 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     ro.S = rs->S;
     ro.E = rs->E;
     ro.ret = rs->ret_b;
+    // SG_STAMPS: {start, after setup, after the events, end, role, events}
+    uint64_t* st = d.stamps && threadIdx.x == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
+    if (st) {
+        st[0] = __builtin_amdgcn_s_memrealtime();
+        st[4] = blk == gridDim.x - 1 ? 3 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
+        st[1] = st[2] = st[3] = st[6] = st[0];
+        st[5] = 0;
+    }
     if (blk == gridDim.x - 1) {
         uint64_t* s16 = (uint64_t*)lds;
         if (ro.listed && d.outn && threadIdx.x < d.G) {  // the next step processes: outboxes refill
@@ -2009,11 +2024,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         if (threadIdx.x == 0) {
             rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : d.bmin[first % R];
             rs->rmin_todo = 0;
+            if (st) st[3] = __builtin_amdgcn_s_memrealtime();
         }
         return;
     }
     if (blk >= g0) {
-        if (ro.listed) gather_role<K3_T>(d, blk - g0, gridDim.x - 1 - g0, lds);
+        if (ro.listed) gather_role<K3_T>(d, blk - g0, gridDim.x - 1 - g0, lds, st);
+        if (st) st[3] = wait_stamp();
         return;
     }
     uint32_t* s_cur = (uint32_t*)lds;    // [RMAX] slot cursor per bucket
@@ -2030,25 +2047,35 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         const uint64_t S = rs->ins_S;
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
         const uint32_t* xo = d.bxoff + (size_t)(blk % XS) * R;
+        Rec r[SU];
         for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
         for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
         __syncthreads();
+        if (st) {
+            st[1] = __builtin_amdgcn_s_memrealtime();
+            st[5] = n;
+        }
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                r[q] = ld_stream(&src[i < n ? i : 0]);
+            }
             bool v[SU];
             uint64_t t[SU], k[SU];
             uint32_t dl[SU];
 #pragma unroll
             for (int q = 0; q < SU; ++q) {
-                const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                const Rec r = ld_stream(&src[i < n ? i : 0]);
-                v[q] = i < n;
-                t[q] = S + (r.a & M40);
-                k[q] = r.k;
-                dl[q] = (uint32_t)(r.a >> 40);
+                v[q] = i0 + threadIdx.x + q * K3_T < n;
+                t[q] = S + (r[q].a & M40);
+                k[q] = r[q].k;
+                dl[q] = (uint32_t)(r[q].a >> 40);
             }
             insert_batch(d, ro, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
+        if (st) st[2] = wait_stamp();
         insert_finish(d, ro, smin, ntomb, s16);
+        if (st) st[3] = wait_stamp();
         return;
     }
     // the received blocks' events, split evenly over G3 workgroups
@@ -2993,7 +3020,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
-    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (P + 1) * SG_STAMP_W);  // + k_plan's row
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (2 * P + D.G3 + D.G1 + 2) * SG_STAMP_W);  // + k_plan's, k_scatter's
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
@@ -3448,7 +3475,7 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
 
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
     if (!e) return SG_ERR_INVAL;
-    const uint64_t n = e->d.stamps ? ((uint64_t)e->d.P + 1) * SG_STAMP_W : 0;
+    const uint64_t n = e->d.stamps ? (2ull * e->d.P + e->d.G3 + e->d.G1 + 2) * SG_STAMP_W : 0;
     if (n_out) *n_out = n;
     if (out && capacity && n) {
         HIPCHK(hipStreamSynchronize(e->stream));

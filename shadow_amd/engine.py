@@ -168,8 +168,9 @@ class Engine:
         return g.as_dict()
 
     def stamps(self) -> np.ndarray:
-        """[P + 1, 32] k_proc phase stamps of the last round (SG_STAMPS=1), the last
-        row k_plan's, or empty."""
+        """[2P + G3 + G1 + 2, 32] stamps of the last round (SG_STAMPS=1): P rows of
+        k_proc phase stamps, k_plan's row, then one row per k_scatter workgroup
+        {start, setup, events, end, role, n}; or empty."""
         n = C.c_uint64()
         L.check(L.lib().sg_engine_stamps(self.h, None, 0, C.byref(n)))
         out = np.zeros(n.value, np.uint64)

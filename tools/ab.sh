@@ -15,5 +15,5 @@ for v in "$@"; do
 done
 if [ -n "$STAMPS" ]; then
   env ${STAMPS//,/ } timeout -k 10 120 python tools/stamps.py > gpurun_out/ab/stamps.log 2>&1 || exit 1
-  tail -11 gpurun_out/ab/stamps.log
+  tail -18 gpurun_out/ab/stamps.log
 fi

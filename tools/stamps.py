@@ -17,7 +17,8 @@ eng.run(40)
 for r in range(3):
     eng.run(1)
     st_all = eng.stamps().astype(np.int64)
-    st, pl = st_all[:-1], st_all[-1]
+    P = eng.geometry()["partitions"]
+    st, pl, sc = st_all[:P], st_all[P], st_all[P + 1:]
     t0 = st[:, 0].min()
     ph = np.diff(st[:, :5], axis=1) * 10 / 1e3  # us (100 MHz ticks)
     print(f"round +{r}: kernel span {(st[:, 4].max() - t0) / 100:.1f} us; WG start spread "
@@ -45,3 +46,19 @@ for r in range(3):
     d = np.diff(pl[:8]) / 100
     print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
           "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
+    sc = sc[sc[:, 0] > 0]
+    s0 = sc[:, 0].min()
+    print(f"   k_scatter: span {(sc[:, 3].max() - s0) / 100:.1f} us, WG start spread {(sc[:, 0].max() - s0) / 100:.1f} us")
+    for role, nm in enumerate(["insert", "received", "gather", "rmin"]):
+        x = sc[sc[:, 4] == role]
+        if not len(x):
+            continue
+        print(f"     {nm:<9} {len(x):4d} WGs  start med {np.median(x[:, 0] - s0) / 100:6.2f}  "
+              f"setup {np.median(x[:, 1] - x[:, 0]) / 100:5.2f}  events {np.median(x[:, 2] - x[:, 1]) / 100:5.2f}  "
+              f"finish {np.median(x[:, 3] - x[:, 2]) / 100:5.2f}  end med {np.median(x[:, 3] - s0) / 100:6.2f} "
+              f"max {(x[:, 3].max() - s0) / 100:6.2f}  n med {np.median(x[:, 5]):.0f}")
+    x = sc[sc[:, 4] == 2]
+    if len(x):
+        q = np.diff(x[:, [0, 1, 2, 6, 3]], axis=1) / 100
+        print("     gather (median us): rs+due loads %.2f  pool loads+count %.2f  reserve %.2f  scatter %.2f" % tuple(np.median(q, axis=0)),
+              " chunks/WG med", np.median(x[:, 5]))
