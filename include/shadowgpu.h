@@ -184,8 +184,12 @@ int sg_graph_attach(const sg_graph* g, uint32_t n_hosts, const sg_attach_hint* h
  * latency for direct and self paths, the minimum over all the source's stored
  * paths for shortest paths (one source run caches every attached target).
  * attached (V flags, NULL = all) selects the shortest-path targets
- * (_topology_getUniqueVertexTargets).  Reverse-direction cache hits of
- * undirected incomplete graphs (topology.c:1986-1990) are not modelled. */
+ * (_topology_getUniqueVertexTargets).  The reference's cache makes
+ * incomplete graphs order-dependent (a reverse-direction hit, topology.c:
+ * 1986-1990, runs no Dijkstra; directed graphs can get the reverse path,
+ * topology.c:1312-1318 / 2034-2036): this is its value when every lookup's
+ * source runs its own Dijkstra first.  tests/test_topology_cache_order.py
+ * models the cache and shows the cases.  Complete graphs are exact. */
 int sg_graph_paths(const sg_graph* g, const uint8_t* attached, double* latency_ms,
                    double* reliability, double* discovered_ms, uint8_t* kind);
 
