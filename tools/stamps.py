@@ -62,3 +62,12 @@ for r in range(3):
         q = np.diff(x[:, [0, 1, 2, 6, 3]], axis=1) / 100
         print("     gather (median us): rs+due loads %.2f  pool loads+count %.2f  reserve %.2f  scatter %.2f" % tuple(np.median(q, axis=0)),
               " chunks/WG med", np.median(x[:, 5]))
+    dur = (st[:, 4] - st[:, 0]) / 100
+    print("   k_proc WG duration: median %.2f  p90 %.2f  max %.2f us; end offsets median %.2f max %.2f"
+          % (np.median(dur), np.percentile(dur, 90), dur.max(), np.median(st[:, 4] - t0) / 100, (st[:, 4].max() - t0) / 100))
+    for nm, col in (("due", 5), ("active", 6), ("sends", 7)):
+        print(f"     corr(duration, {nm}) = {np.corrcoef(dur, st[:, col])[0, 1]:.2f}")
+    top = np.argsort(-(st[:, 4] - t0))[:6]
+    for w in top:
+        print("     slow WG %3d end %.2f start %.2f dur %.2f  phases %s  due/active/sends %s" % (
+            w, (st[w, 4] - t0) / 100, (st[w, 0] - t0) / 100, dur[w], np.round(ph[w], 2), st[w, 5:8]))
