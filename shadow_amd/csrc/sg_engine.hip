@@ -247,6 +247,7 @@ struct Dev {
     uint32_t lds_rows;        // k_proc stages its partition's path rows in LDS
     const void* prow;         // [V][V] full row-major records (4 or 8 B) the rows are staged from
     uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
+    bool snd_lds;                // k_proc's send records in LDS while they fit
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
@@ -1104,17 +1105,6 @@ __device__ __forceinline__ void sort_segment(Rec* seg, uint32_t cnt) {
     }
 }
 
-__device__ __forceinline__ Rec opaque_rec(const Rec (&rq)[4], uint32_t u) {
-    // a select of values (not of addresses: rq stays in registers)
-    uint64_t a = rq[0].a, k = rq[0].k;
-    a = u == 1 ? rq[1].a : a;
-    k = u == 1 ? rq[1].k : k;
-    a = u == 2 ? rq[2].a : a;
-    k = u == 2 ? rq[2].k : k;
-    a = u == 3 ? rq[3].a : a;
-    k = u == 3 ? rq[3].k : k;
-    return Rec{opaque(a), opaque(k)};
-}
 // Diagnostics (SG_STAMPS): a timestamp once this wave's outstanding memory
 // operations have landed.
 constexpr uint32_t SG_STAMP_W = 32;  // stamp slots per workgroup row
@@ -1412,6 +1402,16 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     a.overflow = false;
     Rec* xs = d.extras + ((size_t)p * K2_T + tid) * XCAP;
     Rec* snd = d.sends + (size_t)p * d.ECAP;
+    // Send records (phase A writes, phase B resolves, phase C commits) live in
+    // the event image's unused tail while they fit, in HBM beyond it: phases
+    // B and C then read them at LDS latency.
+    Rec* s_snd = s_ev + (in_lds ? n : 0u);
+    const uint32_t lcap = d.snd_lds ? (in_lds ? d.EVL - n : d.EVL) : 0u;
+    auto sget = [&](uint32_t i) __attribute__((always_inline)) { return i < lcap ? s_snd[i] : snd[i]; };
+    auto sput = [&](uint32_t i, const Rec& r) __attribute__((always_inline)) {
+        if (i < lcap) s_snd[i] = r;
+        else snd[i] = r;
+    };
     const int32_t last = s_last;
 
     // ---- phase A (segments in LDS or in part2: two instantiations)
@@ -1583,10 +1583,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             s_sb[j] = base;
             s_vh[j] = c.vh | (ns << 16);
-            snd[base] = Rec{c.s.evc, HDR_REC | c.h};
+            sput(base, Rec{c.s.evc, HDR_REC | c.h});
             uint32_t k = base + 1;
             pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
-                snd[k++] = Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)};
+                sput(k++, Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
             });
             // {rng, pops, digest} now; evc after phase C
             HostState* hp = d.hs + lh;
@@ -1605,8 +1605,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
         const uint32_t i1 = i0 + K2_T;
         const bool v1 = i1 < nsend;
-        const Rec r0 = snd[i0];
-        const Rec r1 = snd[v1 ? i1 : i0];  // an address select, not a conditional load
+        const Rec r0 = sget(i0);
+        const Rec r1 = sget(v1 ? i1 : i0);  // an index select, not a conditional load
         const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
         const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
         uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
@@ -1630,7 +1630,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
             const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
             if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
-            snd[i0] = Rec{((uint64_t)keep << 63) | (bt + pr0.delay - S), dst0};  // worker.c:275-277
+            const uint64_t rel = bt + pr0.delay - S;  // worker.c:275-277
+            if (rel >> 40) a.overflow = true;
+            sput(i0, Rec{((uint64_t)keep << 63) | ((uint64_t)j0 << 40) | rel, dst0});
         }
         if (v1 && !(r1.k & HDR_REC)) {
             const uint64_t bt = S + (r1.a & M52);
@@ -1638,57 +1640,47 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
             const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
             if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1], 1u);
-            snd[i1] = Rec{((uint64_t)keep << 63) | (bt + pr1.delay - S), dst1};
+            const uint64_t rel = bt + pr1.delay - S;
+            if (rel >> 40) a.overflow = true;
+            sput(i1, Rec{((uint64_t)keep << 63) | ((uint64_t)j1 << 40) | rel, dst1});
         }
     }
     __syncthreads();
     if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- phase C: hosts with phase B sends, per host in send order
-#pragma unroll 1
-    for (uint32_t q = 0; q < HPT; ++q) {
-        const uint32_t j = tid + q * K2_T;
-        if (j >= nact) break;
-        const uint32_t sb = s_sb[j];
-        if (sb == UINT32_MAX) continue;
-        const uint32_t ls = sbase + s_act[j];  // local slot
-        const uint32_t sg = d.lo + ls;
-        const uint32_t ns = s_vh[j] >> 16;
-        // the header and the first four sends in flight together (clamped
-        // addresses: with no send the header is read twice)
-        const uint32_t k0 = sb + 1, klast = sb + ns;
-        Rec rq[4];
-        const Rec hd = snd[sb];
-#pragma unroll
-        for (uint32_t v = 0; v < 4; ++v) rq[v] = snd[k0 + v < klast ? k0 + v : klast];
+    // ---- phase C: one lane per send record.  A send's srcHostEventID is its
+    // host's counter plus the kept sends before it in the host's order
+    // (worker.c:268-279, event.c:38): a short walk back over the host's
+    // records; then endTime drop, barrier bump, staging.
+    for (uint32_t i = tid; i < nsend; i += K2_T) {
+        const Rec r = sget(i);
+        if (r.k & HDR_REC) continue;  // a host's header
+        const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
+        const uint32_t sb = s_sb[j], ns = s_vh[j] >> 16;
+        const Rec hd = sget(sb);
         uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
-        const uint32_t h = (uint32_t)hd.k;
-        for (uint32_t k = k0; k <= klast; ++k) {
-            const uint32_t u = (k - k0) & 3u;
-            if (u == 0 && k != k0) {  // the next four records in flight together
-#pragma unroll
-                for (uint32_t v = 0; v < 4; ++v) rq[v] = snd[k + v < klast ? k + v : klast];
-            }
-            const Rec r = opaque_rec(rq, u);
-            if (!(r.a >> 63)) {
-                ++a.ctr[C_DROPREL];
-                continue;
-            }
-            const uint64_t sq = evc++;              // event.c:38
-            uint64_t tn = S + (r.a & M40);
-            if (tn >= d.end_time) {                 // scheduler.c:343-346
-                ++a.ctr[C_DROPEND];
-                continue;
-            }
-            const uint32_t dst = (uint32_t)r.k;
-            if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
-            if (dst != sg && tn < E) {              // host_single.c:180-184
-                tn = E;
-                ++a.ctr[C_BUMPED];
-            }
-            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
+        for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
+        const bool keep = (r.a >> 63) != 0;
+        if (i == sb + ns) d.hs[sbase + s_act[j]].evc = evc + keep;  // the host's last send
+        if (!keep) {
+            ++a.ctr[C_DROPREL];
+            continue;
         }
-        d.hs[ls].evc = evc;
+        const uint64_t sq = evc;                // event.c:38
+        uint64_t tn = S + (r.a & M40);
+        if (tn >= d.end_time) {                 // scheduler.c:343-346
+            ++a.ctr[C_DROPEND];
+            continue;
+        }
+        const uint32_t dst = (uint32_t)r.k;
+        const uint32_t sg = d.lo + sbase + s_act[j];
+        if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
+        if (dst != sg && tn < E) {              // host_single.c:180-184
+            tn = E;
+            ++a.ctr[C_BUMPED];
+        }
+        const uint32_t h = (uint32_t)hd.k;
+        if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
     }
     __syncthreads();  // staging done: sh.nloc final, bins complete
     if (d.outn) {
@@ -2796,6 +2788,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
     d.check = env_u32("SG_CHECK", 0) != 0;
+    d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
     // host partitions: HP hosts per k_proc workgroup (power of two), about
     // one partition per CU
     const uint32_t hp_env = env_u32("SG_HP", 0);
