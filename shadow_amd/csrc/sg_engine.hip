@@ -260,6 +260,7 @@ struct Dev {
     uint32_t tri;             // narrow tables hold the lower triangle only (symmetric paths)
     uint64_t gjmin;           // smallest discovered ms of any pair: jmin can fall no lower
     const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
+    uint64_t vself_min;       // their minimum: a window no longer than it has no same-round self event
     uint32_t* pcount;         // [V*V] path packet counters (topology.c:2053-2063), or null
     HostState* hs;            // [L]
     // calendar
@@ -1417,6 +1418,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // ---- phase A (segments in LDS or in part2: two instantiations)
     const uint64_t W = d.W, bS = rs->bS;
     const uint32_t bSr = (uint32_t)(bS % R);
+    const bool self_possible = E - S > d.vself_min;
     bool horizon = false;
     auto count_local = [&](uint64_t t) {  // one staged local event into the bucket bins
         const uint64_t b = t / W;
@@ -1466,11 +1468,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     }
                     s_vh[j] = c.vh;
                     ++a.ctr[C_ACTIVE];
-                    const uint64_t self_delay = d.vself[c.vh];
+                    // the vertex's self delay only when some vertex's could land
+                    // inside this window (uniform; never in steady C4 rounds)
+                    const uint64_t self_delay = self_possible ? d.vself[c.vh] : 0;
                     if (st0) stamp[8] = wait_stamp();
                     sort_segment(seg, cnt);  // pop order
                     if (st0) stamp[9] = wait_stamp();
-                    if (d.workload != SG_WORKLOAD_PHOLD || S + (seg[0].a & M52) + self_delay < E) {
+                    if (d.workload != SG_WORKLOAD_PHOLD ||
+                        (self_possible && S + (seg[0].a & M52) + self_delay < E)) {
                         // sequential body: a self event may land inside this window
                         uint32_t nx = 0;
                         auto append = [&](uint64_t trel, uint64_t key) -> bool {
@@ -3057,6 +3062,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     std::vector<uint64_t> vs(D.V);
     for (size_t v = 0; v < D.V; ++v) vs[v] = t->delay_ns[v * D.V + v];
+    D.vself_min = *std::min_element(vs.begin(), vs.end());
     std::vector<HostState> hs(L);
     std::vector<SlotInfo> si(L);
     for (size_t i = 0; i < L; ++i) {
