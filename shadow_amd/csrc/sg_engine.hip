@@ -1442,6 +1442,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             Rec* seg = nullptr;
             HostCtx c;
             const bool st0 = stamp && tid == 0 && q == 0;
+            if (stamp && tid == 0 && q == 1) stamp[23] = __builtin_amdgcn_s_memrealtime();
             if (j < nact) {
                 s_sb[j] = UINT32_MAX;
                 const uint32_t hl = s_act[j];
@@ -1577,6 +1578,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             // state load
             const uint32_t base = wave_reserve(&s_nsend, go ? ns + 1 : 0u);  // wave converged here
             if (st0) stamp[11] = wait_stamp();
+            if (stamp && tid == 0 && q == 1) stamp[25] = wait_stamp();
             if (!go) continue;
             if (base + ns + 1 > d.ECAP) {
                 a.overflow = true;
@@ -1598,10 +1600,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
             hp->digest = c.s.digest;
             if (st0) stamp[12] = wait_stamp();
+            if (stamp && tid == 0 && q == 1) stamp[24] = wait_stamp();
         }
     };
     if (in_lds) phase_a(std::true_type{});
     else phase_a(std::false_type{});
+    if (stamp && (tid & 63) == 0) stamp[26 + (tid >> 8)] = wait_stamp();  // waves 0, 4, 8, 12 done
     __syncthreads();
     if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
 

@@ -71,3 +71,12 @@ for r in range(3):
     for w in top:
         print("     slow WG %3d end %.2f start %.2f dur %.2f  phases %s  due/active/sends %s" % (
             w, (st[w, 4] - t0) / 100, (st[w, 0] - t0) / 100, dur[w], np.round(ph[w], 2), st[w, 5:8]))
+    q1 = st[:, 23] > 0
+    if q1.any():
+        x = st[q1]
+        print("   phase A second host (lane 0, median us): start %.2f after phase A start, reserve done +%.2f, record+store +%.2f"
+              % (np.median(x[:, 23] - x[:, 1]) / 100, np.median(x[:, 25] - x[:, 23]) / 100,
+                 np.median(x[:, 24] - x[:, 25]) / 100))
+    wend = (st[:, 26:30] - st[:, [1]]) / 100
+    print("   phase A end per wave 0/4/8/12 (median us after phase A start):", np.round(np.median(wend, axis=0), 2),
+          " barrier at %.2f" % np.median((st[:, 2] - st[:, 1]) / 100))
