@@ -248,7 +248,7 @@ struct Dev {
     const void* prow;         // [V][V] full row-major records (4 or 8 B) the rows are staged from
     uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
     bool snd_lds;                // k_proc's send records in LDS while they fit
-    uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts       // sends a host may have to run its body inline in phase A
+    uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
