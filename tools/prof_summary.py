@@ -89,6 +89,10 @@ def main():
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             js[k] = {"read_bytes": 2 * avg["FETCH_SIZE"] * 1024, "write_bytes": avg["WRITE_SIZE"] * 1024,
                      "traffic_bytes": (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024,
+                     # tools/calib_fetch.py on this pool: streaming 16-B reads are counted
+                     # at half their bytes, random narrow reads of distinct lines at 64 B
+                     # each (= the bytes fetched): FETCH_SIZE x1 bounds the reads below
+                     "traffic_bytes_lower": (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024,
                      "avg_ns": steady.get(k)}
     print("\n".join(out))
     if len(sys.argv) > 3:
@@ -96,7 +100,10 @@ def main():
         with open(sys.argv[3], "w") as f:
             json.dump({"source": d, "launches_averaged": last,
                        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts 128-B "
-                               "reads at 64 B); WRITE_SIZE as is; KiB -> bytes",
+                               "reads at 64 B); WRITE_SIZE as is; KiB -> bytes.  traffic_bytes_lower "
+                               "takes FETCH_SIZE as is: the calibration (tools/calib_fetch.py, "
+                               "profiles/r02/calib/) counts random narrow reads at the 64 B "
+                               "actually fetched, so x2 over-counts them",
                        "kernels": js}, f, indent=1)
 
 
