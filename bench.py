@@ -43,12 +43,12 @@ def pmc_traffic(n_hosts):
     """(corrected PMC bytes per launch of the dominant kernel, source) from the
     committed profile of this workload, or (None, None)."""
     if n_hosts != 1_000_000 or not os.path.exists(PMC_JSON):
-        return None, None
+        return None, None, None
     ks = json.load(open(PMC_JSON))["kernels"]
     k = next((v for n, v in ks.items() if n == DOMINANT or n.startswith(DOMINANT + "<")), None)
     if not k:
-        return None, None
-    return k["traffic_bytes"], os.path.relpath(PMC_JSON, ROOT)
+        return None, None, None
+    return k["traffic_bytes"], k.get("traffic_bytes_lower"), os.path.relpath(PMC_JSON, ROOT)
 ALG_BYTES_PER_EVENT = 64
 ALG_BYTES_PER_ACTIVE_HOST = 24
 
@@ -182,7 +182,8 @@ def run_single(args):
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(args.hosts)
+    traffic, traffic_lower, traffic_src = pmc_traffic(args.hosts)
+    kus = {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]}
     res = {
         "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
         "value": pops / dt,
@@ -205,12 +206,14 @@ def run_single(args):
                                  else "sg_engine_enqueue_rounds, eager launches"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_lower": traffic_lower,
                      "traffic_source": traffic_src,
                      "traffic_gbs": traffic / avg_launch_s / 1e9 if traffic and avg_launch_s else None,
                      "kernel": DOMINANT, "avg_launch_us": avg_launch_s * 1e6,
                      "alg_bytes_per_launch": per_launch_bytes,
                      "timing_rounds": kr,
-                     "kernel_us_per_round": {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]},
+                     "kernel_us_per_round": kus,
+                     "gaps_us_per_round": dt * 1e6 / args.steps - sum(kus.values()),
                      "timing_method": "HIP events as each launch's dispatch-packet timestamps "
                                       "(hipExtLaunchKernelGGL), rounds after the timed region; "
                                       "the rest of ms_per_step is launch gaps"},
