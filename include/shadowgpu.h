@@ -416,6 +416,20 @@ int sg_engine_set_timing_mask(sg_engine* e, uint32_t mask);
 int sg_engine_path_counters(sg_engine* e, int enable);
 int sg_engine_path_counts(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out);
 
+/* Barrier-idle timers: the Mode S counterpart of the per-worker GTimers that
+ * accumulate the wait at the execute-events barrier (scheduler.c:380-389;
+ * host_single's push/pop idle timers, scheduler_policy_host_single.c:36-37,
+ * 186-200, 242-245, have no counterpart: Mode S takes no locks).  The
+ * "worker" here is a host partition's k_proc workgroup: busy = its time from
+ * start to its last store, idle = from there to the end of the round's last
+ * partition, summed over the rounds since enable (a multi-shard step's wait
+ * in the collective is not included).  enable != 0 zeroes them; they cost
+ * one extra barrier per partition and a P-entry pass in k_plan, so they are
+ * off by default.  barrier_times copies P entries (n_out = P, or 0 while off). */
+int sg_engine_barrier_timers(sg_engine* e, int enable);
+int sg_engine_barrier_times(sg_engine* e, uint64_t* busy_ns, uint64_t* idle_ns, uint64_t capacity,
+                            uint64_t* n_out);
+
 /* ------------------------------------------------------------------------ */
 /* 3. The `gpu` SchedulerPolicy ("Mode P", the drop-in boundary)            */
 /* ------------------------------------------------------------------------ */

@@ -262,6 +262,8 @@ struct Dev {
     const uint64_t* vself;    // [V] self-path delay of each vertex (the pairs diagonal)
     uint64_t vself_min;       // their minimum: a window no longer than it has no same-round self event
     uint32_t* pcount;         // [V*V] path packet counters (topology.c:2053-2063), or null
+    uint64_t* wtime;          // [3][P] barrier timers (scheduler.c:380-389), or null: busy ticks,
+                              // idle ticks (waiting for the round's last partition), this round's end
     HostState* hs;            // [L]
     // calendar
     Rec* pool;                // [NCH][CH]
@@ -1248,6 +1250,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint32_t tid = threadIdx.x;
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
     for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
@@ -1792,6 +1795,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         stamp[6] = nact;
         stamp[7] = s_nsend;
     }
+    if (d.wtime) {  // this partition's busy time; k_plan charges the wait for the last one
+        __syncthreads();
+        if (tid == 0) {
+            const uint64_t t_end = wait_stamp();
+            d.wtime[p] += t_end - t_start;
+            d.wtime[2 * (size_t)d.P + p] = t_end;
+        }
+    }
 }
 
 // --------------------------------------------------------------- insert ----
@@ -2313,6 +2324,17 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     __syncthreads();
     PSTAMP(1);
     const bool round_done = mode == 0 || (mode == 1 && !s_more);
+    if (d.wtime && round_done) {
+        // barrier wait (scheduler.c:380-389): each partition idles from its end
+        // to the round's last partition end
+        uint64_t m = 0;
+        for (uint32_t p = tid; p < d.P; p += PL_T) {
+            const uint64_t t = d.wtime[2 * (size_t)d.P + p];
+            m = t > m ? t : m;
+        }
+        m = ~block_min(~m, s16);  // max; barriers inside
+        for (uint32_t p = tid; p < d.P; p += PL_T) d.wtime[(size_t)d.P + p] += m - d.wtime[2 * (size_t)d.P + p];
+    }
     // listed: a new window (or the first one, at boot)
     const bool list = mode == 2 || (round_done && !s_done);
     if (round_done) {
@@ -2553,6 +2575,7 @@ struct sg_engine {
     bool booted;
     std::vector<void*> allocs;
     uint32_t* pcount_buf = nullptr;  // path packet counters, once enabled
+    uint64_t* wtime_buf = nullptr;   // barrier timers, once enabled
     RoundState* h_rs;  // pinned
     unsigned long long* d_pend;
     bool timing;
@@ -3503,6 +3526,43 @@ int sg_engine_path_counters(sg_engine* e, int enable) {
     HIPCHK(hipMemsetAsync(e->pcount_buf, 0, VV * sizeof(uint32_t), e->stream));
     e->d.pcount = e->pcount_buf;
     e->gen++;
+    return SG_OK;
+}
+
+int sg_engine_barrier_timers(sg_engine* e, int enable) {
+    if (!e) return SG_ERR_INVAL;
+    HIPCHK(hipSetDevice(e->device));
+    if (!enable) {
+        e->d.wtime = nullptr;  // the buffer stays allocated until destroy
+        e->gen++;
+        return SG_OK;
+    }
+    const size_t n = 3 * (size_t)e->d.P;
+    if (!e->wtime_buf) {
+        int rc = dalloc(e, &e->wtime_buf, n);
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemsetAsync(e->wtime_buf, 0, n * sizeof(uint64_t), e->stream));
+    e->d.wtime = e->wtime_buf;
+    e->gen++;
+    return SG_OK;
+}
+
+int sg_engine_barrier_times(sg_engine* e, uint64_t* busy_ns, uint64_t* idle_ns, uint64_t capacity,
+                            uint64_t* n_out) {
+    if (!e) return SG_ERR_INVAL;
+    const uint64_t n = e->d.wtime ? e->d.P : 0;
+    if (n_out) *n_out = n;
+    if (capacity && n) {
+        const uint64_t m = n < capacity ? n : capacity;
+        std::vector<uint64_t> tmp(2 * (size_t)n);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(tmp.data(), e->d.wtime, 2 * n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < m; ++i) {  // s_memrealtime ticks at 100 MHz
+            if (busy_ns) busy_ns[i] = tmp[i] * 10;
+            if (idle_ns) idle_ns[i] = tmp[n + i] * 10;
+        }
+    }
     return SG_OK;
 }
 

@@ -137,6 +137,21 @@ class Engine:
         return {"event_new": new, "event_free": st["pops"] + st["drop_endtime"],
                 "event_live": st["pending"]}
 
+    def barrier_timers(self, enable: bool = True):
+        """Per-partition busy / barrier-idle time from now on (zeroed);
+        scheduler.c:380-389's per-worker wait timers, a partition's k_proc
+        workgroup as the worker."""
+        L.check(L.lib().sg_engine_barrier_timers(self.h, int(enable)))
+
+    def barrier_times(self) -> dict:
+        """{"busy_ns": [P], "idle_ns": [P]} since barrier_timers(True)."""
+        n = C.c_uint64()
+        L.check(L.lib().sg_engine_barrier_times(self.h, None, None, 0, C.byref(n)))
+        b, i = np.zeros(n.value, np.uint64), np.zeros(n.value, np.uint64)
+        if n.value:
+            L.check(L.lib().sg_engine_barrier_times(self.h, b.ctypes.data, i.ctypes.data, n.value, C.byref(n)))
+        return {"busy_ns": b, "idle_ns": i}
+
     def path_counts(self) -> np.ndarray:
         n = C.c_uint64()
         L.check(L.lib().sg_engine_path_counts(self.h, None, 0, C.byref(n)))
