@@ -393,7 +393,7 @@ enum sg_kernel_class {
     SG_K_PROCESS = 0,  /* k_proc: per-host pops + PHOLD body + send resolution */
     SG_K_INSERT = 1,   /* k_ins: new / received events into time buckets */
     SG_K_PLAN = 2,     /* k_plan (+ k_fill when sharded) */
-    SG_K_GATHER = 3,   /* k_gather: due chunks → host partitions */
+    SG_K_GATHER = 3,   /* unused: the gather is a k_scatter role now (class kept for ABI stability) */
     SG_K_EXCHANGE = 4, /* the step's RCCL all-to-all (sg_engine_run_steps): this shard's
                           wait for the slowest shard plus the transfer — the barrier
                           idle time of scheduler.c:380-389 */
