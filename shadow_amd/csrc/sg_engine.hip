@@ -2115,30 +2115,31 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
 
 // ----------------------------------------------------------------- plan ----
 // master_slaveFinishedCurrentRound (master.c:450-480) on a reduced triple.
-__device__ void apply_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t not_overflow) {
-    RoundState* rs = d.rs;
-    rs->overflow |= ~not_overflow;
-    if (d.wlog && rs->rounds < d.wlog_cap) {  // the window just executed
-        d.wlog[2 * rs->rounds] = rs->S;
-        d.wlog[2 * rs->rounds + 1] = rs->E;
-    }
-    rs->rounds += 1;
-    rs->last_min = minNext;
+struct Window {
+    uint64_t S, E, done, min_jump, next_min_jump;
+};
+// The next window from the global MIN and the discovery minimum (ms), given
+// the round state's jump fields (computed in registers; the caller stores).
+__device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t mj0, uint64_t nmj0) {
+    Window w;
+    w.next_min_jump = nmj0;
+    w.min_jump = mj0;
     uint64_t jump;
     if (d.window_rule == SG_WINDOW_FIXED) {
         jump = d.fixed_jump;
     } else {
-        if (jmin != UINT64_MAX) rs->next_min_jump = jmin * SG_ONE_MS;  // master.c:153
-        rs->min_jump = rs->next_min_jump;                            // master.c:459
-        jump = rs->min_jump > 0 ? rs->min_jump : 10 * SG_ONE_MS;     // master.c:137
+        if (jmin != UINT64_MAX) w.next_min_jump = jmin * SG_ONE_MS;  // master.c:153
+        w.min_jump = w.next_min_jump;                                // master.c:459
+        jump = w.min_jump > 0 ? w.min_jump : 10 * SG_ONE_MS;         // master.c:137
         if (d.runahead_min > 0 && jump < d.runahead_min) jump = d.runahead_min;
     }
     const uint64_t start = minNext;
     uint64_t end = minNext + jump;  // unsigned wrap as in the reference
     if (end > d.end_time) end = d.end_time;
-    rs->S = start;
-    rs->E = end;
-    rs->done = start < end ? 0 : 1;
+    w.S = start;
+    w.E = end;
+    w.done = start < end ? 0 : 1;
+    return w;
 }
 
 __device__ __forceinline__ void reset_bucket(const Dev& d, uint32_t rb) {
@@ -2218,6 +2219,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     }
     // the free ring from the head, for the allocation below (nothing writes
     // the ring in this launch before the allocation reads it)
+    // the previous listing's fields, read now with the rest (this launch
+    // rewrites them only at its own listing)
+    const uint64_t ndueb0 = rs->ndueb, nfree0 = rs->nfree, retb0 = rs->ret_b;
     uint32_t fr0;
     {
         const uint64_t h0 = rs->fl_head;
@@ -2235,10 +2239,16 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         if (tid == 0 && ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj)) flag(d, OV_BUG);
     }
     if (tid == 0) {
+        // every round-state field the window needs in one round trip; the new
+        // values are computed in registers and stored once (a load after a
+        // store to the round state would be a memory round trip of its own)
+        const uint64_t S0 = rs->S, E0 = rs->E, rounds0 = rs->rounds, nmj0 = rs->next_min_jump, mj0 = rs->min_jump;
+        const uint64_t jmin0 = rs->jmin, ovf0 = rs->overflow, rmin0 = rs->rmin;
+        const uint64_t xc0 = rs->xcarry, xa0 = rs->xacc[0], xa1 = rs->xacc[1];
         s_head = rs->fl_head;
         s_tail = rs->fl_tail;
-        s_S = rs->S;
-        s_E = rs->E;
+        s_S = S0;
+        s_E = E0;
         s_done = 0;
         s_more = 0;
         s_spent = UINT64_MAX;
@@ -2266,12 +2276,11 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             // the local MIN terms, accumulated by k_scatter's and k_proc's
             // workgroups with device-scope atomics (reduce_local's terms);
             // only this thread reads them, so it resets them too
-            const uint64_t cm = rs->xcarry, em = rs->xacc[0], jm = rs->xacc[1];
-            uint64_t m = cm < em ? cm : em;
-            m = rs->rmin < m ? rs->rmin : m;
+            uint64_t m = xc0 < xa0 ? xc0 : xa0;
+            m = rmin0 < m ? rmin0 : m;
             s_m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
-            s_j = rs->jmin < jm ? rs->jmin : jm;
-            s_ovf = rs->overflow;
+            s_j = jmin0 < xa1 ? jmin0 : xa1;
+            s_ovf = ovf0;
             rs->xcarry = UINT64_MAX;
             rs->xacc[0] = UINT64_MAX;
             rs->xacc[1] = UINT64_MAX;
@@ -2279,16 +2288,29 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // the next window (master.c:450-480), under the other threads' loads
         if (mode == 1 && s_more) {  // drain step: same window, more exchange
             rs->phase = 1;
-            rs->overflow |= s_ovf;
+            rs->overflow = ovf0 | s_ovf;
         } else if (mode != 2) {
             if (mode == 1) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
             rs->phase = 0;
             rs->jmin = s_j;
-            apply_window(d, s_m, s_j, ~s_ovf);
-            if (rs->overflow) rs->done = 1;  // a capacity ran out: stop, the host reports it
-            s_S = rs->S;
-            s_E = rs->E;
-            s_done = rs->done;
+            const Window w = next_window(d, s_m, s_j, mj0, nmj0);
+            const uint64_t ovf = ovf0 | s_ovf;
+            if (d.wlog && rounds0 < d.wlog_cap) {  // the window just executed
+                d.wlog[2 * rounds0] = S0;
+                d.wlog[2 * rounds0 + 1] = E0;
+            }
+            rs->overflow = ovf;
+            rs->rounds = rounds0 + 1;
+            rs->last_min = s_m;
+            rs->next_min_jump = w.next_min_jump;
+            rs->min_jump = w.min_jump;
+            rs->S = w.S;
+            rs->E = w.E;
+            const uint64_t done = w.done | (ovf ? 1u : 0u);  // a capacity ran out: stop, the host reports it
+            rs->done = done;
+            s_S = w.S;
+            s_E = w.E;
+            s_done = done;
         }
     }
     // fold: each shard's range starts where the previous one's ends (k_scatter
@@ -2340,7 +2362,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     if (round_done) {
         // k_gather returned the window's chunks (not the retained bucket's) to
         // the ring behind the tail: take them, and reset the consumed buckets
-        const uint64_t ndb = rs->ndueb;
+        const uint64_t ndb = ndueb0;
         for (uint64_t i = tid; i < ndb; i += PL_T) {
             const uint32_t rb = d.dueb[i];
             B.cnt[rb] = 0;
@@ -2348,7 +2370,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             B.nal[rb] = 0;
             B.mn[rb] = UINT64_MAX;
         }
-        if (tid == 0) s_tail = s_tail + rs->nfree;
+        if (tid == 0) s_tail = s_tail + nfree0;
         __syncthreads();
     }
     PSTAMP(2);
@@ -2438,7 +2460,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // before this launch (old); k_scatter routes the new ones itself
         const uint64_t S = s_S, E = s_E;
         const uint64_t bS = S / W, bL = (E - 1) / W;
-        const uint64_t pr = rs->ret_b;
+        const uint64_t pr = retb0;
         if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
             const uint32_t rb = (uint32_t)(pr % R);
             const uint32_t nc = B.nal[rb];
