@@ -493,22 +493,16 @@ __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 }
 
 // Workgroup-wide reductions through a [16] LDS scratch (blocks of <= 1024);
-// every thread of the block must call them.  The 16 wave partials are read
-// from clamped slots, unconditionally, so all the LDS reads are in flight at
-// once (a read under a condition waits for itself).
+// every thread of the block must call them.  The wave partials come back one
+// per lane and are combined across the wave (DPP / shuffles), so a thread
+// issues one LDS read instead of sixteen.
 __device__ __forceinline__ uint64_t block_min(uint64_t v, uint64_t* s16) {
     v = wave_min(v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
     __syncthreads();
     if (lane == 0) s16[wid] = v;
     __syncthreads();
-    uint64_t r = UINT64_MAX;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) {
-        const uint64_t x = s16[w < nw ? w : 0];  // slot 0 again: harmless for a min
-        r = x < r ? x : r;
-    }
-    return r;
+    return wave_min(lane < nw ? s16[lane] : UINT64_MAX);
 }
 __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
     v = wave_sum(v);
@@ -516,13 +510,7 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
     __syncthreads();
     if (lane == 0) s16[wid] = v;
     __syncthreads();
-    uint64_t r = 0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) {
-        const uint64_t x = s16[w < nw ? w : 0];
-        r += w < nw ? x : 0;
-    }
-    return r;
+    return wave_sum(lane < nw ? s16[lane] : (uint64_t)0);
 }
 // Inclusive scan of a u32 over the wave with DPP row shifts and broadcasts
 // (no LDS round trips).
@@ -544,14 +532,17 @@ __device__ __forceinline__ uint64_t block_excl_scan_2x32(uint64_t v, uint64_t* s
     __syncthreads();  // s16 may still be read by a previous use
     if (lane == 63) s16[wid] = x;
     __syncthreads();
-    uint64_t add = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) {
-        const uint64_t y = s16[w < nw ? w : 0];
-        add += w < wid ? y : 0;
-        tot += w < nw ? y : 0;
-    }
-    *total = tot;
+    // the wave totals one per lane, scanned across the wave: lane w holds the
+    // sum of waves 0..w (each half stays within 32 bits by the contract)
+    const uint64_t y = lane < nw ? s16[lane] : 0;
+    const uint32_t ylo = wave_incl_scan_u32((uint32_t)y), yhi = wave_incl_scan_u32((uint32_t)(y >> 32));
+    const int w0 = __builtin_amdgcn_readfirstlane(wid);
+    uint64_t add = 0;
+    if (w0 > 0)
+        add = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)yhi, w0 - 1) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)ylo, w0 - 1);
+    *total = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)yhi, nw - 1) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)ylo, nw - 1);
     return x - v + add;
 }
 // Exclusive scan of u32 counts whose workgroup total fits 32 bits.
@@ -2402,7 +2393,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             mine += need[q];
         }
         uint64_t total;
+        PSTAMP(8);
         uint64_t off = block_excl_scan(mine, s16, &total);
+        PSTAMP(9);
         // new chunk i's owner: an LDS table when the run fits it (every steady
         // round), else a bucket search per chunk (the boot round)
         const bool table = total <= RMAX;
@@ -2415,6 +2408,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             off += need[q];
         }
         __syncthreads();
+        PSTAMP(10);
         const uint64_t head = s_head, avail = s_tail - head;
         const uint32_t give = (uint32_t)(total < avail ? total : avail);
         const uint32_t head_r = (uint32_t)(head % NCH);
@@ -2438,6 +2432,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             d.btab[(size_t)lo * NCH + B.nal[lo] + k] = id;
         }
         __syncthreads();
+        PSTAMP(11);
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;

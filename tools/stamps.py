@@ -44,6 +44,8 @@ for r in range(3):
     print("   light host, lane 0 (median us): pop+draws %.2f  dst loads %.2f  pair loads %.2f  commit %.2f"
           % tuple(np.median(f, axis=0)))
     d = np.diff(pl[:8]) / 100
+    a8 = np.diff(pl[[2, 8, 9, 10, 11, 3]]) / 100
+    print("   k_plan alloc (us): need %.2f  scan %.2f  owner table %.2f  ring->btab %.2f  nal+head %.2f" % tuple(a8))
     print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
           "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
     sc = sc[sc[:, 0] > 0]
