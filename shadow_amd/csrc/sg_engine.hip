@@ -2174,7 +2174,7 @@ struct PlanLds {
 __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int mode) {
     RoundState* rs = d.rs;
     if (rs->done) return;
-    __shared__ PlanLds B;
+    __shared__ __align__(16) PlanLds B;
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_head, s_tail, s_S, s_E, s_done, s_more, s_spent, s_m, s_j, s_ovf;
     constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
@@ -2376,7 +2376,12 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // search in LDS per chunk) so every ring load is independent.  A
         // bucket the new window takes whole gets none: k_scatter routes its
         // new events straight to the host partitions and never writes them.
-        uint32_t need[PER];
+        // a thread's PER = 4 buckets are adjacent: one 16-B LDS access per array
+        static_assert(PER == 4, "allocation pass assumes four buckets per thread");
+        const uint4 c4 = reinterpret_cast<const uint4*>(B.cnt)[tid];
+        const uint4 n4 = reinterpret_cast<const uint4*>(B.nal)[tid];
+        const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w}, nq[4] = {n4.x, n4.y, n4.z, n4.w};
+        uint32_t need[PER], offq[PER];
         uint64_t mine = 0;
         const uint32_t nbSr = (uint32_t)(nbS % R);
 #pragma unroll
@@ -2384,9 +2389,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             const uint32_t rb = tid * PER + q;
             need[q] = 0;
             if (rb < R) {
-                const uint64_t want = ((uint64_t)B.cnt[rb] + CH - 1) >> CH_SHIFT;
+                const uint64_t want = ((uint64_t)cq[q] + CH - 1) >> CH_SHIFT;
                 const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
-                need[q] = w > B.nal[rb] ? w - B.nal[rb] : 0;
+                need[q] = w > nq[q] ? w - nq[q] : 0;
                 const uint64_t o = rb >= nbSr ? rb - nbSr : rb + R - nbSr;  // bucket nbS + o
                 if (list && o <= nbL - nbS && !(nstraddle && o == nbL - nbS)) need[q] = 0;
             }
@@ -2402,11 +2407,12 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;
-            if (rb < R) B.off[rb] = (uint32_t)off;
+            offq[q] = (uint32_t)off;
             if (table)
                 for (uint32_t k = 0; k < need[q]; ++k) B.own[off + k] = rb | (k << 12);
             off += need[q];
         }
+        reinterpret_cast<uint4*>(B.off)[tid] = make_uint4(offq[0], offq[1], offq[2], offq[3]);
         __syncthreads();
         PSTAMP(10);
         const uint64_t head = s_head, avail = s_tail - head;
@@ -2433,16 +2439,14 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         }
         __syncthreads();
         PSTAMP(11);
+        uint32_t gq[PER];
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t rb = tid * PER + q;
-            if (rb >= R || !need[q]) continue;
-            const uint32_t o = B.off[rb];
-            const uint32_t got = give <= o ? 0 : (give - o < need[q] ? give - o : need[q]);
-            B.nal[rb] += got;
+            const uint32_t o = offq[q];
+            gq[q] = nq[q] + (give <= o ? 0 : (give - o < need[q] ? give - o : need[q]));
         }
-        __syncthreads();
-        if (tid == 0) {
+        reinterpret_cast<uint4*>(B.nal)[tid] = make_uint4(gq[0], gq[1], gq[2], gq[3]);
+        if (tid == 0) {  // s_head: read again only by this thread
             if (total > avail) flag(d, OV_POOL);
             s_head = head + give;
         }
