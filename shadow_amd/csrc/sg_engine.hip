@@ -238,6 +238,8 @@ struct Dev {
     uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
                                               // events at, dynamic bytes
     uint64_t W;
+    uint32_t wdiv_m, wdiv_s1, wdiv_s2;  // n / W for n < 2^32 by multiply-high (wdiv)
+    bool ring32;                        // R * W < 2^32: bucket offsets from the window's first bucket fit 32 bits
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
     const HostInfo* hinfo;    // [N]
@@ -335,6 +337,14 @@ __device__ __forceinline__ PairRec load_pair(const Dev& d, uint32_t sv, uint32_t
     }
     pr.jump = want_jump ? d.pjump[idx] : UINT32_MAX;
     return pr;
+}
+
+// n / W for 32-bit n without a division: Granlund-Montgomery multiply-high
+// with the host's constants (exact for every n < 2^32).  The 64-bit divisions
+// it replaces expand to ~70 VALU instructions each.
+__device__ __forceinline__ uint32_t wdiv(const Dev& d, uint32_t n) {
+    const uint32_t t = __umulhi(d.wdiv_m, n);
+    return (t + ((n - t) >> d.wdiv_s1)) >> d.wdiv_s2;
 }
 
 __device__ __forceinline__ int32_t dev_rand_r(uint32_t& state) {
@@ -1414,16 +1424,30 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint32_t bSr = (uint32_t)(bS % R);
     const bool self_possible = E - S > d.vself_min;
     bool horizon = false;
+    const uint64_t bSW = bS * W;
     auto count_local = [&](uint64_t t) {  // one staged local event into the bucket bins
-        const uint64_t b = t / W;
-        if (b < bS || b - bS >= R) {
-            horizon = true;
-            return;
+        uint32_t o, off;  // bucket bS + o, the offset in it
+        if (d.ring32) {   // launch-uniform: no 64-bit division
+            const uint64_t rel = t - bSW;
+            o = wdiv(d, (uint32_t)rel);
+            off = (uint32_t)rel - o * (uint32_t)W;
+            if (t < bSW || (rel >> 32) || o >= R) {
+                horizon = true;
+                return;
+            }
+        } else {
+            const uint64_t b = t / W;
+            if (b < bS || b - bS >= R) {
+                horizon = true;
+                return;
+            }
+            o = (uint32_t)(b - bS);
+            off = (uint32_t)(t - b * W);
         }
-        uint32_t rb = bSr + (uint32_t)(b - bS);
+        uint32_t rb = bSr + o;
         rb = rb >= R ? rb - R : rb;
         atomicAdd(&s_bc[rb], 1u);
-        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
+        atomicMin(&s_bm[rb], off);
     };
     auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
         Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
@@ -1901,6 +1925,9 @@ constexpr size_t SCAT_LDS = INS_LDS > GATHER_LDS ? INS_LDS : GATHER_LDS;
 struct Route {
     bool listed;
     uint64_t S, E, ret;   // the new window, its straddling bucket (UINT64_MAX: none)
+    uint64_t bS, bSW;     // the window's first bucket and its start: every event inserted is at or
+                          // after it and within R buckets of it (k_proc's horizon check)
+    uint32_t bSr;         // bS % R
 };
 
 // One batch of up to SU events per thread (every thread of the workgroup
@@ -1913,12 +1940,24 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
                                              uint64_t& ntomb) {
     const uint64_t W = d.W;
     const uint32_t R = d.R;
-    uint32_t rb[SU], pos[SU];
+    uint32_t rb[SU], pos[SU], off[SU];
     bool due[SU], write[SU];
 #pragma unroll
     for (int q = 0; q < SU; ++q) {
-        const uint64_t b = t[q] / W;
-        rb[q] = v[q] ? (uint32_t)(b % R) : 0u;
+        uint64_t b;
+        if (d.ring32) {  // launch-uniform: offsets from the window's first bucket, no 64-bit division
+            const uint64_t rel = t[q] - ro.bSW;
+            const uint32_t o = wdiv(d, (uint32_t)rel);
+            b = ro.bS + o;
+            off[q] = (uint32_t)rel - o * (uint32_t)W;
+            const uint32_t r0 = ro.bSr + o;
+            rb[q] = v[q] ? (r0 >= R ? r0 - R : r0) : 0u;
+            if (v[q] && (t[q] < ro.bSW || (rel >> 32) || o >= R)) flag(d, OV_BUG);
+        } else {
+            b = t[q] / W;
+            off[q] = (uint32_t)(t[q] - b * W);
+            rb[q] = v[q] ? (uint32_t)(b % R) : 0u;
+        }
         pos[q] = v[q] ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
         due[q] = v[q] && ro.listed && t[q] < ro.E;
         const bool in_ret = ro.listed && b == ro.ret;
@@ -1937,8 +1976,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
     for (int q = 0; q < SU; ++q) {
         // beyond the allocation only when the pool ran out (k_plan flagged it)
         if (!write[q] || (pos[q] >> CH_SHIFT) >= na[q] || id[q] >= d.NCH) continue;
-        const uint64_t b = t[q] / W;
-        Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | (t[q] - b * W)), k[q]};
+        Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
         ntomb += due[q];
         d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r;
     }
@@ -1995,6 +2033,9 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     ro.S = rs->S;
     ro.E = rs->E;
     ro.ret = rs->ret_b;
+    ro.bS = rs->bS;
+    ro.bSW = ro.bS * d.W;
+    ro.bSr = (uint32_t)(ro.bS % R);
     // SG_STAMPS: {start, after setup, after the events, end, role, events}
     uint64_t* st = d.stamps && threadIdx.x == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
     if (st) {
@@ -2177,6 +2218,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     __shared__ __align__(16) PlanLds B;
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_head, s_tail, s_S, s_E, s_done, s_more, s_spent, s_m, s_j, s_ovf;
+    __shared__ uint64_t s_nbS, s_nbL;                    // the window's first and last bucket
+    __shared__ uint32_t s_nbSr, s_headr, s_tailr;        // nbS % R, head % NCH, tail % NCH
     constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
     const uint32_t R = d.R, NCH = d.NCH;
     const uint64_t W = d.W;
@@ -2216,7 +2259,9 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
     uint32_t fr0;
     {
         const uint64_t h0 = rs->fl_head;
-        fr0 = d.fring[(h0 + tid) % NCH];  // NCH may be below PL_T (small engines)
+        uint32_t pos = (uint32_t)(h0 % NCH) + tid;  // one 64-bit remainder, uniform
+        if (pos >= NCH) pos = NCH >= PL_T ? pos - NCH : pos % NCH;  // NCH may be below PL_T (small engines)
+        fr0 = d.fring[pos];
     }
     if (mode == 1 && d.check) {
         // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in this
@@ -2303,6 +2348,13 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             s_E = w.E;
             s_done = done;
         }
+        // the bucket arithmetic every thread needs, divided once here
+        const uint64_t nbS = s_S / W;
+        s_nbS = nbS;
+        s_nbL = (s_E - 1) / W;
+        s_nbSr = (uint32_t)(nbS % R);
+        s_headr = (uint32_t)(s_head % NCH);
+        s_tailr = (uint32_t)(s_tail % NCH);
     }
     // fold: each shard's range starts where the previous one's ends (k_scatter
     // adds it to the workgroup's own base)
@@ -2361,13 +2413,16 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
             B.nal[rb] = 0;
             B.mn[rb] = UINT64_MAX;
         }
-        if (tid == 0) s_tail = s_tail + nfree0;
+        if (tid == 0) {
+            s_tail = s_tail + nfree0;
+            s_tailr = (uint32_t)(s_tail % NCH);
+        }
         __syncthreads();
     }
     PSTAMP(2);
     PSTAMP(4);
     // the new window's buckets (when listed): [nbS, nbL], nbL straddling E or not
-    const uint64_t nbS = s_S / W, nbL = (s_E - 1) / W;
+    const uint64_t nbS = s_nbS, nbL = s_nbL;
     const bool nstraddle = s_E < (nbL + 1) * W;
     if (mode != 2) {
         // every bucket gets the chunks its count needs (k_proc / k_count
@@ -2383,7 +2438,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w}, nq[4] = {n4.x, n4.y, n4.z, n4.w};
         uint32_t need[PER], offq[PER];
         uint64_t mine = 0;
-        const uint32_t nbSr = (uint32_t)(nbS % R);
+        const uint32_t nbSr = s_nbSr;
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t rb = tid * PER + q;
@@ -2417,7 +2472,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         PSTAMP(10);
         const uint64_t head = s_head, avail = s_tail - head;
         const uint32_t give = (uint32_t)(total < avail ? total : avail);
-        const uint32_t head_r = (uint32_t)(head % NCH);
+        const uint32_t head_r = s_headr;
         for (uint32_t i = tid; i < give; i += PL_T) {
             uint32_t lo, k;
             if (table) {
@@ -2458,13 +2513,16 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         // list the due chunks of the new window [S, E): the slots written
         // before this launch (old); k_scatter routes the new ones itself
         const uint64_t S = s_S, E = s_E;
-        const uint64_t bS = S / W, bL = (E - 1) / W;
+        const uint64_t bS = s_nbS, bL = s_nbL;
+        const uint32_t bSr = s_nbSr;
+        // ring slot of bucket bS + o (o < R)
+        auto ring_of = [&](uint64_t o) -> uint32_t { const uint32_t r = bSr + (uint32_t)o; return r >= R ? r - R : r; };
         const uint64_t pr = retb0;
         if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
             const uint32_t rb = (uint32_t)(pr % R);
             const uint32_t nc = B.nal[rb];
             const uint64_t tail = s_tail;
-            const uint32_t tail_r = (uint32_t)(tail % NCH);
+            const uint32_t tail_r = s_tailr;
             for (uint32_t ci = tid; ci < nc; ci += PL_T) {
                 const uint32_t pos = tail_r + ci;  // nc <= NCH: one wrap at most
                 d.fring[pos >= NCH ? pos - NCH : pos] = d.btab[(size_t)rb * NCH + ci];
@@ -2485,7 +2543,7 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         const bool straddle = E < (bL + 1) * W;
         uint64_t nd = 0, ndb = 0, nf = 0;
         for (uint64_t b = bS; b <= bL; ++b) {
-            const uint32_t rb = (uint32_t)(b % R);
+            const uint32_t rb = ring_of(b - bS);
             const uint32_t c = B.cnt[rb], co = B.old[rb];
             const bool ret = straddle && b == bL;
             // a retained bucket lists the chunks holding old slots; a bucket
@@ -2504,14 +2562,14 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         }
         __syncthreads();
         PSTAMP(5);
-        if (straddle && tid == 0) B.mn[bL % R] = UINT64_MAX;  // k_gather's carry min and k_count restore it
+        if (straddle && tid == 0) B.mn[ring_of(bL - bS)] = UINT64_MAX;  // k_gather's carry min and k_count restore it
         // exact min beyond the window: the first non-empty bucket in (bL, bS + R).
         // Off the plan's critical path: k_scatter's last workgroup finds it
         // from the written-back metadata (first_live_bucket) — except at boot,
         // where no k_scatter follows.
         uint64_t first = UINT64_MAX;
         if (mode == 2) {
-            const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
+            const uint32_t span = (uint32_t)(bL - bS), bLr = ring_of(bL - bS);
             for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
                 const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
                 if (rb == s_spent) continue;
@@ -2825,6 +2883,14 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.W = W;
     d.R = (uint32_t)(span / W + 3);
+    d.ring32 = (uint64_t)d.R * W < (1ull << 32);
+    {  // Granlund-Montgomery constants for 32-bit division by W (W < 2^32)
+        uint32_t l = 0;
+        while ((1ull << l) < W) ++l;
+        d.wdiv_m = (uint32_t)(((1ull << 32) * ((1ull << l) - W)) / W + 1);
+        d.wdiv_s1 = l < 1 ? l : 1;
+        d.wdiv_s2 = l > 1 ? l - 1 : 0;
+    }
     d.G3 = env_u32("SG_INS_GRID", 128);
     // default event slots per host: PHOLD keeps `load` events per host in flight;
     // gossip floods keep about ten fan-outs' worth (configs[4]: 82 per host at peak)
