@@ -89,7 +89,9 @@ constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
 constexpr uint32_t RETAINED = 1u << 31;
-constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record {evc, HDR_REC | host}
+constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record
+                                          // {evc, HDR_REC | active index << 32 | host}
+constexpr uint64_t PAD_REC = 1ull << 62;  // with HDR_REC: a skip record (a draw that selected no host)
 // exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
 constexpr int HDR = 2;
 enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND };
@@ -1526,18 +1528,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                         }
                         d.hs[lh] = c.s;
                     } else {
-                        // count this host's sends (arithmetic only)
-                        uint32_t r = c.s.rng;
+                        // this host's sends, at most: a draw that selects no host
+                        // (test_phold.c:176-177) sends nothing, so the path is
+                        // picked without the draws; the record path pads for them
                         for (uint32_t i = 0; i < cnt; ++i) {
                             const uint64_t bk = seg[i].k;
                             const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
-                            const uint32_t nsend = boot ? d.load : 1u;
-                            for (uint32_t m = 0; m < nsend; ++m) {
-                                const int32_t x = dev_rand_r(r);
-                                if (x > last) continue;
-                                (void)dev_rand_r(r);
-                                ++ns;
-                            }
+                            ns += boot ? d.load : 1u;
                         }
                         if (ns <= d.light_max && q < d.light_q) {
                             // light host (most hosts in steady state): the whole
@@ -1608,11 +1605,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             s_sb[j] = base;
             s_vh[j] = c.vh | (ns << 16);
-            sput(base, Rec{c.s.evc, HDR_REC | c.h});
+            sput(base, Rec{c.s.evc, HDR_REC | ((uint64_t)j << 32) | c.h});
             uint32_t k = base + 1;
             pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
                 sput(k++, Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
             });
+            for (; k <= base + ns; ++k) sput(k, Rec{0, HDR_REC | PAD_REC});  // draws that selected no host
             // {rng, pops, digest} now; evc after phase C
             HostState* hp = d.hs + lh;
             reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
@@ -1681,14 +1679,21 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // records; then endTime drop, barrier bump, staging.
     for (uint32_t i = tid; i < nsend; i += K2_T) {
         const Rec r = sget(i);
-        if (r.k & HDR_REC) continue;  // a host's header
+        if (r.k & HDR_REC) {
+            if (r.k & PAD_REC) continue;
+            // a host's header: its counter after all its kept sends
+            const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
+            uint64_t evc = r.a;
+            for (uint32_t k = i + 1; k <= i + ns; ++k) evc += sget(k).a >> 63;
+            d.hs[sbase + s_act[j]].evc = evc;
+            continue;
+        }
         const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
-        const uint32_t sb = s_sb[j], ns = s_vh[j] >> 16;
+        const uint32_t sb = s_sb[j];
         const Rec hd = sget(sb);
         uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
         for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
         const bool keep = (r.a >> 63) != 0;
-        if (i == sb + ns) d.hs[sbase + s_act[j]].evc = evc + keep;  // the host's last send
         if (!keep) {
             ++a.ctr[C_DROPREL];
             continue;
