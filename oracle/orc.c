@@ -142,16 +142,14 @@ struct orc_sim {
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
 #define FMIX(z) (z ^= z >> 33, z *= 0xff51afd7ed558ccdULL, z ^= z >> 33, z *= 0xc4ceb9fe1a85ec53ULL, z ^= z >> 33)
-    uint64_t z = pos + 0x9E3779B97F4A7C15ULL;
+    /* test infrastructure: the per-host trace digest term, order-sensitive
+       through pos (the device computes the same) */
+    uint64_t z = time ^ (pos * 0x9E3779B97F4A7C15ULL);
     FMIX(z);
-    z ^= time;
+    z ^= ((uint64_t)src << 40) | seq;
     FMIX(z);
-    z ^= (uint64_t)src;
-    FMIX(z);
-    z ^= seq;
-    FMIX(z);
-    return z;
 #undef FMIX
+    return z;
 }
 
 orc_sim* orc_create(const orc_params* p, const uint32_t* host_vertex, const uint32_t* host_rng,

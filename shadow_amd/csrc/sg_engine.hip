@@ -376,10 +376,8 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
 
 // Per-host trace digest term (order-sensitive through pos); same as the oracle.
 __device__ __forceinline__ uint64_t digest_mix(uint64_t pos, uint64_t t, uint32_t src, uint64_t seq) {
-    uint64_t z = fmix64(pos + 0x9E3779B97F4A7C15ULL);
-    z = fmix64(z ^ t);
-    z = fmix64(z ^ (uint64_t)src);
-    return fmix64(z ^ seq);
+    uint64_t z = fmix64(t ^ (pos * 0x9E3779B97F4A7C15ULL));
+    return fmix64(z ^ (((uint64_t)src << 40) | seq));  // seq < 2^40 (SRC_SHIFT)
 }
 
 // Destination draw; returns the chosen host's global slot, or N when no host

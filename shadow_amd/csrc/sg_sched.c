@@ -55,16 +55,12 @@ struct drv {
 
 static uint64_t digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
 #define FMIX(z) (z ^= z >> 33, z *= 0xff51afd7ed558ccdULL, z ^= z >> 33, z *= 0xc4ceb9fe1a85ec53ULL, z ^= z >> 33)
-    uint64_t z = pos + 0x9E3779B97F4A7C15ULL;
+    uint64_t z = time ^ (pos * 0x9E3779B97F4A7C15ULL);  /* the device engine's trace digest term */
     FMIX(z);
-    z ^= time;
+    z ^= ((uint64_t)src << 40) | seq;
     FMIX(z);
-    z ^= (uint64_t)src;
-    FMIX(z);
-    z ^= seq;
-    FMIX(z);
-    return z;
 #undef FMIX
+    return z;
 }
 
 static uint32_t choose_dst(const drv* d, int32_t x) {
