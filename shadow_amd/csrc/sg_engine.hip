@@ -197,6 +197,22 @@ struct HostState {
     uint64_t evc;     // eventIDCounter (host.c:397-400); k_proc writes it last (phase C)
 };
 
+// Unsigned 32-bit division by a launch constant without a divide:
+// Granlund-Montgomery multiply-high with host-made constants, exact for every
+// n < 2^32 (the 64-bit divisions it replaces expand to ~70 VALU instructions).
+struct Div32 {
+    uint32_t m, s1, s2;
+};
+inline Div32 make_div32(uint64_t dv) {  // 1 <= dv < 2^32
+    uint32_t l = 0;
+    while ((1ull << l) < dv) ++l;
+    return Div32{(uint32_t)(((1ull << 32) * ((1ull << l) - dv)) / dv + 1), l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
+}
+__device__ __forceinline__ uint32_t udiv32(const Div32& q, uint32_t n) {
+    const uint32_t t = __umulhi(q.m, n);
+    return (t + ((n - t) >> q.s1)) >> q.s2;
+}
+
 struct RoundState {
     uint64_t S, E, done, rounds;
     uint64_t min_jump, next_min_jump, jmin;
@@ -236,11 +252,12 @@ struct Dev {
     uint32_t workload, msg_shift, gossip_msgs, mw;
     uint64_t gossip_start, gossip_interval;
     uint32_t* seen;           // [L][mw] per-host message bitsets
-    uint32_t R, NCH, HP, hp_shift, P, CAPP, ECAP, G1, G3;
+    uint32_t R, NCH, HP, P, CAPP, ECAP, G1, G3;
+    Div32 hpdiv;              // a local slot's partition: slot / HP (HP need not be a power of two)
     uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
                                               // events at, dynamic bytes
     uint64_t W;
-    uint32_t wdiv_m, wdiv_s1, wdiv_s2;  // n / W for n < 2^32 by multiply-high (wdiv)
+    Div32 wdiv;                         // n / W for n < 2^32
     bool ring32;                        // R * W < 2^32: bucket offsets from the window's first bucket fit 32 bits
     uint64_t end_time, bootstrap_end, fixed_jump, runahead_min, trace_cap, xcap, xrows;
     uint32_t bounds[MAXG + 1];
@@ -341,13 +358,8 @@ __device__ __forceinline__ PairRec load_pair(const Dev& d, uint32_t sv, uint32_t
     return pr;
 }
 
-// n / W for 32-bit n without a division: Granlund-Montgomery multiply-high
-// with the host's constants (exact for every n < 2^32).  The 64-bit divisions
-// it replaces expand to ~70 VALU instructions each.
-__device__ __forceinline__ uint32_t wdiv(const Dev& d, uint32_t n) {
-    const uint32_t t = __umulhi(d.wdiv_m, n);
-    return (t + ((n - t) >> d.wdiv_s1)) >> d.wdiv_s2;
-}
+__device__ __forceinline__ uint32_t wdiv(const Dev& d, uint32_t n) { return udiv32(d.wdiv, n); }
+__device__ __forceinline__ uint32_t part_of(const Dev& d, uint32_t dl) { return udiv32(d.hpdiv, dl); }
 
 __device__ __forceinline__ int32_t dev_rand_r(uint32_t& state) {
     // glibc rand_r, utility/random.c:32-37
@@ -690,7 +702,6 @@ template <bool SCATTER, int GT>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
                                             uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
                                             uint64_t& cmin, uint64_t& ntomb) {
-    const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
     const uint32_t tot = nb * CH;
     for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += GT * GUNR) {
         Rec r[GUNR];
@@ -717,14 +728,14 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
                 if (!SCATTER) cmin = t < cmin ? t : cmin;
                 continue;
             }
-            const uint32_t p = dl >> sh;
+            const uint32_t p = part_of(d, dl);
             if (!SCATTER) {
                 atomicAdd(&s_cnt[p], 1u);
                 continue;
             }
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             if (slot < d.CAPP)
-                st_stream(&d.part[(size_t)p * d.CAPP + slot], Rec{((uint64_t)(dl & hmask) << 52) | (t - S), r[q].k});
+                st_stream(&d.part[(size_t)p * d.CAPP + slot], Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k});
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
                 ++ntomb;
@@ -790,7 +801,6 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[5] = nb;
         }
-        const uint32_t sh = d.hp_shift, hmask = d.HP - 1;
         Rec r[GR];
         uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
 #pragma unroll
@@ -816,8 +826,8 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
                 cmin = t < cmin ? t : cmin;
                 continue;
             }
-            pp[q] = dl >> sh;
-            r[q].a = ((uint64_t)(dl & hmask) << 52) | (t - S);  // the partition record
+            pp[q] = part_of(d, dl);
+            r[q].a = ((uint64_t)(dl - pp[q] * d.HP) << 52) | (t - S);  // the partition record
             atomicAdd(&s_cnt[pp[q]], 1u);
         }
         __syncthreads();
@@ -1966,7 +1976,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         const bool in_ret = ro.listed && b == ro.ret;
         write[q] = v[q] && (!due[q] || in_ret);  // fully due buckets: the slot stays empty
         if (v[q] && !due[q] && in_ret) smin = t[q] < smin ? t[q] : smin;
-        if (due[q]) atomicAdd(&s_pc[dl[q] >> d.hp_shift], 1u);
+        if (due[q]) atomicAdd(&s_pc[part_of(d, dl[q])], 1u);
     }
     uint32_t na[SU], id[SU];
 #pragma unroll
@@ -1996,14 +2006,13 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         }
     }
     __syncthreads();
-    const uint32_t hmask = d.HP - 1;
 #pragma unroll
     for (int q = 0; q < SU; ++q) {
         if (!due[q]) continue;
-        const uint32_t p = dl[q] >> d.hp_shift;
+        const uint32_t p = part_of(d, dl[q]);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
         if (slot < d.CAPP)
-            d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl[q] & hmask) << 52) | (t[q] - ro.S), k[q]};
+            d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]};
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
@@ -2887,13 +2896,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.W = W;
     d.R = (uint32_t)(span / W + 3);
     d.ring32 = (uint64_t)d.R * W < (1ull << 32);
-    {  // Granlund-Montgomery constants for 32-bit division by W (W < 2^32)
-        uint32_t l = 0;
-        while ((1ull << l) < W) ++l;
-        d.wdiv_m = (uint32_t)(((1ull << 32) * ((1ull << l) - W)) / W + 1);
-        d.wdiv_s1 = l < 1 ? l : 1;
-        d.wdiv_s2 = l > 1 ? l - 1 : 0;
-    }
+    d.wdiv = make_div32(W);
     d.G3 = env_u32("SG_INS_GRID", 128);
     // default event slots per host: PHOLD keeps `load` events per host in flight;
     // gossip floods keep about ten fan-outs' worth (configs[4]: 82 per host at peak)
@@ -2914,9 +2917,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // host partitions: HP hosts per k_proc workgroup (power of two), about
     // one partition per CU
     const uint32_t hp_env = env_u32("SG_HP", 0);
-    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, next_pow2(hp_env ? hp_env : (d.L + 255) / 256)));
-    d.hp_shift = 0;
-    while ((1u << d.hp_shift) < d.HP) ++d.hp_shift;
+    // one partition per CU: HP = ceil(L / 256) rounded up to a multiple of 16
+    // (P = 245 at 1M hosts with powers of two left 11 CUs idle)
+    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, hp_env ? hp_env : ((d.L + 255) / 256 + 15) / 16 * 16));
+    d.hpdiv = make_div32(d.HP);
     d.P = (d.L + d.HP - 1) / d.HP;
     if (d.P > PMAX) {
         sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
