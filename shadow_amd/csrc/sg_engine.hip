@@ -86,9 +86,12 @@ constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
 constexpr uint32_t XS = SG_XS;
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
+constexpr uint32_t G3MAX = 512;          // k_count workgroups (received-block split)
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
 constexpr uint32_t RETAINED = 1u << 31;
+constexpr uint32_t ST = 16;           // chunk ids in a reserving row's stash
+constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (bucket width set to fit)
 constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record
                                           // {evc, HDR_REC | active index << 32 | host}
 constexpr uint64_t PAD_REC = 1ull << 62;  // with HDR_REC: a skip record (a draw that selected no host)
@@ -222,14 +225,14 @@ struct RoundState {
     uint64_t last_min;
     // calendar
     uint64_t bS, bL;         // due bucket range of the current window (absolute indices)
+    uint64_t pbS, pbL, pret; // the window before it (its consumed buckets are reset by the next
+                             // k_proc) and its straddling bucket, or UINT64_MAX
     uint64_t rmin;           // min time in buckets beyond bL (exact, at plan time)
-    uint64_t ndue;           // due chunk entries
-    uint64_t ndueb;          // listed non-retained buckets (reset at the next plan)
-    uint64_t nfree;          // due chunks outside the retained bucket (a prefix of the list):
-                             // k_gather returns them to the free ring behind fl_tail
-    uint64_t rmin_todo;      // k_plan listed a window: k_scatter's last workgroup computes rmin
-    uint64_t listed;         // k_plan listed a new window: k_scatter gathers and routes for it
+    uint64_t nfree;          // due chunks the last gather returned to the free ring behind fl_tail
+    uint64_t rmin_todo;      // a window was listed: k_scatter's last workgroup computes rmin
+    uint64_t listed;         // a new window was listed: k_scatter gathers and routes for it
     uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
+    uint64_t fold;           // steps planned: k_scatter reads bw[fold & 1], writes bw[fold & 1 ^ 1]
     uint64_t fl_head, fl_tail;
     uint64_t ins_local;      // k_count took the staged local events (process step)
     uint64_t ins_S;          // their window start (staged times are relative to it)
@@ -286,21 +289,19 @@ struct Dev {
     uint64_t* wtime;          // [3][P] barrier timers (scheduler.c:380-389), or null: busy ticks,
                               // idle ticks (waiting for the round's last partition), this round's end
     HostState* hs;            // [L]
-    // calendar
+    // calendar: bucket rb is XS sub-lists; a reserving row (k_proc partition p,
+    // k_count workgroup w) appends to sub-list p % XS (w % XS)
     Rec* pool;                // [NCH][CH]
-    uint32_t* btab;           // [R][NCH] chunk ids of each bucket
-    uint32_t* bcnt;           // [R] records appended (tombstones included)
+    uint32_t* btab;           // [XS][R][NCH] chunk ids of each sub-list
+    uint32_t* bk;             // [XS][R] slots reserved (k_proc / k_count atomics)
+    uint32_t* bw;             // [2][XS][R] slots written before the step: k_scatter reads
+                              // bw[fold & 1] and copies bk into the other half for the next step
     uint32_t* btomb;          // [R] tombstones
     uint64_t* bmin;           // [R] min live time
-    uint32_t* fring;          // [NCH] free chunk ring
-    uint32_t* nal;            // [R] chunks allocated to each bucket
-    uint32_t* wbase;          // [P + G3][R] reserved base per (source, bucket): rows < P
-                              // partitions (k_proc), then k_count's received-block split;
-                              // relative to the source's shard range in bxoff
-    uint32_t* bdel;           // [XS][R] this step's reservations, per reserving shard
-    uint32_t* bxoff;          // [XS][R] first slot of each shard's reservations (k_plan)
-    DueEnt* due;              // [NCH]
-    uint32_t* dueb;           // [R] ring slots of the listed non-retained buckets
+    uint32_t* fring;          // [NCH] free chunk ring (head: rs->fl_head, taken atomically)
+    uint32_t* stash;          // [P + G3][ST] chunk ids each reserving row keeps at hand
+    uint32_t* stn;            // [P + G3] ids in the row's stash
+    uint32_t* wbase;          // [P + G3][R] reserved base per (row, bucket) in the row's sub-list
     // partitions
     uint32_t* pcnt;           // [P] due events of the partition this round
     Rec* part;                // [P][CAPP]
@@ -637,16 +638,18 @@ __global__ void k_boot(Dev d) {
         d.hs[i] = s;
     }
     if (i < d.NCH) d.fring[i] = i;
-    for (uint32_t j = i; j < XS * d.R; j += gridDim.x * blockDim.x) d.bdel[j] = 0;
     if (d.seen)
         for (size_t j = i; j < (size_t)d.L * d.mw; j += (size_t)gridDim.x * blockDim.x) d.seen[j] = 0;
-    if (i < nb0) d.btab[i] = i;  // bucket 0 is ring slot 0
+    if (i < nb0) d.btab[i] = i;  // bucket 0 is ring slot 0, its sub-list 0
+    for (uint32_t j = i; j < XS * d.R; j += gridDim.x * blockDim.x) {
+        d.bk[j] = j == 0 ? d.L : 0u;
+        d.bw[j] = d.bw[(size_t)XS * d.R + j] = j == 0 ? d.L : 0u;
+    }
     if (i < d.R) {
-        d.nal[i] = i == 0 ? nb0 : 0;
-        d.bcnt[i] = i == 0 ? d.L : 0;
         d.btomb[i] = 0;
         d.bmin[i] = i == 0 ? 0 : UINT64_MAX;
     }
+    if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
     if (i < d.P) {
         d.pcnt[i] = 0;
         d.rcnt[i] = 0;
@@ -667,9 +670,10 @@ __global__ void k_boot(Dev d) {
         for (int c = 0; c < NCTR; ++c) rs->ctr[c] = 0;
         rs->last_min = 0;
         rs->bS = rs->bL = 0;
+        rs->pbS = rs->pbL = rs->pret = UINT64_MAX;
         rs->rmin = SIMTIME_MAX;
-        rs->ndue = 0;
-        rs->ndueb = 0;
+        rs->nfree = 0;
+        rs->fold = 0;
         rs->listed = 0;
         rs->ret_b = UINT64_MAX;
         rs->fl_head = nb0;
@@ -744,13 +748,108 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
     }
 }
 
-// Gather role of k_scatter's workgroups [g0, g0 + nw): the due chunks k_plan
-// listed for the new window [S, E) into the host partitions.  GR events per
-// thread in registers on the one-pass path (4 chunks per workgroup).  The
-// listed counts cover only the slots filled before this launch ("old"
-// slots); the same launch's insert workgroups route the new due events
-// themselves, so the two never touch the same slot.
-constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8;
+// The listed window's due chunks as one list of segments, derived by every
+// gather workgroup from the bucket words (no listing pass): each fully due
+// bucket's sub-lists (all their chunks; the slots written before this step
+// hold its events), then the previous window's straddling bucket if the new
+// window left it behind (spent: its chunks only go back to the ring), then
+// the new window's straddling bucket (retained: the chunks holding written
+// slots; its events at or after E stay).  The first nfree entries go back to
+// the free ring.  Written slots come from bw[fold & 1]; this launch's inserts
+// fill the slots reserved since (and route the due ones themselves).
+constexpr uint32_t SEGMAX = (NBMAX + 2) * XS;  // segments, at most
+// Segment j is bucket sub-list x = j % XS of the list's k-th bucket, k = j / XS:
+// k < nfull: bucket bS + k (taken whole); then the spent bucket, if any; then
+// the straddling bucket bL (retained).  LDS keeps each segment's first list
+// index and written slots.
+struct DueList {
+    uint64_t bS, bL, pret, W;
+    uint32_t nfull, nseg, R;
+    bool spent;
+    __device__ __forceinline__ void seg(uint32_t j, uint64_t& b, uint32_t& x, uint32_t& flags, bool& events) const {
+        const uint32_t k = j / XS;
+        x = j % XS;
+        b = bL;
+        flags = RETAINED;
+        events = true;
+        if (k < nfull) {
+            b = bS + k;
+            flags = 0;
+        } else if (spent && k == nfull) {
+            b = pret;
+            flags = 0;
+            events = false;
+        }
+    }
+};
+template <int GT>
+__device__ uint32_t due_segments(const Dev& d, DueList& dl, uint32_t* s_start, uint32_t* s_lo, uint64_t* s16,
+                                 uint64_t* nfree_out) {
+    const RoundState* rs = d.rs;
+    dl.bS = rs->bS;
+    dl.bL = rs->bL;
+    dl.pret = rs->pret;
+    dl.W = d.W;
+    dl.R = d.R;
+    const uint64_t ret = rs->ret_b;
+    const uint32_t cur = (uint32_t)(rs->fold & 1);
+    dl.spent = dl.pret != UINT64_MAX && dl.pret < dl.bS;
+    const uint32_t nb = (uint32_t)(dl.bL - dl.bS + 1);
+    dl.nfull = nb - (ret != UINT64_MAX ? 1u : 0u);
+    dl.nseg = (dl.nfull + (dl.spent ? 1u : 0u) + (ret != UINT64_MAX ? 1u : 0u)) * XS;
+    const uint32_t per = (dl.nseg + GT - 1) / GT, j0 = threadIdx.x * per;
+    const uint32_t j1 = j0 + per < dl.nseg ? j0 + per : dl.nseg;
+    uint32_t nc = 0, ncf = 0;
+    for (uint32_t j = j0; j < j1; ++j) {
+        uint64_t b;
+        uint32_t x, flags;
+        bool events;
+        dl.seg(j, b, x, flags, events);
+        const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
+        const uint32_t hi = d.bk[row], lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
+        const uint32_t n = ((flags ? lo : hi) + CH - 1) >> CH_SHIFT;
+        s_lo[j] = lo;
+        s_start[j] = n;  // the count for now
+        nc += n;
+        ncf += flags ? 0u : n;
+    }
+    uint64_t tot;
+    uint64_t off = block_excl_scan_2x32(((uint64_t)ncf << 32) | nc, s16, &tot);  // barriers inside
+    uint32_t o = (uint32_t)off;
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t n = s_start[j];
+        s_start[j] = o;
+        o += n;
+    }
+    __syncthreads();
+    *nfree_out = tot >> 32;
+    return (uint32_t)tot;
+}
+// List entry i: its chunk id (from the table), events, flags and bucket base.
+__device__ __forceinline__ DueEnt due_entry(const Dev& d, const DueList& dl, const uint32_t* s_start,
+                                            const uint32_t* s_lo, uint32_t i) {
+    uint32_t lo = 0, hi = dl.nseg - 1;  // the last segment starting at or before i
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_start[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    uint64_t b;
+    uint32_t x, flags;
+    bool events;
+    dl.seg(lo, b, x, flags, events);
+    const uint32_t ci = i - s_start[lo], w = s_lo[lo];
+    const uint32_t left = w > (ci << CH_SHIFT) ? w - (ci << CH_SHIFT) : 0u;
+    const size_t row = (size_t)x * dl.R + (uint32_t)(b % dl.R);
+    return DueEnt{d.btab[row * d.NCH + ci], (left < CH ? left : CH) | flags, b * dl.W};
+}
+
+// Gather role of k_scatter's workgroups [g0, g0 + nw): the due chunks of the
+// new window [S, E) into the host partitions.  GR events per thread in
+// registers on the one-pass path (4 chunks per workgroup).  The counts cover
+// only the slots written before this launch ("old" slots); the same launch's
+// insert workgroups route the new due events themselves, so the two never
+// touch the same slot.
+constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8 + 2 * SEGMAX * 4;
 template <int GT>
 __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char* lds, uint64_t* st) {
     constexpr int GR = 4 * (int)CH / GT;
@@ -759,15 +858,34 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
     uint32_t* s_cur = s_cnt + PMAX;                        // [PMAX]
     DueEnt* s_de = (DueEnt*)(s_cur + PMAX);                // [GDMAX]
     uint64_t* s16 = (uint64_t*)(s_de + GDMAX);             // [16]
+    uint32_t* s_start = (uint32_t*)(s16 + 16);             // [SEGMAX] the due list's segments
+    uint32_t* s_lo = s_start + SEGMAX;                     // [SEGMAX]
     const uint64_t S = rs->S, E = rs->E;
-    const uint64_t nd = rs->ndue;
-    const uint64_t c0 = nd * w / nw, c1 = nd * (w + 1) / nw;
     const uint32_t P = d.P;
     // The window's chunks outside the retained bucket go back to the free ring
-    // behind fl_tail, from the due entries as they are staged below (k_plan
-    // advances the tail once the round is done; nothing allocates before it).
-    const uint64_t nfree = rs->nfree;
+    // behind fl_tail as the entries are staged below (the next round's plan
+    // advances the tail; nothing allocates before it).
     const uint32_t tail_r = (uint32_t)(rs->fl_tail % d.NCH);
+    for (uint32_t p = threadIdx.x; p < P; p += GT) {
+        s_cnt[p] = 0;
+        s_cur[p] = 0;
+    }
+    DueList dl;
+    uint64_t nfree;
+    const uint64_t nd = due_segments<GT>(d, dl, s_start, s_lo, s16, &nfree);  // barriers inside
+    if (w == 0 && threadIdx.x == 0) d.rs->nfree = nfree;
+    if (st) {  // the list's shape (SG_STAMPS)
+        st[5] = nd;
+        st[7] = dl.nseg;
+        st[8] = nfree;
+        st[9] = rs->bS;
+        st[10] = rs->bL;
+        st[11] = rs->ret_b;
+        st[12] = rs->pret;
+        st[13] = rs->S;
+        st[14] = rs->E;
+    }
+    const uint64_t c0 = nd * w / nw, c1 = nd * (w + 1) / nw;
     auto free_chunk = [&](const DueEnt& de, uint64_t i) {
         if (i >= nfree || (de.nflags & RETAINED) || de.id >= d.NCH) return;  // not in the prefix
         const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
@@ -792,15 +910,12 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
         // the workgroup's chunks fit in registers: load once, count, reserve, scatter
         const uint32_t nb = (uint32_t)(c1 - c0), tot = nb * CH;
         if (threadIdx.x < nb) {
-            const DueEnt de = d.due[c0 + threadIdx.x];
+            const DueEnt de = due_entry(d, dl, s_start, s_lo, (uint32_t)(c0 + threadIdx.x));
             s_de[threadIdx.x] = de;
             free_chunk(de, c0 + threadIdx.x);
         }
         __syncthreads();
-        if (st) {
-            st[1] = __builtin_amdgcn_s_memrealtime();
-            st[5] = nb;
-        }
+        if (st) st[1] = __builtin_amdgcn_s_memrealtime();
         Rec r[GR];
         uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
 #pragma unroll
@@ -853,7 +968,7 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
         for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
             const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
             __syncthreads();
-            if (threadIdx.x < nb) s_de[threadIdx.x] = d.due[cb + threadIdx.x];
+            if (threadIdx.x < nb) s_de[threadIdx.x] = due_entry(d, dl, s_start, s_lo, (uint32_t)(cb + threadIdx.x));
             __syncthreads();
             gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
         }
@@ -863,7 +978,7 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
             const uint32_t nb = (uint32_t)(c1 - cb < GDMAX ? c1 - cb : GDMAX);
             __syncthreads();
             if (threadIdx.x < nb) {
-                const DueEnt de = d.due[cb + threadIdx.x];
+                const DueEnt de = due_entry(d, dl, s_start, s_lo, (uint32_t)(cb + threadIdx.x));
                 s_de[threadIdx.x] = de;
                 free_chunk(de, cb + threadIdx.x);
             }
@@ -1127,6 +1242,188 @@ __device__ __forceinline__ uint64_t wait_stamp() {
     return __builtin_amdgcn_s_memrealtime();
 }
 
+// ------------------------------------------------------- reservations ----
+// A reserving row's staged events by ring slot (s_bc counts, s_bm min offsets
+// in the bucket; slot (bSr + o) % R is bucket bS + o) into the calendar: one
+// reservation per (row, bucket) in the row's sub-list x, the bucket minima,
+// and the chunks whose first slot falls inside one of the row's reservations.
+// Those come from the row's stash (sid: this lane's stash entry, sn: the
+// stash count, both loaded at launch), beyond it from the free ring (one
+// reservation of its head; avail: the ring's usable end at launch).  k_scatter
+// writes the events into the reserved slots and refills the stashes.  Every
+// thread of the block (T threads) calls it.
+template <int T>
+__device__ void reserve_buckets(const Dev& d, uint32_t row, uint32_t x, const uint32_t* s_bc, const uint32_t* s_bm,
+                                uint64_t bS, uint32_t bSr, uint32_t sid, uint32_t sn, uint64_t avail,
+                                uint32_t* s_ids, uint64_t* s_h, uint64_t* s16) {
+    constexpr uint32_t PER = RMAX / T;
+    const uint32_t R = d.R, NCH = d.NCH, tid = threadIdx.x;
+    const uint64_t W = d.W;
+    uint32_t* bkx = d.bk + (size_t)x * R;
+    uint32_t* wb = d.wbase + (size_t)row * R;
+    if (tid < ST) s_ids[tid] = sid;  // read after the scan's barriers
+    uint32_t first[PER], nn[PER];
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * T;
+        nn[q] = 0;
+        first[q] = 0;
+        const uint32_t c = rb < R ? s_bc[rb] : 0u;
+        if (!c) continue;
+        const uint32_t base = atomicAdd(&bkx[rb], c);
+        wb[rb] = base;
+        const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
+        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
+        const uint32_t f = (base + CH - 1) >> CH_SHIFT, l = (base + c - 1) >> CH_SHIFT;
+        first[q] = f;
+        nn[q] = l + 1 > f ? l + 1 - f : 0u;
+        mine += nn[q];
+    }
+    uint64_t total;
+    uint64_t off = block_excl_scan(mine, s16, &total);  // barriers inside
+    if (total > sn) {  // uniform: beyond the stash, one ring reservation for the row
+        if (tid == 0) *s_h = atomicAdd((unsigned long long*)&d.rs->fl_head, (unsigned long long)(total - sn));
+        __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t rb = tid + q * T;
+        for (uint32_t k = 0; k < nn[q]; ++k, ++off) {
+            uint32_t id = EMPTY;
+            if (off < sn) {
+                id = s_ids[off];
+            } else {
+                const uint64_t pos = *s_h + (off - sn);
+                if (pos < avail) id = d.fring[pos % NCH];
+                else flag(d, OV_POOL);
+            }
+            const uint32_t ci = first[q] + k;
+            if (ci < NCH) d.btab[((size_t)x * R + rb) * NCH + ci] = id;
+            else flag(d, OV_POOL);
+        }
+    }
+    const uint32_t left = total < sn ? sn - (uint32_t)total : 0u;
+    if (tid < left) d.stash[(size_t)row * ST + tid] = s_ids[total + tid];
+    if (tid == 0) d.stn[row] = left;
+}
+
+// ------------------------------------------------------------ plan ----
+// The end of a round (k_proc's last workgroup, one shard; k_plan, several
+// shards or boot): master_slaveFinishedCurrentRound (master.c:450-480), the
+// next window from the MIN next time m and the discovery minimum j (ms), or,
+// mode 1 with `more`, a drain step of the same window.  The window's due
+// chunks are not listed here: every gather workgroup of the following
+// k_scatter derives them from the bucket words (due_segments).
+struct Window {
+    uint64_t S, E, done, min_jump, next_min_jump;
+};
+// The next window from the global MIN and the discovery minimum (ms), given
+// the round state's jump fields (computed in registers; the caller stores).
+__device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t mj0, uint64_t nmj0) {
+    Window w;
+    w.next_min_jump = nmj0;
+    w.min_jump = mj0;
+    uint64_t jump;
+    if (d.window_rule == SG_WINDOW_FIXED) {
+        jump = d.fixed_jump;
+    } else {
+        if (jmin != UINT64_MAX) w.next_min_jump = jmin * SG_ONE_MS;  // master.c:153
+        w.min_jump = w.next_min_jump;                                // master.c:459
+        jump = w.min_jump > 0 ? w.min_jump : 10 * SG_ONE_MS;         // master.c:137
+        if (d.runahead_min > 0 && jump < d.runahead_min) jump = d.runahead_min;
+    }
+    const uint64_t start = minNext;
+    uint64_t end = minNext + jump;  // unsigned wrap as in the reference
+    if (end > d.end_time) end = d.end_time;
+    w.S = start;
+    w.E = end;
+    w.done = start < end ? 0 : 1;
+    return w;
+}
+
+__device__ __forceinline__ uint64_t rmw_read(uint64_t* p) {
+    return atomicAdd((unsigned long long*)p, 0ull);
+}
+// One thread.  ovf: the overflow flags to keep.
+__device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, uint64_t ovf, bool more) {
+    RoundState* rs = d.rs;
+    const uint64_t W = d.W;
+    const uint64_t S0 = rs->S, E0 = rs->E, rounds0 = rs->rounds, nmj0 = rs->next_min_jump, mj0 = rs->min_jump;
+    const uint64_t bS0 = rs->bS, bL0 = rs->bL, ret0 = rs->ret_b, nfree0 = rs->nfree, tail0 = rs->fl_tail;
+    const uint64_t fold0 = rs->fold;
+    rs->overflow = ovf;
+    rs->fold = fold0 + 1;  // one k_scatter follows every plan
+    if (more) {            // drain step: same window, more exchange
+        rs->phase = 1;
+        rs->listed = 0;
+        rs->rmin_todo = 0;
+        return;
+    }
+    uint64_t S = S0, E = E0, done = 0;
+    if (mode != 2) {
+        rs->phase = 0;
+        rs->jmin = j;
+        const Window w = next_window(d, m, j, mj0, nmj0);
+        if (d.wlog && rounds0 < d.wlog_cap) {  // the window just executed
+            d.wlog[2 * rounds0] = S0;
+            d.wlog[2 * rounds0 + 1] = E0;
+        }
+        rs->rounds = rounds0 + 1;
+        rs->last_min = m;
+        rs->next_min_jump = w.next_min_jump;
+        rs->min_jump = w.min_jump;
+        S = w.S;
+        E = w.E;
+        done = w.done | (ovf ? 1u : 0u);  // a capacity ran out: stop, the host reports it
+        rs->S = S;
+        rs->E = E;
+        rs->done = done;
+        // the last gather's chunks are in the ring now
+        rs->fl_tail = tail0 + nfree0;
+        // the executed window: its consumed buckets are skipped by rmin until
+        // the next k_proc resets them; its straddling bucket is spent unless
+        // the new window starts in it
+        rs->pbS = bS0;
+        rs->pbL = bL0;
+        rs->pret = ret0;
+    }
+    const bool listing = mode == 2 || !done;
+    if (listing) {
+        const uint64_t bS = S / W, bL = (E - 1) / W;
+        rs->bS = bS;
+        rs->bL = bL;
+        rs->ret_b = E < (bL + 1) * W ? bL : UINT64_MAX;
+        rs->rmin_todo = mode != 2;
+        if (mode == 2) rs->rmin = SIMTIME_MAX;  // boot: every event is in bucket 0, the window's
+    }
+    rs->listed = listing ? 1 : 0;  // k_scatter gathers and routes for the new window
+}
+
+// Resets the buckets the window before the current one consumed (fully due,
+// or a straddling bucket the current window left behind): no reservation can
+// reach them (new events are at or after the current window's start), and
+// k_scatter's gather and rmin of the previous step are done with them.
+// Threads [0, XS * nb) of one workgroup at launch.
+__device__ void reset_consumed(const Dev& d) {
+    const RoundState* rs = d.rs;
+    const uint64_t pbS = rs->pbS, pbL = rs->pbL, pret = rs->pret, bS = rs->bS;
+    if (pbS == UINT64_MAX) return;
+    const uint32_t R = d.R, nb = (uint32_t)(pbL - pbS + 1);
+    for (uint32_t i = threadIdx.x; i < nb * XS; i += blockDim.x) {
+        const uint64_t b = pbS + i / XS;
+        if (b == pret && pret >= bS) continue;  // still live: the current window starts in it
+        const uint32_t x = i % XS, rb = (uint32_t)(b % R), row = x * R + rb;
+        atomicExch(&d.bk[row], 0u);
+        d.bw[row] = 0;
+        d.bw[(size_t)XS * R + row] = 0;
+        if (x == 0) {
+            atomicExch(&d.btomb[rb], 0u);
+            atomicExch((unsigned long long*)&d.bmin[rb], (unsigned long long)UINT64_MAX);
+        }
+    }
+}
+
 // One workgroup per partition of HP hosts.
 //   sort     the partition's due events by host (LDS counting sort into an LDS
 //            image of the events when they fit, else into part2) and list the
@@ -1264,6 +1561,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
+    // the partition's chunk stash (reserve_buckets), loaded now, used at the end
+    const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
+    const uint64_t ring_end = rs->fl_tail + rs->nfree;  // the gather of the listed window freed nfree more
     for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
     for (uint32_t rb = tid; rb < R; rb += K2_T) {
         s_bc[rb] = 0;
@@ -1388,6 +1688,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
+    if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
 #pragma unroll
         for (uint32_t q = 0; q < EPT; ++q) {
@@ -1764,15 +2065,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
-    uint32_t* wb = d.wbase + (size_t)p * R;
-    uint32_t* xd = d.bdel + (size_t)(p % XS) * R;
-    for (uint32_t rb = tid; rb < R; rb += K2_T) {
-        const uint32_t c = s_bc[rb];
-        if (!c) continue;
-        const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
-        wb[rb] = atomicAdd(&xd[rb], c);
-        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
-    }
+    __shared__ uint32_t s_ids[ST];
+    __shared__ uint64_t s_h;
+    reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
     if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid < NCTR + 2) {
         const int i = tid;
@@ -1790,31 +2085,47 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
-    if (d.xsend) {
-        // The last workgroup to finish writes the exchange block headers.  No
-        // fences (an L2 write-back per workgroup costs more than a launch):
-        // everything it reads from the others was performed by device-scope
-        // atomics (MIN accumulators, outbox counts, flags), which the barrier's
-        // vmcnt(0) completes before this workgroup takes its ticket.  No
-        // workgroup waits for another.
+    {
+        // The last workgroup to finish ends the round: one shard, the next
+        // window (publish_window); several, the exchange block headers.  No fences (an L2 write-back per workgroup costs more than
+        // a launch): everything it reads from the others was performed by
+        // device-scope atomics (MIN accumulators, reservations, outbox counts,
+        // flags), which every wave waits for (vmcnt(0)) before the workgroup
+        // takes its ticket.  No workgroup waits for another.
         __shared__ bool s_lastwg;
+        __shared__ uint64_t s_mj[2];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0)
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
         __syncthreads();
         if (s_lastwg) {
-            uint64_t m = rs->xcarry;  // carry min (k_scatter's atomics, a kernel ago)
-            const uint64_t em = atomic_read(&rs->xacc[0]), jm = atomic_read(&rs->xacc[1]);
-            m = em < m ? em : m;
-            m = rs->rmin < m ? rs->rmin : m;
-            m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
-            const uint64_t j = rs->jmin < jm ? rs->jmin : jm;
-            write_headers(d, m, j);
+            uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
+            if (pst) pst[0] = __builtin_amdgcn_s_memrealtime();
             if (tid == 0) {
+                // the three accumulators in one round trip
+                const uint64_t em = rmw_read(&rs->xacc[0]), jm = rmw_read(&rs->xacc[1]);
+                const uint64_t ovf = d.xsend ? 0 : rmw_read(&rs->overflow);
+                uint64_t m = rs->xcarry;  // carry min (k_scatter's atomics, a kernel ago)
+                m = em < m ? em : m;
+                m = rs->rmin < m ? rs->rmin : m;
+                m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+                const uint64_t j = rs->jmin < jm ? rs->jmin : jm;
                 rs->ticket = 0;
                 rs->xacc[0] = UINT64_MAX;
                 rs->xacc[1] = UINT64_MAX;
+                if (!d.xsend) {
+                    rs->xcarry = UINT64_MAX;  // k_scatter's gather and inserts refill it
+                    publish_window(d, 0, m, j, ovf, false);
+                }
+                s_mj[0] = m;
+                s_mj[1] = j;
             }
+            if (d.xsend) {
+                __syncthreads();
+                write_headers(d, s_mj[0], s_mj[1]);
+            }
+            if (pst) pst[7] = wait_stamp();
         }
     }
     if (stamp && tid == 0) {
@@ -1882,8 +2193,13 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     __shared__ uint32_t s_bc[RMAX];  // per bucket: events of this workgroup
     __shared__ uint32_t s_bm[RMAX];  // per bucket: min time offset within the bucket
     __shared__ uint64_t s16[16];
+    __shared__ uint32_t s_ids[ST];
+    __shared__ uint64_t s_h;
     const uint64_t W = d.W, bS = rs->bS;
     const uint32_t R = d.R;
+    const uint32_t row = d.P + blockIdx.x;
+    const uint32_t stash_id = d.stash[(size_t)row * ST + (threadIdx.x & (ST - 1))], stash_n = d.stn[row];
+    const uint64_t ring_end = rs->fl_tail + rs->nfree;
     if (blockIdx.x == 0 && threadIdx.x == 0) rs->ins_local = rs->phase == 0;
     for (uint32_t b = threadIdx.x; b < R; b += K3_T) {
         s_bc[b] = 0;
@@ -1908,15 +2224,8 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
         atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
     }
     __syncthreads();
-    uint32_t* wb = d.wbase + (size_t)(d.P + blockIdx.x) * R;
-    uint32_t* xd = d.bdel + (size_t)(blockIdx.x % XS) * R;
-    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) {
-        const uint32_t c = s_bc[rb];
-        if (!c) continue;
-        const uint64_t b = bS + ((rb + R - (uint32_t)(bS % R)) % R);  // absolute bucket of slot rb
-        wb[rb] = atomicAdd(&xd[rb], c);
-        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
-    }
+    reserve_buckets<K3_T>(d, row, blockIdx.x % XS, s_bc, s_bm, bS, (uint32_t)(bS % R), stash_id, stash_n, ring_end,
+                          s_ids, &s_h, s16);
 }
 
 // k_scatter: new (and received) events into the calendar, fused with the
@@ -1933,7 +2242,9 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
 // gather's leftovers do.
 constexpr int SU = 4;  // events per thread in flight
 constexpr size_t INS_LDS = (RMAX + 2 * PMAX) * 4 + 16 * 8 + MAXG * 4;
-constexpr size_t SCAT_LDS = INS_LDS > GATHER_LDS ? INS_LDS : GATHER_LDS;
+constexpr size_t REFILL_LDS = 16 * 8 + 8 + 2 * (PMAX + G3MAX) * 4;
+constexpr size_t SCAT_LDS0 = INS_LDS > GATHER_LDS ? INS_LDS : GATHER_LDS;
+constexpr size_t SCAT_LDS = SCAT_LDS0 > REFILL_LDS ? SCAT_LDS0 : REFILL_LDS;
 
 struct Route {
     bool listed;
@@ -1947,7 +2258,7 @@ struct Route {
 // calls it): slot from the (partition, bucket) reservation cursor, chunk
 // from k_plan's allocation; due events routed.  Returns nothing; carry min
 // and tombstones accumulate in smin / ntomb.
-__device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t* s_cur, uint32_t* s_pc,
+__device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t x, uint32_t* s_cur, uint32_t* s_pc,
                                              uint32_t* s_pk, const bool (&v)[SU], const uint64_t (&t)[SU],
                                              const uint64_t (&k)[SU], const uint32_t (&dl)[SU], uint64_t& smin,
                                              uint64_t& ntomb) {
@@ -1978,17 +2289,17 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (v[q] && !due[q] && in_ret) smin = t[q] < smin ? t[q] : smin;
         if (due[q]) atomicAdd(&s_pc[part_of(d, dl[q])], 1u);
     }
-    uint32_t na[SU], id[SU];
+    uint32_t id[SU];
+    const uint32_t* tab = d.btab + (size_t)x * R * d.NCH;
 #pragma unroll
     for (int q = 0; q < SU; ++q) {
         const uint32_t ci = pos[q] >> CH_SHIFT;
-        na[q] = d.nal[rb[q]];
-        id[q] = d.btab[(size_t)rb[q] * d.NCH + (ci < d.NCH ? ci : d.NCH - 1)];
+        id[q] = tab[(size_t)rb[q] * d.NCH + (ci < d.NCH ? ci : d.NCH - 1)];
     }
 #pragma unroll
     for (int q = 0; q < SU; ++q) {
-        // beyond the allocation only when the pool ran out (k_plan flagged it)
-        if (!write[q] || (pos[q] >> CH_SHIFT) >= na[q] || id[q] >= d.NCH) continue;
+        // no chunk only when the pool ran out (reserve_buckets flagged it)
+        if (!write[q] || (pos[q] >> CH_SHIFT) >= d.NCH || id[q] >= d.NCH) continue;
         Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
         ntomb += due[q];
         d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r;
@@ -2052,40 +2363,127 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     uint64_t* st = d.stamps && threadIdx.x == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
     if (st) {
         st[0] = __builtin_amdgcn_s_memrealtime();
-        st[4] = blk == gridDim.x - 1 ? 3 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
+        st[4] = blk == gridDim.x - 1 ? 3 : blk == gridDim.x - 2 ? 4 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
         st[1] = st[2] = st[3] = st[6] = st[0];
         st[5] = 0;
     }
+    const uint32_t tid = threadIdx.x;
     if (blk == gridDim.x - 1) {
         uint64_t* s16 = (uint64_t*)lds;
-        if (ro.listed && d.outn && threadIdx.x < d.G) {  // the next step processes: outboxes refill
-            d.outn[threadIdx.x] = 0;
-            d.sent[threadIdx.x] = 0;
+        if (ro.listed && d.outn && tid < d.G) {  // the next step processes: outboxes refill
+            d.outn[tid] = 0;
+            d.sent[tid] = 0;
         }
-        // rmin for the window k_plan just listed: the first non-empty bucket in
-        // (bL, bS + R) and its min time.  k_plan wrote the metadata back; this
-        // launch changes only the straddling bucket's, so the counts read are final.
-        if (!rs->rmin_todo) return;
-        const uint64_t bS = rs->bS, bL = rs->bL;
-        const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
-        uint64_t first = UINT64_MAX;
-        for (uint32_t o = threadIdx.x + 1; o + span < R; o += K3_T) {
-            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
-            if (d.bcnt[rb] > d.btomb[rb]) {
-                const uint64_t b = bL + o;
-                first = b < first ? b : first;
+        if (d.wtime && !recv) {
+            // one shard: the round k_proc just ended; barrier wait
+            // (scheduler.c:380-389): each partition idles from its end to the
+            // round's last partition end
+            uint64_t mx = 0;
+            for (uint32_t p = tid; p < d.P; p += K3_T) {
+                const uint64_t t = d.wtime[2 * (size_t)d.P + p];
+                mx = t > mx ? t : mx;
             }
+            mx = ~block_min(~mx, s16);  // max; barriers inside
+            for (uint32_t p = tid; p < d.P; p += K3_T) d.wtime[(size_t)d.P + p] += mx - d.wtime[2 * (size_t)d.P + p];
         }
-        first = block_min(first, s16);  // barriers inside
-        if (threadIdx.x == 0) {
-            rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : d.bmin[first % R];
+        // rmin for the window just listed: the min time of the buckets beyond
+        // it, (bL, bS + R), but those of the window before it (consumed, reset
+        // by the next k_proc).  The rest hold no tombstones or were reset, and
+        // this launch changes only the straddling bucket's minimum, so the
+        // minima read are final.
+        if (!rs->rmin_todo) return;
+        const uint64_t bS = rs->bS, bL = rs->bL, pbS = rs->pbS, pbL = rs->pbL;
+        const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
+        uint64_t mn = UINT64_MAX;
+        for (uint32_t o = tid + 1; o + span < R; o += K3_T) {
+            const uint64_t b = bL + o - R;  // the ring slot's consumed bucket, if any
+            if (pbS != UINT64_MAX && b >= pbS && b <= pbL) continue;
+            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
+            const uint64_t v = d.bmin[rb];
+            mn = v < mn ? v : mn;
+        }
+        mn = block_min(mn, s16);  // barriers inside
+        if (tid == 0) {
+            rs->rmin = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
             rs->rmin_todo = 0;
             if (st) st[3] = __builtin_amdgcn_s_memrealtime();
         }
         return;
     }
+    if (blk == gridDim.x - 2) {
+        // fold: every slot reserved so far is written by this launch, so the
+        // next step's gather may read them all
+        {
+            const uint32_t nx = (uint32_t)((rs->fold & 1) ^ 1);
+            for (uint32_t i = tid; i < XS * R; i += K3_T) d.bw[(size_t)nx * XS * R + i] = d.bk[i];
+        }
+        // stash refill: every reserving row back to ST chunk ids, one ring
+        // reservation for all of them; the ring is usable up to the tail the
+        // plan set (this launch's gather frees more behind it).  The ids are
+        // copied as one flat list of (row, slot) entries, every load of a
+        // batch in flight together.
+        constexpr uint32_t RPT = (PMAX + G3MAX + K3_T - 1) / K3_T;
+        constexpr int FU = 8;
+        uint64_t* s16 = (uint64_t*)lds;
+        uint64_t* s_hh = s16 + 16;
+        uint32_t* s_have = (uint32_t*)(s_hh + 1);  // [PMAX + G3MAX]
+        uint32_t* s_roff = s_have + PMAX + G3MAX;  // [PMAX + G3MAX] first list entry of each row
+        const uint32_t rows = d.P + (d.outn ? d.G3 : 0u), NCH = d.NCH;
+        const uint64_t avail = rs->fl_tail;
+        uint32_t have[RPT];
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < RPT; ++q) {
+            const uint32_t r = tid + q * K3_T;
+            have[q] = r < rows ? d.stn[r] : ST;
+            mine += ST - have[q];
+        }
+        uint64_t total;
+        uint32_t off = (uint32_t)block_excl_scan(mine, s16, &total);  // barriers inside
+        if (total == 0) return;  // uniform
+#pragma unroll
+        for (uint32_t q = 0; q < RPT; ++q) {
+            const uint32_t r = tid + q * K3_T;
+            if (r < rows) {
+                s_have[r] = have[q];
+                s_roff[r] = off;
+            }
+            off += ST - have[q];
+        }
+        if (tid == 0) *s_hh = atomicAdd((unsigned long long*)&rs->fl_head, (unsigned long long)total);
+        __syncthreads();
+        const uint64_t h = *s_hh;
+        const uint32_t hr = (uint32_t)(h % NCH);
+        if (h + total > avail && tid == 0) flag(d, OV_POOL);
+        for (uint32_t f0 = 0; f0 < rows * ST; f0 += K3_T * FU) {
+            uint32_t id[FU], dst[FU];
+            bool v[FU];
+#pragma unroll
+            for (int u = 0; u < FU; ++u) {
+                const uint32_t f = f0 + tid + u * K3_T, r = f / ST < rows ? f / ST : 0u, k = f % ST;
+                const uint32_t e = s_roff[r] + (k - s_have[r]);  // list entry (when k >= have)
+                v[u] = f < rows * ST && k >= s_have[r] && h + e < avail;
+                const uint32_t pos = hr + (v[u] ? e : 0u);  // e < total <= NCH: one wrap at most
+                id[u] = d.fring[pos >= NCH ? pos - NCH : pos];  // unconditional (clamped)
+                dst[u] = r * ST + k;
+            }
+#pragma unroll
+            for (int u = 0; u < FU; ++u)
+                if (v[u]) d.stash[dst[u]] = id[u];
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < RPT; ++q) {
+            const uint32_t r = tid + q * K3_T;
+            if (r >= rows || have[q] == ST) continue;
+            const uint64_t e0 = h + s_roff[r];  // the row's first entry's ring position
+            const uint64_t got = e0 >= avail ? 0 : std::min<uint64_t>(avail - e0, ST - have[q]);
+            d.stn[r] = have[q] + (uint32_t)got;
+        }
+        return;
+    }
+    const uint32_t gx = gridDim.x - 2;  // gather workgroups [g0, gx)
     if (blk >= g0) {
-        if (ro.listed) gather_role<K3_T>(d, blk - g0, gridDim.x - 1 - g0, lds, st);
+        if (ro.listed) gather_role<K3_T>(d, blk - g0, gx - g0, lds, st);
         if (st) st[3] = wait_stamp();
         return;
     }
@@ -2102,9 +2500,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         if (n == 0) return;  // uniform: nothing routed, nothing to finish
         const uint64_t S = rs->ins_S;
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
-        const uint32_t* xo = d.bxoff + (size_t)(blk % XS) * R;
         Rec r[SU];
-        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
+        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
         for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
         __syncthreads();
         if (st) {
@@ -2127,7 +2524,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
                 k[q] = r[q].k;
                 dl[q] = (uint32_t)(r[q].a >> 40);
             }
-            insert_batch(d, ro, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+            insert_batch(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
         if (st) st[2] = wait_stamp();
         insert_finish(d, ro, smin, ntomb, s16);
@@ -2136,8 +2533,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     }
     // the received blocks' events, split evenly over G3 workgroups
     const uint32_t g3 = d.G3, w = blk - d.P;
-    const uint32_t* xo = d.bxoff + (size_t)(w % XS) * R;
-    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb] + xo[rb];
+    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
     const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
@@ -2152,49 +2548,15 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
             dl[q] = 0;
             v[q] = idx < hi && recv_event(d, recv, s_off, (uint32_t)idx, t[q], k[q], dl[q]);
         }
-        insert_batch(d, ro, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+        insert_batch(d, ro, w % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
     }
     insert_finish(d, ro, smin, ntomb, s16);
 }
 
 // ----------------------------------------------------------------- plan ----
-// master_slaveFinishedCurrentRound (master.c:450-480) on a reduced triple.
-struct Window {
-    uint64_t S, E, done, min_jump, next_min_jump;
-};
-// The next window from the global MIN and the discovery minimum (ms), given
-// the round state's jump fields (computed in registers; the caller stores).
-__device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t mj0, uint64_t nmj0) {
-    Window w;
-    w.next_min_jump = nmj0;
-    w.min_jump = mj0;
-    uint64_t jump;
-    if (d.window_rule == SG_WINDOW_FIXED) {
-        jump = d.fixed_jump;
-    } else {
-        if (jmin != UINT64_MAX) w.next_min_jump = jmin * SG_ONE_MS;  // master.c:153
-        w.min_jump = w.next_min_jump;                                // master.c:459
-        jump = w.min_jump > 0 ? w.min_jump : 10 * SG_ONE_MS;         // master.c:137
-        if (d.runahead_min > 0 && jump < d.runahead_min) jump = d.runahead_min;
-    }
-    const uint64_t start = minNext;
-    uint64_t end = minNext + jump;  // unsigned wrap as in the reference
-    if (end > d.end_time) end = d.end_time;
-    w.S = start;
-    w.E = end;
-    w.done = start < end ? 0 : 1;
-    return w;
-}
-
-__device__ __forceinline__ void reset_bucket(const Dev& d, uint32_t rb) {
-    d.nal[rb] = 0;
-    d.bcnt[rb] = 0;
-    d.btomb[rb] = 0;
-    d.bmin[rb] = UINT64_MAX;
-}
-
-// The local MIN terms of a round: carry min (k_gather), emitted min and
-// discovery min (k_proc), and the buckets beyond the window (rmin).
+// The local MIN terms of a round: carry min (k_scatter's gather and inserts),
+// emitted min and discovery min (k_proc), and the buckets beyond the window
+// (rmin).
 __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
     uint64_t mm = d.rs->xcarry, jj = UINT64_MAX;
     for (uint32_t i = threadIdx.x; i < d.P; i += blockDim.x) {
@@ -2210,71 +2572,18 @@ __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t&
     j = rs->jmin < j ? rs->jmin : j;
 }
 
-// k_plan keeps the ring's bucket metadata in LDS for the whole launch: one
-// coalesced load, scans and updates in LDS, one write-back.
-struct PlanLds {
-    uint32_t cnt[RMAX], tomb[RMAX], nal[RMAX];
-    uint32_t old[RMAX];  // count before this step's reservations: the slots already written
-    uint32_t off[RMAX];  // allocation: first new chunk of each bucket in this launch's run
-    uint32_t own[RMAX];  // allocation: new chunk i's bucket | its index among the bucket's new ones << 12
-    uint64_t mn[RMAX];
-    uint32_t fr[PL_T];   // the free ring's first PL_T entries from the head, read at launch
-};
-
-// mode 0: single shard, end of round.  mode 1: multi-shard, window from the
-// received headers (or the end of a drain step).  mode 2: boot (list the
-// first window).  Values one thread computes for the others go through LDS.
+// k_plan: the multi-shard end of a step (mode 1: the next window from the G
+// received headers, the MIN all-reduce of scheduler.c:386-408 carried by the
+// all-to-all, or a drain step) and the boot listing (mode 2).  One workgroup.
+// A single-shard round ends in k_proc's last workgroup instead.
 __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int mode) {
     RoundState* rs = d.rs;
     if (rs->done) return;
-    __shared__ __align__(16) PlanLds B;
     __shared__ uint64_t s16[16];
-    __shared__ uint64_t s_head, s_tail, s_S, s_E, s_done, s_more, s_spent, s_m, s_j, s_ovf;
-    __shared__ uint64_t s_nbS, s_nbL;                    // the window's first and last bucket
-    __shared__ uint32_t s_nbSr, s_headr, s_tailr;        // nbS % R, head % NCH, tail % NCH
-    constexpr uint32_t PER = (RMAX + PL_T - 1) / PL_T;
-    const uint32_t R = d.R, NCH = d.NCH;
-    const uint64_t W = d.W;
+    __shared__ uint64_t s_mj[4];
     const uint32_t tid = threadIdx.x;
     uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
-#define PSTAMP(k) \
-    if (pst) pst[k] = __builtin_amdgcn_s_memrealtime()
-    PSTAMP(0);
-    // bucket metadata: loads issued together with reduce_local's, LDS stores after
-    uint32_t rc[PER], rt[PER], rn[PER], ro[PER];
-    uint64_t rm[PER];
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint32_t rb = tid + q * PL_T;
-        if (rb < R) {
-            rc[q] = d.bcnt[rb];
-            ro[q] = rc[q];
-            rt[q] = d.btomb[rb];
-            rn[q] = d.nal[rb];
-            rm[q] = d.bmin[rb];
-        }
-    }
-    // this step's shard reservations, loaded unconditionally (clamped) so all
-    // PER * XS loads are in flight together; folded below
-    uint32_t v[PER][XS];
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint32_t rb = tid + q * PL_T < R ? tid + q * PL_T : R - 1;
-#pragma unroll
-        for (uint32_t x = 0; x < XS; ++x) v[q][x] = d.bdel[(size_t)x * R + rb];
-    }
-    // the free ring from the head, for the allocation below (nothing writes
-    // the ring in this launch before the allocation reads it)
-    // the previous listing's fields, read now with the rest (this launch
-    // rewrites them only at its own listing)
-    const uint64_t ndueb0 = rs->ndueb, nfree0 = rs->nfree, retb0 = rs->ret_b;
-    uint32_t fr0;
-    {
-        const uint64_t h0 = rs->fl_head;
-        uint32_t pos = (uint32_t)(h0 % NCH) + tid;  // one 64-bit remainder, uniform
-        if (pos >= NCH) pos = NCH >= PL_T ? pos - NCH : pos % NCH;  // NCH may be below PL_T (small engines)
-        fr0 = d.fring[pos];
-    }
+    if (pst) pst[0] = __builtin_amdgcn_s_memrealtime();
     if (mode == 1 && d.check) {
         // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in this
         // shard's headers, from device-scope atomics it read without a fence,
@@ -2287,21 +2596,8 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         if (tid == 0 && ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj)) flag(d, OV_BUG);
     }
     if (tid == 0) {
-        // every round-state field the window needs in one round trip; the new
-        // values are computed in registers and stored once (a load after a
-        // store to the round state would be a memory round trip of its own)
-        const uint64_t S0 = rs->S, E0 = rs->E, rounds0 = rs->rounds, nmj0 = rs->next_min_jump, mj0 = rs->min_jump;
-        const uint64_t jmin0 = rs->jmin, ovf0 = rs->overflow, rmin0 = rs->rmin;
-        const uint64_t xc0 = rs->xcarry, xa0 = rs->xacc[0], xa1 = rs->xacc[1];
-        s_head = rs->fl_head;
-        s_tail = rs->fl_tail;
-        s_S = S0;
-        s_E = E0;
-        s_done = 0;
-        s_more = 0;
-        s_spent = UINT64_MAX;
+        uint64_t more = 0, m = UINT64_MAX, j = UINT64_MAX, ovf = rs->overflow;
         if (mode == 1) {
-            uint64_t more = 0, m = UINT64_MAX, j = UINT64_MAX, ovf = 0;
             for (uint32_t p = 0; p < d.G; ++p) {
                 const int64_t* blk = recv + (size_t)p * d.xrows * 3;
                 more |= (uint64_t)blk[H_MORE];
@@ -2316,308 +2612,28 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
                 d.sent[q] += left < d.xcap ? left : d.xcap;
             }
             rs->steps += 1;
-            s_more = more;
-            s_m = m;
-            s_j = j;
-            s_ovf = ovf;
-        } else if (mode == 0) {
-            // the local MIN terms, accumulated by k_scatter's and k_proc's
-            // workgroups with device-scope atomics (reduce_local's terms);
-            // only this thread reads them, so it resets them too
-            uint64_t m = xc0 < xa0 ? xc0 : xa0;
-            m = rmin0 < m ? rmin0 : m;
-            s_m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
-            s_j = jmin0 < xa1 ? jmin0 : xa1;
-            s_ovf = ovf0;
-            rs->xcarry = UINT64_MAX;
-            rs->xacc[0] = UINT64_MAX;
-            rs->xacc[1] = UINT64_MAX;
+            if (!more) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
         }
-        // the next window (master.c:450-480), under the other threads' loads
-        if (mode == 1 && s_more) {  // drain step: same window, more exchange
-            rs->phase = 1;
-            rs->overflow = ovf0 | s_ovf;
-        } else if (mode != 2) {
-            if (mode == 1) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
-            rs->phase = 0;
-            rs->jmin = s_j;
-            const Window w = next_window(d, s_m, s_j, mj0, nmj0);
-            const uint64_t ovf = ovf0 | s_ovf;
-            if (d.wlog && rounds0 < d.wlog_cap) {  // the window just executed
-                d.wlog[2 * rounds0] = S0;
-                d.wlog[2 * rounds0 + 1] = E0;
-            }
-            rs->overflow = ovf;
-            rs->rounds = rounds0 + 1;
-            rs->last_min = s_m;
-            rs->next_min_jump = w.next_min_jump;
-            rs->min_jump = w.min_jump;
-            rs->S = w.S;
-            rs->E = w.E;
-            const uint64_t done = w.done | (ovf ? 1u : 0u);  // a capacity ran out: stop, the host reports it
-            rs->done = done;
-            s_S = w.S;
-            s_E = w.E;
-            s_done = done;
-        }
-        // the bucket arithmetic every thread needs, divided once here
-        const uint64_t nbS = s_S / W;
-        s_nbS = nbS;
-        s_nbL = (s_E - 1) / W;
-        s_nbSr = (uint32_t)(nbS % R);
-        s_headr = (uint32_t)(s_head % NCH);
-        s_tailr = (uint32_t)(s_tail % NCH);
-    }
-    // fold: each shard's range starts where the previous one's ends (k_scatter
-    // adds it to the workgroup's own base)
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint32_t rb = tid + q * PL_T;
-        if (rb < R) {
-            uint32_t base = rc[q];
-#pragma unroll
-            for (uint32_t x = 0; x < XS; ++x) {
-                if (v[q][x]) {
-                    d.bxoff[(size_t)x * R + rb] = base;
-                    d.bdel[(size_t)x * R + rb] = 0;
-                }
-                base += v[q][x];
-            }
-            rc[q] = base;
-        }
-    }
-    B.fr[tid] = fr0;
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint32_t rb = tid + q * PL_T;
-        if (rb < R) {
-            B.cnt[rb] = rc[q];
-            B.old[rb] = ro[q];
-            B.tomb[rb] = rt[q];
-            B.nal[rb] = rn[q];
-            B.mn[rb] = rm[q];
-        }
+        s_mj[0] = m;
+        s_mj[1] = j;
+        s_mj[2] = ovf;
+        s_mj[3] = more;
     }
     __syncthreads();
-    PSTAMP(1);
-    const bool round_done = mode == 0 || (mode == 1 && !s_more);
-    if (d.wtime && round_done) {
+    const bool more = s_mj[3] != 0;
+    if (d.wtime && mode == 1 && !more) {
         // barrier wait (scheduler.c:380-389): each partition idles from its end
         // to the round's last partition end
-        uint64_t m = 0;
+        uint64_t mx = 0;
         for (uint32_t p = tid; p < d.P; p += PL_T) {
             const uint64_t t = d.wtime[2 * (size_t)d.P + p];
-            m = t > m ? t : m;
+            mx = t > mx ? t : mx;
         }
-        m = ~block_min(~m, s16);  // max; barriers inside
-        for (uint32_t p = tid; p < d.P; p += PL_T) d.wtime[(size_t)d.P + p] += m - d.wtime[2 * (size_t)d.P + p];
+        mx = ~block_min(~mx, s16);  // max; barriers inside
+        for (uint32_t p = tid; p < d.P; p += PL_T) d.wtime[(size_t)d.P + p] += mx - d.wtime[2 * (size_t)d.P + p];
     }
-    // listed: a new window (or the first one, at boot)
-    const bool list = mode == 2 || (round_done && !s_done);
-    if (round_done) {
-        // k_gather returned the window's chunks (not the retained bucket's) to
-        // the ring behind the tail: take them, and reset the consumed buckets
-        const uint64_t ndb = ndueb0;
-        for (uint64_t i = tid; i < ndb; i += PL_T) {
-            const uint32_t rb = d.dueb[i];
-            B.cnt[rb] = 0;
-            B.tomb[rb] = 0;
-            B.nal[rb] = 0;
-            B.mn[rb] = UINT64_MAX;
-        }
-        if (tid == 0) {
-            s_tail = s_tail + nfree0;
-            s_tailr = (uint32_t)(s_tail % NCH);
-        }
-        __syncthreads();
-    }
-    PSTAMP(2);
-    PSTAMP(4);
-    // the new window's buckets (when listed): [nbS, nbL], nbL straddling E or not
-    const uint64_t nbS = s_nbS, nbL = s_nbL;
-    const bool nstraddle = s_E < (nbL + 1) * W;
-    if (mode != 2) {
-        // every bucket gets the chunks its count needs (k_proc / k_count
-        // reserved the slots), from the ring: per-bucket offsets into the run
-        // of new chunks, then one cooperative pass over the run (a bucket
-        // search in LDS per chunk) so every ring load is independent.  A
-        // bucket the new window takes whole gets none: k_scatter routes its
-        // new events straight to the host partitions and never writes them.
-        // a thread's PER = 4 buckets are adjacent: one 16-B LDS access per array
-        static_assert(PER == 4, "allocation pass assumes four buckets per thread");
-        const uint4 c4 = reinterpret_cast<const uint4*>(B.cnt)[tid];
-        const uint4 n4 = reinterpret_cast<const uint4*>(B.nal)[tid];
-        const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w}, nq[4] = {n4.x, n4.y, n4.z, n4.w};
-        uint32_t need[PER], offq[PER];
-        uint64_t mine = 0;
-        const uint32_t nbSr = s_nbSr;
-#pragma unroll
-        for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t rb = tid * PER + q;
-            need[q] = 0;
-            if (rb < R) {
-                const uint64_t want = ((uint64_t)cq[q] + CH - 1) >> CH_SHIFT;
-                const uint32_t w = (uint32_t)(want < NCH ? want : NCH);
-                need[q] = w > nq[q] ? w - nq[q] : 0;
-                const uint64_t o = rb >= nbSr ? rb - nbSr : rb + R - nbSr;  // bucket nbS + o
-                if (list && o <= nbL - nbS && !(nstraddle && o == nbL - nbS)) need[q] = 0;
-            }
-            mine += need[q];
-        }
-        uint64_t total;
-        PSTAMP(8);
-        uint64_t off = block_excl_scan(mine, s16, &total);
-        PSTAMP(9);
-        // new chunk i's owner: an LDS table when the run fits it (every steady
-        // round), else a bucket search per chunk (the boot round)
-        const bool table = total <= RMAX;
-#pragma unroll
-        for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t rb = tid * PER + q;
-            offq[q] = (uint32_t)off;
-            if (table)
-                for (uint32_t k = 0; k < need[q]; ++k) B.own[off + k] = rb | (k << 12);
-            off += need[q];
-        }
-        reinterpret_cast<uint4*>(B.off)[tid] = make_uint4(offq[0], offq[1], offq[2], offq[3]);
-        __syncthreads();
-        PSTAMP(10);
-        const uint64_t head = s_head, avail = s_tail - head;
-        const uint32_t give = (uint32_t)(total < avail ? total : avail);
-        const uint32_t head_r = s_headr;
-        for (uint32_t i = tid; i < give; i += PL_T) {
-            uint32_t lo, k;
-            if (table) {
-                const uint32_t o = B.own[i];
-                lo = o & 0xFFFu;
-                k = o >> 12;
-            } else {
-                lo = 0;
-                uint32_t hi = R - 1;  // the last bucket whose run starts at or before i
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi + 1) >> 1;
-                    if (B.off[mid] <= i) lo = mid; else hi = mid - 1;
-                }
-                k = i - B.off[lo];
-            }
-            const uint32_t pos = head_r + i;  // give <= NCH: one wrap at most
-            const uint32_t id = i < PL_T ? B.fr[i] : d.fring[pos >= NCH ? pos - NCH : pos];
-            d.btab[(size_t)lo * NCH + B.nal[lo] + k] = id;
-        }
-        __syncthreads();
-        PSTAMP(11);
-        uint32_t gq[PER];
-#pragma unroll
-        for (uint32_t q = 0; q < PER; ++q) {
-            const uint32_t o = offq[q];
-            gq[q] = nq[q] + (give <= o ? 0 : (give - o < need[q] ? give - o : need[q]));
-        }
-        reinterpret_cast<uint4*>(B.nal)[tid] = make_uint4(gq[0], gq[1], gq[2], gq[3]);
-        if (tid == 0) {  // s_head: read again only by this thread
-            if (total > avail) flag(d, OV_POOL);
-            s_head = head + give;
-        }
-        __syncthreads();
-    }
-    PSTAMP(3);
-    PSTAMP(4);
-    if (list) {
-        // list the due chunks of the new window [S, E): the slots written
-        // before this launch (old); k_scatter routes the new ones itself
-        const uint64_t S = s_S, E = s_E;
-        const uint64_t bS = s_nbS, bL = s_nbL;
-        const uint32_t bSr = s_nbSr;
-        // ring slot of bucket bS + o (o < R)
-        auto ring_of = [&](uint64_t o) -> uint32_t { const uint32_t r = bSr + (uint32_t)o; return r >= R ? r - R : r; };
-        const uint64_t pr = retb0;
-        if (pr != UINT64_MAX && pr < bS) {  // last round's straddling bucket is spent
-            const uint32_t rb = (uint32_t)(pr % R);
-            const uint32_t nc = B.nal[rb];
-            const uint64_t tail = s_tail;
-            const uint32_t tail_r = s_tailr;
-            for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-                const uint32_t pos = tail_r + ci;  // nc <= NCH: one wrap at most
-                d.fring[pos >= NCH ? pos - NCH : pos] = d.btab[(size_t)rb * NCH + ci];
-            }
-            __syncthreads();
-            if (tid == 0) {
-                s_tail = tail + nc;
-                s_spent = rb;
-                B.cnt[rb] = 0;
-                B.tomb[rb] = 0;
-                B.nal[rb] = 0;
-                B.mn[rb] = UINT64_MAX;
-            }
-            __syncthreads();
-        }
-        // Fully due buckets keep their tables until the next plan (k_scatter of
-        // this round still writes the events k_count counted into them).
-        const bool straddle = E < (bL + 1) * W;
-        uint64_t nd = 0, ndb = 0, nf = 0;
-        for (uint64_t b = bS; b <= bL; ++b) {
-            const uint32_t rb = ring_of(b - bS);
-            const uint32_t c = B.cnt[rb], co = B.old[rb];
-            const bool ret = straddle && b == bL;
-            // a retained bucket lists the chunks holding old slots; a bucket
-            // taken whole lists every chunk, all of them go back to the ring
-            const uint32_t nc = ret ? std::min<uint32_t>(B.nal[rb], (co + CH - 1) >> CH_SHIFT) : B.nal[rb];
-            const uint32_t* tab = d.btab + (size_t)rb * NCH;
-            for (uint32_t ci = tid; ci < nc; ci += PL_T) {
-                const uint32_t left = co > (ci << CH_SHIFT) ? co - (ci << CH_SHIFT) : 0u;
-                const uint32_t n = left < CH ? left : CH;
-                d.due[nd + ci] = DueEnt{tab[ci], n | (ret ? RETAINED : 0u), b * W};
-            }
-            nd += nc;
-            nf += ret ? 0 : nc;
-            if (tid == 0 && !ret && c) d.dueb[ndb] = rb;
-            if (!ret && c) ++ndb;
-        }
-        __syncthreads();
-        PSTAMP(5);
-        if (straddle && tid == 0) B.mn[ring_of(bL - bS)] = UINT64_MAX;  // k_gather's carry min and k_count restore it
-        // exact min beyond the window: the first non-empty bucket in (bL, bS + R).
-        // Off the plan's critical path: k_scatter's last workgroup finds it
-        // from the written-back metadata (first_live_bucket) — except at boot,
-        // where no k_scatter follows.
-        uint64_t first = UINT64_MAX;
-        if (mode == 2) {
-            const uint32_t span = (uint32_t)(bL - bS), bLr = ring_of(bL - bS);
-            for (uint32_t o = tid + 1; o + span < R; o += PL_T) {
-                const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
-                if (rb == s_spent) continue;
-                if (B.cnt[rb] > B.tomb[rb]) {
-                    const uint64_t b = bL + o;
-                    first = b < first ? b : first;
-                }
-            }
-            first = block_min(first, s16);  // barriers inside
-        }
-        if (tid == 0) {
-            if (mode == 2) rs->rmin = first == UINT64_MAX ? SIMTIME_MAX : B.mn[first % R];
-            rs->rmin_todo = mode != 2;
-            rs->bS = bS;
-            rs->bL = bL;
-            rs->ndue = nd;
-            rs->nfree = nf;
-            rs->ndueb = ndb;
-            rs->ret_b = straddle ? bL : UINT64_MAX;
-        }
-    }
-    if (tid == 0) rs->listed = list ? 1 : 0;  // k_scatter gathers and routes for the new window
-    __syncthreads();
-    PSTAMP(6);
-    for (uint32_t rb = tid; rb < R; rb += PL_T) {
-        d.bcnt[rb] = B.cnt[rb];
-        d.btomb[rb] = B.tomb[rb];
-        d.nal[rb] = B.nal[rb];
-        d.bmin[rb] = B.mn[rb];
-    }
-    if (tid == 0) {
-        rs->fl_head = s_head;
-        rs->fl_tail = s_tail;
-    }
-    PSTAMP(7);
-#undef PSTAMP
+    if (tid == 0) publish_window(d, mode, s_mj[0], s_mj[1], s_mj[2], more);
+    if (pst) pst[7] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Cumulative counters (stats on demand) and pending events.
@@ -2627,19 +2643,25 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
     for (int i = 0; i < NCTR; ++i) c[i] = 0;
     for (uint32_t b = threadIdx.x; b < d.P; b += 1024)
         for (int i = 0; i < NCTR; ++i) c[i] += d.pcum[(size_t)i * d.P + b];
-    // pending: live calendar events outside the listed window's buckets (the
-    // straddling one's stay), plus the window's events already in the host
-    // partitions (gathered or routed by k_scatter, not yet popped)
+    // pending: live calendar events outside the current window's buckets (the
+    // straddling one's stay; the window's events are in the host partitions,
+    // gathered or routed by k_scatter and not yet popped, or, when none was
+    // listed, popped) and outside the window before it (consumed, reset by the
+    // next k_proc)
     const RoundState* rs = d.rs;
     const bool listed = rs->listed != 0;
     const uint64_t bS = rs->bS, span = rs->bL - rs->bS;
     const uint32_t bSr = (uint32_t)(bS % d.R);
     const uint32_t retr = rs->ret_b != UINT64_MAX ? (uint32_t)(rs->ret_b % d.R) : UINT32_MAX;
+    const uint64_t pbS = rs->pbS, pbL = rs->pbL;
     uint64_t pend = 0;
     for (uint32_t rb = threadIdx.x; rb < d.R; rb += 1024) {
         const uint64_t o = rb >= bSr ? rb - bSr : rb + d.R - bSr;
-        if (listed && o <= span && rb != retr) continue;
-        pend += d.bcnt[rb] - d.btomb[rb];
+        if (o <= span && rb != retr) continue;  // listed (gathered), or, none listed, consumed
+        const uint64_t past = bS + o - d.R;  // the slot's bucket before the window (wraps when none)
+        if (pbS != UINT64_MAX && past >= pbS && past <= pbL) continue;  // consumed, reset by the next k_proc
+        for (uint32_t x = 0; x < XS; ++x) pend += d.bk[(size_t)x * d.R + rb];
+        pend -= d.btomb[rb];
     }
     if (listed)
         for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += d.pcnt[p];
@@ -2888,6 +2910,9 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
                      (unsigned long long)span);
         return SG_ERR_INVAL;
     }
+    // a window spans at most max_jump / W + 2 buckets: at most NBMAX (the
+    // gather's due segments)
+    if (max_jump / W + 2 > NBMAX) W = max_jump / (NBMAX - 2) + 1;
     if (span / W + 3 > RMAX) W = (span + RMAX - 4) / (RMAX - 3);
     if (W >= (1ULL << 32)) {
         sg_set_error("sg_engine_create: bucket width %llu ns too large", (unsigned long long)W);
@@ -2903,14 +2928,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     const uint64_t qc = p.queue_cap ? p.queue_cap
                                     : p.workload == SG_WORKLOAD_GOSSIP ? std::max<uint64_t>(64, 24ull * p.load) : 64;
     const uint64_t base_ch = ((uint64_t)d.L * qc + CH - 1) / CH;
-    // every live bucket may hold one partly filled chunk
-    const uint64_t nch = base_ch + d.R + 64;
-    if (nch >= (1ULL << 31) || (uint64_t)d.R * nch > (3ULL << 30)) {
-        sg_set_error("sg_engine_create: calendar too large (R=%u chunks=%llu); lower queue_cap",
-                     d.R, (unsigned long long)nch);
+    if (d.G3 > G3MAX) {
+        sg_set_error("sg_engine_create: SG_INS_GRID %u exceeds %u", d.G3, G3MAX);
         return SG_ERR_INVAL;
     }
-    d.NCH = (uint32_t)nch;
     d.G1 = env_u32("SG_GATHER_GRID", 128);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
@@ -2925,6 +2946,17 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     if (d.P > PMAX) {
         sg_set_error("sg_engine_create: %u partitions exceed %u", d.P, PMAX);
         return SG_ERR_INVAL;
+    }
+    {
+        // every live sub-list may hold one partly filled chunk; the reserving
+        // rows' stashes hold ST chunks each
+        const uint64_t nch = base_ch + (uint64_t)XS * d.R + 64 + (uint64_t)(d.P + d.G3) * ST;
+        if (nch >= (1ULL << 31) || (uint64_t)XS * d.R * nch > (1ULL << 31)) {
+            sg_set_error("sg_engine_create: calendar too large (R=%u chunks=%llu); lower queue_cap",
+                         d.R, (unsigned long long)nch);
+            return SG_ERR_INVAL;
+        }
+        d.NCH = (uint32_t)nch;
     }
     // Slots: every shard's hosts in (vertex, index) order.  Every shard knows
     // every host's global slot (the destination of a send is a slot).
@@ -3107,17 +3139,15 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.hs, L);
     if (D.workload == SG_WORKLOAD_GOSSIP) ALLOC(D.seen, L * D.mw);
     ALLOC(D.pool, (size_t)D.NCH * CH);
-    ALLOC(D.btab, (size_t)D.R * D.NCH);
-    ALLOC(D.bcnt, D.R);
+    ALLOC(D.btab, (size_t)XS * D.R * D.NCH);
+    ALLOC(D.bk, (size_t)XS * D.R);
+    ALLOC(D.bw, (size_t)2 * XS * D.R);
     ALLOC(D.btomb, D.R);
     ALLOC(D.bmin, D.R);
     ALLOC(D.fring, D.NCH);
-    ALLOC(D.nal, D.R);
+    ALLOC(D.stash, (size_t)(D.P + D.G3) * ST);
+    ALLOC(D.stn, D.P + D.G3);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
-    ALLOC(D.bdel, (size_t)XS * D.R);
-    ALLOC(D.bxoff, (size_t)XS * D.R);
-    ALLOC(D.due, D.NCH);
-    ALLOC(D.dueb, D.R);
     ALLOC(D.pcnt, P);
     ALLOC(D.part, P * D.CAPP);
     ALLOC(D.part2, P * D.CAPP);
@@ -3139,7 +3169,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
-    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (2 * P + D.G3 + D.G1 + 2) * SG_STAMP_W);  // + k_plan's, k_scatter's
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (2 * P + D.G3 + D.G1 + 3) * SG_STAMP_W);  // + k_plan's, k_scatter's
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC
@@ -3283,14 +3313,15 @@ int sg_engine_boot(sg_engine* e) {
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)d.R * d.NCH * sizeof(uint32_t), e->stream));
-    const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P));
+    HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
+    const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P + d.G3));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, (const int64_t*)nullptr, 2);
     HIPCHK(hipGetLastError());
-    // the first window's gather (k_scatter's gather role; nothing is staged yet)
-    hipLaunchKernelGGL(k_scatter, dim3(d.P + d.G1 + 1), dim3(K3_T), 0, e->stream, d, (const int64_t*)nullptr);
+    // the first window's gather (k_scatter's gather role; nothing is staged
+    // yet) and the first stash refill
+    hipLaunchKernelGGL(k_scatter, dim3(d.P + d.G1 + 2), dim3(K3_T), 0, e->stream, d, (const int64_t*)nullptr);
     HIPCHK(hipGetLastError());
     e->booted = true;
     return SG_OK;
@@ -3307,10 +3338,11 @@ static int enqueue_process(sg_engine* e) {
     });
 }
 
-// [k_count →] k_plan (mode) → k_scatter: the new (and received) events into
-// the calendar, the window and the next round's due list.  k_proc already
-// counted the local events; k_count counts received blocks (multi-shard).
-static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
+// k_scatter: the new (and received) events into the calendar and the listed
+// window's gather.  One shard: k_proc's last workgroup already ended the
+// round (window, due list).  Multi-shard (recv): k_count reserves the received
+// events, k_plan (mode 1) ends the step from the headers.
+static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
     int rc;
     if (recv) {
@@ -3318,13 +3350,13 @@ static int enqueue_insert_plan(sg_engine* e, const int64_t* recv, int mode) {
             SG_LAUNCH(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, a, b, d, recv);
         });
         if (rc) return rc;
+        rc = timed_launch(e, SG_K_PLAN, [&](hipEvent_t a, hipEvent_t b) {
+            SG_LAUNCH(k_plan, dim3(1), dim3(PL_T), 0, e->stream, a, b, d, recv, 1);
+        });
+        if (rc) return rc;
     }
-    rc = timed_launch(e, SG_K_PLAN, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_plan, dim3(1), dim3(PL_T), 0, e->stream, a, b, d, recv, mode);
-    });
-    if (rc) return rc;
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 1), dim3(K3_T), 0, e->stream, a, b, d, recv);
+        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv);
     });
 }
 
@@ -3339,7 +3371,7 @@ int sg_engine_enqueue_round(sg_engine* e) {
     }
     int rc;
     if ((rc = enqueue_process(e))) return rc;
-    return enqueue_insert_plan(e, nullptr, 0);
+    return enqueue_insert_plan(e, nullptr);
 }
 
 // Enqueues n iterations of body (one round or one step each) on the engine
@@ -3590,12 +3622,12 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
         sg_set_error("sg_engine_step_recv: NULL receive buffer");
         return SG_ERR_INVAL;
     }
-    return enqueue_insert_plan(e, recv, 1);
+    return enqueue_insert_plan(e, recv);
 }
 
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out) {
     if (!e) return SG_ERR_INVAL;
-    const uint64_t n = e->d.stamps ? (2ull * e->d.P + e->d.G3 + e->d.G1 + 2) * SG_STAMP_W : 0;
+    const uint64_t n = e->d.stamps ? (2ull * e->d.P + e->d.G3 + e->d.G1 + 3) * SG_STAMP_W : 0;
     if (n_out) *n_out = n;
     if (out && capacity && n) {
         HIPCHK(hipStreamSynchronize(e->stream));

@@ -183,7 +183,7 @@ class Engine:
         return g.as_dict()
 
     def stamps(self) -> np.ndarray:
-        """[2P + G3 + G1 + 2, 32] stamps of the last round (SG_STAMPS=1): P rows of
+        """[2P + G3 + G1 + 3, 32] stamps of the last round (SG_STAMPS=1): P rows of
         k_proc phase stamps, k_plan's row, then one row per k_scatter workgroup
         {start, setup, events, end, role, n}; or empty."""
         n = C.c_uint64()

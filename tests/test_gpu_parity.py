@@ -137,15 +137,16 @@ def test_full_size_c4_invariants():
 @pytest.mark.parametrize("cap", [1, 128])
 def test_queue_capacity_paths(cap):
     """queue_cap sizes the calendar's chunk pool (n_local * queue_cap events plus
-    one chunk per ring bucket).  A pool far below the live event count must fail
+    one chunk per ring sub-list and the stashes).  A pool far below the live event count must fail
     loudly (SG_ERR_OVERFLOW), never silently; a large one stays bit-exact."""
     if cap == 1:
         # log-normal delays keep events in many future buckets (with C2's one
         # 50 ms path every new event is due in the next window and k_scatter
         # routes it past the calendar, so that config needs no chunks at all)
-        # (the pool also holds one chunk per ring bucket: 200k hosts' 3.2M live
-        # events need far more than that headroom)
-        cfg = phold.c4_config(n_hosts=200_000, V=64, end_time_s=0.3)
+        # (the pool also holds one chunk per ring sub-list and the reserving
+        # workgroups' stashes, about 12.7k chunks here: 200k hosts x 128 live
+        # events need twice that)
+        cfg = phold.c4_config(n_hosts=200_000, V=64, end_time_s=0.3, load=128)
         eng = Engine(cfg, queue_cap=cap)
         eng.boot()
         with pytest.raises(L.SgError) as ei:

@@ -43,15 +43,13 @@ for r in range(3):
     f = np.diff(st[:, [9, 16, 17, 18, 19]], axis=1) / 100
     print("   light host, lane 0 (median us): pop+draws %.2f  dst loads %.2f  pair loads %.2f  commit %.2f"
           % tuple(np.median(f, axis=0)))
-    d = np.diff(pl[:8]) / 100
-    a8 = np.diff(pl[[2, 8, 9, 10, 11, 3]]) / 100
-    print("   k_plan alloc (us): need %.2f  scan %.2f  owner table %.2f  ring->btab %.2f  nal+head %.2f" % tuple(a8))
-    print("   k_plan phases (us): load+reduce %.2f  free %.2f  alloc %.2f  window %.2f  list %.2f  "
-          "first %.2f  writeback %.2f  (total %.2f)" % (*d, (pl[7] - pl[0]) / 100))
+    # one shard: k_proc's last workgroup ends the round (plan_round), stamps 0 and 7 of row P
+    print("   round end in the last k_proc WG: %.2f us (ticket at %.2f us after the kernel's first start)"
+          % ((pl[7] - pl[0]) / 100, (pl[0] - t0) / 100))
     sc = sc[sc[:, 0] > 0]
     s0 = sc[:, 0].min()
     print(f"   k_scatter: span {(sc[:, 3].max() - s0) / 100:.1f} us, WG start spread {(sc[:, 0].max() - s0) / 100:.1f} us")
-    for role, nm in enumerate(["insert", "received", "gather", "rmin"]):
+    for role, nm in enumerate(["insert", "received", "gather", "rmin", "refill"]):
         x = sc[sc[:, 4] == role]
         if not len(x):
             continue
@@ -61,9 +59,13 @@ for r in range(3):
               f"max {(x[:, 3].max() - s0) / 100:6.2f}  n med {np.median(x[:, 5]):.0f}")
     x = sc[sc[:, 4] == 2]
     if len(x):
+        g0 = x[0]
+        print("     due list: %d entries in %d segments, %d freed; window [%d, %d) buckets %d..%d, straddling %d, "
+              "previous straddling %d" % (g0[5], g0[7], g0[8], g0[13], g0[14], g0[9], g0[10],
+                                          np.int64(g0[11]), np.int64(g0[12])))
         q = np.diff(x[:, [0, 1, 2, 6, 3]], axis=1) / 100
         print("     gather (median us): rs+due loads %.2f  pool loads+count %.2f  reserve %.2f  scatter %.2f" % tuple(np.median(q, axis=0)),
-              " chunks/WG med", np.median(x[:, 5]))
+              " chunks/WG med", np.median(x[:, 5]) / len(x))
     dur = (st[:, 4] - st[:, 0]) / 100
     print("   k_proc WG duration: median %.2f  p90 %.2f  max %.2f us; end offsets median %.2f max %.2f"
           % (np.median(dur), np.percentile(dur, 90), dur.max(), np.median(st[:, 4] - t0) / 100, (st[:, 4].max() - t0) / 100))
