@@ -1559,6 +1559,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
+    const Rec* part = d.part + (size_t)p * d.CAPP;
+    // the first SPEC records per lane are loaded before the count arrives
+    // (CAPP >= SPEC * K2_T; records past the count are ignored)
+    constexpr uint32_t SPEC = 2;
+    Rec rr[EPT];
+#pragma unroll
+    for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
     uint32_t n = d.pcnt[p];
     n = n < d.CAPP ? n : d.CAPP;
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
@@ -1580,31 +1587,33 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     if (tid < MAXG) sh.peer[tid] = 0;
-    const Rec* part = d.part + (size_t)p * d.CAPP;
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
     const bool in_lds = n <= d.EVL;
-    Rec rr[EPT];
     if (in_lds) {
 #pragma unroll
-        for (uint32_t q = 0; q < EPT; ++q) {
+        for (uint32_t q = SPEC; q < EPT; ++q) {
             const uint32_t i = tid + q * K2_T;
             rr[q] = i < n ? ld_stream(&part[i]) : Rec{0, 0};
         }
     }
     // the partition's hosts share a few vertices (slots are vertex-sorted):
-    // their path rows into LDS, one coalesced pass
-    uint32_t vlo = 0;
+    // their path rows (<= 32 KB: RQ words per lane) are loaded now into
+    // registers, every load unconditional so the sort below waits for none of
+    // them, and stored into LDS after the scatter
+    constexpr uint32_t RQ = (32u << 10) / 4 / K2_T;
+    uint32_t vlo = 0, rw[RQ], nwords = 0;
     if constexpr (ROWS) {
         const uint32_t s0 = p * HP, s1 = (p + 1) * HP < d.L ? (p + 1) * HP : d.L;
         vlo = d.sinfo[s0].v;
         const uint32_t nrow = d.sinfo[s1 - 1].v - vlo + 1;
-        const uint32_t nent = (nrow < d.rows_max ? nrow : d.rows_max) * d.V;
-        const size_t r0 = (size_t)vlo * d.V;  // the rows are contiguous in the full table
-        for (uint32_t i = tid; i < nent; i += K2_T) {
-            if (d.pair_fmt == PAIR_NARROW)
-                reinterpret_cast<uint2*>(dyn + d.row_off)[i] = reinterpret_cast<const uint2*>(d.prow)[r0 + i];
-            else
-                reinterpret_cast<uint32_t*>(dyn + d.row_off)[i] = reinterpret_cast<const uint32_t*>(d.prow)[r0 + i];
+        const uint32_t wpe = d.pair_fmt == PAIR_NARROW ? 2u : 1u;  // words per record
+        nwords = (nrow < d.rows_max ? nrow : d.rows_max) * d.V * wpe;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(d.prow) + (size_t)vlo * d.V * wpe;
+        const uint32_t last = (d.V - vlo) * d.V * wpe - 1;  // the table's end, from the first row
+#pragma unroll
+        for (uint32_t q = 0; q < RQ; ++q) {
+            const uint32_t i = tid + q * K2_T;
+            rw[q] = src[i < last ? i : last];
         }
         if (nrow > d.rows_max && tid == 0) flag(d, OV_BUG);  // the host sized rows_max
     }
@@ -1707,7 +1716,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (pos < n) part2[pos] = r;
         }
     }
-    __syncthreads();  // the grouped events are read back by other lanes
+    if constexpr (ROWS) {
+#pragma unroll
+        for (uint32_t q = 0; q < RQ; ++q) {
+            const uint32_t i = tid + q * K2_T;
+            if (i < nwords) reinterpret_cast<uint32_t*>(dyn + d.row_off)[i] = rw[q];
+        }
+    }
+    __syncthreads();  // the grouped events (and rows) are read back by other lanes
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
     Acc a;
@@ -2065,10 +2081,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
-    __shared__ uint32_t s_ids[ST];
-    __shared__ uint64_t s_h;
-    reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
-    if (stamp && tid == 0) stamp[15] = wait_stamp();
+    // wave 0: the partials and the MIN accumulators (the last workgroup reads
+    // them), issued before the reservations
     if (tid < NCTR + 2) {
         const int i = tid;
         uint64_t r = s_red[0][i];
@@ -2080,6 +2094,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
         if (i >= NCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
     }
+    __shared__ uint32_t s_ids[ST];
+    __shared__ uint64_t s_h;
+    reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
+    if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
         d.rcnt[p] = nl;
@@ -2087,14 +2105,18 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     {
         // The last workgroup to finish ends the round: one shard, the next
-        // window (publish_window); several, the exchange block headers.  No fences (an L2 write-back per workgroup costs more than
-        // a launch): everything it reads from the others was performed by
-        // device-scope atomics (MIN accumulators, reservations, outbox counts,
-        // flags), which every wave waits for (vmcnt(0)) before the workgroup
-        // takes its ticket.  No workgroup waits for another.
+        // window (publish_window); several, the exchange block headers.  No
+        // fences (an L2 write-back per workgroup costs more than a launch):
+        // what it reads from the others was performed by device-scope atomics
+        // (MIN accumulators, outbox counts), which the issuing wave waits for
+        // (vmcnt(0)) before the workgroup takes its ticket: wave 0 for the MIN
+        // accumulators, every wave's outbox reservations returned their value.
+        // An overflow flag another workgroup sets may reach the next round's
+        // plan instead; the run still stops and reports it.  No workgroup waits
+        // for another.
         __shared__ bool s_lastwg;
         __shared__ uint64_t s_mj[2];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0)
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
