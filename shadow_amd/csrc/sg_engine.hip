@@ -77,11 +77,13 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 constexpr int CH_SHIFT = 10;
 constexpr uint32_t CH = 1u << CH_SHIFT;  // events per chunk (16 KB)
 constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
-// Reservation shards: a workgroup reserves bucket slots in the counter of its
-// shard (workgroup index mod XS, which follows the XCD round-robin), so about
-// P / XS workgroups contend per counter instead of P; k_plan folds them.
+// Bucket sub-lists: a reserving row appends to sub-list (row mod XS) of a
+// bucket, so about P / XS rows contend per counter.  XS = 1 measured fastest
+// since the reservations moved into k_proc (profiles/r02/knobs/xs_ab.log:
+// 58.3 us/round against 61.0 at XS = 2, 63.2 at XS = 4): fewer partly filled
+// chunks and due-list segments outweigh the contention.
 #ifndef SG_XS
-#define SG_XS 2
+#define SG_XS 1
 #endif
 constexpr uint32_t XS = SG_XS;
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
