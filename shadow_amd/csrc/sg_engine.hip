@@ -1675,28 +1675,22 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
     const uint32_t sbase = p * HP;  // the partition's first local slot
-    // phase A's first NPRE hosts of every lane: state loads issued now, under
-    // the LDS scatter below
-    constexpr uint32_t NPRE = 2;
-    // HostState as two 16-B words per host, kept in plain scalars
-    ulonglong2 pre_a0 = make_ulonglong2(0, 0), pre_b0 = pre_a0, pre_a1 = pre_a0, pre_b1 = pre_a0;
-    uint2 pre_s0 = make_uint2(0, 0), pre_s1 = pre_s0;  // SlotInfo {h, v}
+    // phase A's first host of every lane: state loads issued now, under the
+    // LDS scatter below (profiles/r02/knobs/prefetch_ab.log: 57.6 against 58.3
+    // us/round with conditional loads of the first two hosts)
+    // the lane's first host only (the second is rare), loaded unconditionally
+    // from a clamped slot: a conditional load is waited for where it is issued
+    constexpr uint32_t NPRE = 1;
+    ulonglong2 pre_a0, pre_b0, pre_a1 = make_ulonglong2(0, 0), pre_b1 = pre_a1;
+    uint2 pre_s0, pre_s1 = make_uint2(0, 0);
     {
         const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
         const uint2* siw = reinterpret_cast<const uint2*>(d.sinfo);
-        const uint32_t l0 = sbase + (tid < nact ? s_act[tid] : 0u);
-        if (tid < nact && l0 < d.L) {
-            pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
-            pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-            pre_s0 = siw[l0];
-        }
-        const uint32_t j1 = tid + K2_T;
-        const uint32_t l1 = sbase + (j1 < nact ? s_act[j1] : 0u);
-        if (j1 < nact && l1 < d.L) {
-            pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
-            pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
-            pre_s1 = siw[l1];
-        }
+        uint32_t l0 = sbase + s_act[tid < nact ? tid : 0u];
+        l0 = l0 < d.L ? l0 : d.L - 1;
+        pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
+        pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
+        pre_s0 = siw[l0];
     }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
@@ -2519,12 +2513,12 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     const uint32_t* wb = d.wbase + (size_t)blk * R;
     uint64_t smin = UINT64_MAX, ntomb = 0;
     if (blk < d.P) {  // partition blk's staged local events
+        const Rec* src = d.loc + (size_t)blk * d.ECAP;
+        Rec r[SU];
         if (!rs->ins_local) return;
         const uint32_t n = d.rcnt[blk];
         if (n == 0) return;  // uniform: nothing routed, nothing to finish
         const uint64_t S = rs->ins_S;
-        const Rec* src = d.loc + (size_t)blk * d.ECAP;
-        Rec r[SU];
         for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
         for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
         __syncthreads();
