@@ -93,6 +93,7 @@ constexpr uint32_t XCAP = 32;            // same-round self events in flight per
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
 constexpr uint32_t RETAINED = 1u << 31;
 constexpr uint32_t ST = 16;           // chunk ids in a reserving row's stash
+constexpr uint32_t NH = 4;            // buckets of the due-list hint (publish_window)
 constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (bucket width set to fit)
 constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record
                                           // {evc, HDR_REC | active index << 32 | host}
@@ -235,6 +236,9 @@ struct RoundState {
     uint64_t listed;         // a new window was listed: k_scatter gathers and routes for it
     uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
     uint64_t fold;           // steps planned: k_scatter reads bw[fold & 1], writes bw[fold & 1 ^ 1]
+    uint64_t hint_b0;        // the due-list hint: the bucket words of buckets [hint_b0, hint_b0 + NH)
+    uint32_t hint_ok;        // as the plan read them (covers the listed window and a spent bucket),
+    uint32_t hint_hi[NH * XS], hint_lo[NH * XS];  // so the gather need not read them
     uint64_t fl_head, fl_tail;
     uint64_t ins_local;      // k_count took the staged local events (process step)
     uint64_t ins_S;          // their window start (staged times are relative to it)
@@ -793,8 +797,9 @@ __device__ uint32_t due_segments(const Dev& d, DueList& dl, uint32_t* s_start, u
     dl.pret = rs->pret;
     dl.W = d.W;
     dl.R = d.R;
-    const uint64_t ret = rs->ret_b;
+    const uint64_t ret = rs->ret_b, hb0 = rs->hint_b0;
     const uint32_t cur = (uint32_t)(rs->fold & 1);
+    const bool hint = rs->hint_ok != 0;
     dl.spent = dl.pret != UINT64_MAX && dl.pret < dl.bS;
     const uint32_t nb = (uint32_t)(dl.bL - dl.bS + 1);
     dl.nfull = nb - (ret != UINT64_MAX ? 1u : 0u);
@@ -807,8 +812,16 @@ __device__ uint32_t due_segments(const Dev& d, DueList& dl, uint32_t* s_start, u
         uint32_t x, flags;
         bool events;
         dl.seg(j, b, x, flags, events);
-        const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
-        const uint32_t hi = d.bk[row], lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
+        uint32_t hi, lo;
+        if (hint) {  // the plan's copy of the bucket words: no dependent load
+            const uint32_t k = (uint32_t)(b - hb0) * XS + x;
+            hi = rs->hint_hi[k];
+            lo = events ? rs->hint_lo[k] : 0u;
+        } else {
+            const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
+            hi = d.bk[row];
+            lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
+        }
         const uint32_t n = ((flags ? lo : hi) + CH - 1) >> CH_SHIFT;
         s_lo[j] = lo;
         s_start[j] = n;  // the count for now
@@ -1347,8 +1360,32 @@ __device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uin
 __device__ __forceinline__ uint64_t rmw_read(uint64_t* p) {
     return atomicAdd((unsigned long long*)p, 0ull);
 }
-// One thread.  ovf: the overflow flags to keep.
-__device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, uint64_t ovf, bool more) {
+// The bucket words of the NH buckets from the one holding the executed
+// window's end: the new window starts there or later, and the window just
+// executed leaves at most its straddling bucket behind (in the range).  Read
+// with the MIN terms, in the same round trip (one thread); rmw: device-scope
+// reads (other workgroups of the launch reserved slots).
+struct Hint {
+    uint64_t b0;
+    uint32_t hi[NH * XS], lo[NH * XS];
+};
+__device__ __forceinline__ void load_hint(const Dev& d, Hint& h, bool rmw) {
+    const RoundState* rs = d.rs;
+    const uint32_t R = d.R;
+    h.b0 = rs->E / d.W;
+    const uint32_t nx = (uint32_t)((rs->fold + 1) & 1), r0 = (uint32_t)(h.b0 % R);
+#pragma unroll
+    for (uint32_t k = 0; k < NH; ++k)
+#pragma unroll
+        for (uint32_t x = 0; x < XS; ++x) {
+            const uint32_t rb = r0 + k < R ? r0 + k : r0 + k - R, row = x * R + rb;
+            h.hi[k * XS + x] = rmw ? atomicAdd(&d.bk[row], 0u) : d.bk[row];
+            h.lo[k * XS + x] = d.bw[(size_t)nx * XS * R + row];
+        }
+}
+// One thread.  ovf: the overflow flags to keep; h: load_hint's words.
+__device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, uint64_t ovf, bool more,
+                               const Hint& h) {
     RoundState* rs = d.rs;
     const uint64_t W = d.W;
     const uint64_t S0 = rs->S, E0 = rs->E, rounds0 = rs->rounds, nmj0 = rs->next_min_jump, mj0 = rs->min_jump;
@@ -1391,6 +1428,7 @@ __device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, u
         rs->pret = ret0;
     }
     const bool listing = mode == 2 || !done;
+    uint32_t hint = 0;
     if (listing) {
         const uint64_t bS = S / W, bL = (E - 1) / W;
         rs->bS = bS;
@@ -1398,7 +1436,18 @@ __device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, u
         rs->ret_b = E < (bL + 1) * W ? bL : UINT64_MAX;
         rs->rmin_todo = mode != 2;
         if (mode == 2) rs->rmin = SIMTIME_MAX;  // boot: every event is in bucket 0, the window's
+        const uint64_t pret = mode == 2 ? UINT64_MAX : ret0;
+        hint = bS >= h.b0 && bL < h.b0 + NH && (pret == UINT64_MAX || pret >= bS || pret >= h.b0);
+        if (hint) {
+            rs->hint_b0 = h.b0;
+#pragma unroll
+            for (uint32_t i = 0; i < NH * XS; ++i) {
+                rs->hint_hi[i] = h.hi[i];
+                rs->hint_lo[i] = h.lo[i];
+            }
+        }
     }
+    rs->hint_ok = hint;
     rs->listed = listing ? 1 : 0;  // k_scatter gathers and routes for the new window
 }
 
@@ -2121,9 +2170,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
             if (pst) pst[0] = __builtin_amdgcn_s_memrealtime();
             if (tid == 0) {
-                // the three accumulators in one round trip
+                // the accumulators and the due-list hint in one round trip
                 const uint64_t em = rmw_read(&rs->xacc[0]), jm = rmw_read(&rs->xacc[1]);
                 const uint64_t ovf = d.xsend ? 0 : rmw_read(&rs->overflow);
+                Hint h;
+                if (!d.xsend) load_hint(d, h, true);
                 uint64_t m = rs->xcarry;  // carry min (k_scatter's atomics, a kernel ago)
                 m = em < m ? em : m;
                 m = rs->rmin < m ? rs->rmin : m;
@@ -2134,7 +2185,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 rs->xacc[1] = UINT64_MAX;
                 if (!d.xsend) {
                     rs->xcarry = UINT64_MAX;  // k_scatter's gather and inserts refill it
-                    publish_window(d, 0, m, j, ovf, false);
+                    publish_window(d, 0, m, j, ovf, false, h);
                 }
                 s_mj[0] = m;
                 s_mj[1] = j;
@@ -2650,7 +2701,11 @@ __global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int m
         mx = ~block_min(~mx, s16);  // max; barriers inside
         for (uint32_t p = tid; p < d.P; p += PL_T) d.wtime[(size_t)d.P + p] += mx - d.wtime[2 * (size_t)d.P + p];
     }
-    if (tid == 0) publish_window(d, mode, s_mj[0], s_mj[1], s_mj[2], more);
+    if (tid == 0) {
+        Hint h;
+        load_hint(d, h, false);
+        publish_window(d, mode, s_mj[0], s_mj[1], s_mj[2], more, h);
+    }
     if (pst) pst[7] = __builtin_amdgcn_s_memrealtime();
 }
 
