@@ -93,7 +93,6 @@ constexpr uint32_t XCAP = 32;            // same-round self events in flight per
 constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
 constexpr uint32_t RETAINED = 1u << 31;
 constexpr uint32_t ST = 16;           // chunk ids in a reserving row's stash
-constexpr uint32_t NH = 4;            // buckets of the due-list hint (publish_window)
 constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (bucket width set to fit)
 constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record
                                           // {evc, HDR_REC | active index << 32 | host}
@@ -230,15 +229,16 @@ struct RoundState {
     uint64_t bS, bL;         // due bucket range of the current window (absolute indices)
     uint64_t pbS, pbL, pret; // the window before it (its consumed buckets are reset by the next
                              // k_proc) and its straddling bucket, or UINT64_MAX
-    uint64_t rmin;           // min time in buckets beyond bL (exact, at plan time)
-    uint64_t nfree;          // due chunks the last gather returned to the free ring behind fl_tail
-    uint64_t rmin_todo;      // a window was listed: k_scatter's last workgroup computes rmin
-    uint64_t listed;         // a new window was listed: k_scatter gathers and routes for it
+    uint64_t listed;         // the current window was listed: its k_scatter gathered and routed for it
     uint64_t ret_b;          // retained (straddling) bucket, absolute, or UINT64_MAX
-    uint64_t fold;           // steps planned: k_scatter reads bw[fold & 1], writes bw[fold & 1 ^ 1]
-    uint64_t hint_b0;        // the due-list hint: the bucket words of buckets [hint_b0, hint_b0 + NH)
-    uint32_t hint_ok;        // as the plan read them (covers the listed window and a spent bucket),
-    uint32_t hint_hi[NH * XS], hint_lo[NH * XS];  // so the gather need not read them
+    uint64_t fold;           // k_scatter launches: the values below are current at [fold & 1]; a
+                             // k_scatter reads [cur] and writes [cur ^ 1] (bw, rmin2, nfree2, xcarry2)
+    uint64_t rmin2[2];       // min time in buckets beyond the window's bL
+    uint64_t nfree2[2];      // due chunks the last gather returned to the free ring behind fl_tail
+    uint64_t xcarry2[2];     // carry min: what stays in the straddling bucket after the gather and
+                             // inserts (k_scatter's atomics)
+    uint64_t splan;          // k_scatter workgroups that read the round state this launch: the
+                             // last one publishes the next (SG step plan, k_scatter)
     uint64_t fl_head, fl_tail;
     uint64_t ins_local;      // k_count took the staged local events (process step)
     uint64_t ins_S;          // their window start (staged times are relative to it)
@@ -247,10 +247,7 @@ struct RoundState {
     uint64_t steps;      // exchange steps executed
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
     uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
-    uint64_t xacc[2];    // emitted min, discovery min of this launch's workgroups (atomics)
-    uint64_t xcarry;     // carry min: what stays in the straddling bucket after k_scatter's gather
-                         // and inserts (atomics; read by k_plan mode 0 and the step headers,
-                         // reset by k_plan when a round completes)
+    uint64_t xacc[2];    // emitted min, discovery min of k_proc's workgroups (atomics)
 };
 
 struct Dev {
@@ -675,13 +672,19 @@ __global__ void k_boot(Dev d) {
         rs->trace_len = 0;
         for (int c = 0; c < NCTR; ++c) rs->ctr[c] = 0;
         rs->last_min = 0;
+        // the first window [0, 1) (slave.c:431) is listed: bucket 0, straddling
+        // E = 1 (the bucket width is at least 1 ms); the boot k_scatter gathers it
         rs->bS = rs->bL = 0;
         rs->pbS = rs->pbL = rs->pret = UINT64_MAX;
-        rs->rmin = SIMTIME_MAX;
-        rs->nfree = 0;
+        rs->listed = 1;
+        rs->ret_b = 1 < d.W ? 0 : UINT64_MAX;
         rs->fold = 0;
-        rs->listed = 0;
-        rs->ret_b = UINT64_MAX;
+        rs->splan = 0;
+        for (int q = 0; q < 2; ++q) {
+            rs->rmin2[q] = SIMTIME_MAX;
+            rs->nfree2[q] = 0;
+            rs->xcarry2[q] = UINT64_MAX;
+        }
         rs->fl_head = nb0;
         rs->fl_tail = d.NCH;
         rs->ins_local = 0;
@@ -692,7 +695,6 @@ __global__ void k_boot(Dev d) {
         rs->ticket = 0;
         rs->xacc[0] = UINT64_MAX;
         rs->xacc[1] = UINT64_MAX;
-        rs->xcarry = UINT64_MAX;
     }
     if (i < d.G && d.outn) {
         d.outn[i] = 0;
@@ -763,6 +765,24 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
 // slots; its events at or after E stay).  The first nfree entries go back to
 // the free ring.  Written slots come from bw[fold & 1]; this launch's inserts
 // fill the slots reserved since (and route the due ones themselves).
+// What one k_scatter launch works with (step_view): the window it routes and
+// gathers for, computed by thread 0 of every workgroup from the round state
+// the previous kernels left, before anything in the launch changes it.
+struct Window {
+    uint64_t S, E, done, min_jump, next_min_jump;
+};
+struct StepView {
+    uint64_t S, E;           // the new window (or, drain step / boot, the current one)
+    uint64_t bS, bL, ret;    // its buckets and straddling bucket
+    uint64_t pbS, pbL, pret; // the window before it (consumed) and its straddling bucket
+    uint64_t tail;           // the free ring's usable end with the plan applied
+    uint64_t nfree0, carry0, rmin0;  // the current [cur] values (carried over on a drain step)
+    uint64_t ins_S;          // staged local events' time base (k_proc's window start)
+    uint64_t m, j, ovf;      // the MIN terms and overflow flags of the plan
+    uint64_t fold, rounds0, S0, E0;
+    Window w;
+    uint32_t cur, listed, ins_local, round_done, more, done, quit;
+};
 constexpr uint32_t SEGMAX = (NBMAX + 2) * XS;  // segments, at most
 // Segment j is bucket sub-list x = j % XS of the list's k-th bucket, k = j / XS:
 // k < nfull: bucket bS + k (taken whole); then the spent bucket, if any; then
@@ -789,17 +809,15 @@ struct DueList {
     }
 };
 template <int GT>
-__device__ uint32_t due_segments(const Dev& d, DueList& dl, uint32_t* s_start, uint32_t* s_lo, uint64_t* s16,
-                                 uint64_t* nfree_out) {
-    const RoundState* rs = d.rs;
-    dl.bS = rs->bS;
-    dl.bL = rs->bL;
-    dl.pret = rs->pret;
+__device__ uint32_t due_segments(const Dev& d, const StepView& sv, DueList& dl, uint32_t* s_start, uint32_t* s_lo,
+                                 uint64_t* s16, uint64_t* nfree_out) {
+    dl.bS = sv.bS;
+    dl.bL = sv.bL;
+    dl.pret = sv.pret;
     dl.W = d.W;
     dl.R = d.R;
-    const uint64_t ret = rs->ret_b, hb0 = rs->hint_b0;
-    const uint32_t cur = (uint32_t)(rs->fold & 1);
-    const bool hint = rs->hint_ok != 0;
+    const uint64_t ret = sv.ret;
+    const uint32_t cur = sv.cur;
     dl.spent = dl.pret != UINT64_MAX && dl.pret < dl.bS;
     const uint32_t nb = (uint32_t)(dl.bL - dl.bS + 1);
     dl.nfull = nb - (ret != UINT64_MAX ? 1u : 0u);
@@ -812,16 +830,8 @@ __device__ uint32_t due_segments(const Dev& d, DueList& dl, uint32_t* s_start, u
         uint32_t x, flags;
         bool events;
         dl.seg(j, b, x, flags, events);
-        uint32_t hi, lo;
-        if (hint) {  // the plan's copy of the bucket words: no dependent load
-            const uint32_t k = (uint32_t)(b - hb0) * XS + x;
-            hi = rs->hint_hi[k];
-            lo = events ? rs->hint_lo[k] : 0u;
-        } else {
-            const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
-            hi = d.bk[row];
-            lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
-        }
+        const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
+        const uint32_t hi = d.bk[row], lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
         const uint32_t n = ((flags ? lo : hi) + CH - 1) >> CH_SHIFT;
         s_lo[j] = lo;
         s_start[j] = n;  // the count for now
@@ -866,39 +876,39 @@ __device__ __forceinline__ DueEnt due_entry(const Dev& d, const DueList& dl, con
 // touch the same slot.
 constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8 + 2 * SEGMAX * 4;
 template <int GT>
-__device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char* lds, uint64_t* st) {
+__device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32_t nw, unsigned char* lds,
+                            uint64_t* st) {
     constexpr int GR = 4 * (int)CH / GT;
-    const RoundState* rs = d.rs;
     uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
     uint32_t* s_cur = s_cnt + PMAX;                        // [PMAX]
     DueEnt* s_de = (DueEnt*)(s_cur + PMAX);                // [GDMAX]
     uint64_t* s16 = (uint64_t*)(s_de + GDMAX);             // [16]
     uint32_t* s_start = (uint32_t*)(s16 + 16);             // [SEGMAX] the due list's segments
     uint32_t* s_lo = s_start + SEGMAX;                     // [SEGMAX]
-    const uint64_t S = rs->S, E = rs->E;
+    const uint64_t S = sv.S, E = sv.E;
     const uint32_t P = d.P;
     // The window's chunks outside the retained bucket go back to the free ring
-    // behind fl_tail as the entries are staged below (the next round's plan
+    // behind the tail as the entries are staged below (the next step's plan
     // advances the tail; nothing allocates before it).
-    const uint32_t tail_r = (uint32_t)(rs->fl_tail % d.NCH);
+    const uint32_t tail_r = (uint32_t)(sv.tail % d.NCH);
     for (uint32_t p = threadIdx.x; p < P; p += GT) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
     }
     DueList dl;
     uint64_t nfree;
-    const uint64_t nd = due_segments<GT>(d, dl, s_start, s_lo, s16, &nfree);  // barriers inside
-    if (w == 0 && threadIdx.x == 0) d.rs->nfree = nfree;
+    const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree);  // barriers inside
+    if (w == 0 && threadIdx.x == 0) d.rs->nfree2[sv.cur ^ 1] = nfree;
     if (st) {  // the list's shape (SG_STAMPS)
         st[5] = nd;
         st[7] = dl.nseg;
         st[8] = nfree;
-        st[9] = rs->bS;
-        st[10] = rs->bL;
-        st[11] = rs->ret_b;
-        st[12] = rs->pret;
-        st[13] = rs->S;
-        st[14] = rs->E;
+        st[9] = sv.bS;
+        st[10] = sv.bL;
+        st[11] = sv.ret;
+        st[12] = sv.pret;
+        st[13] = sv.S;
+        st[14] = sv.E;
     }
     const uint64_t c0 = nd * w / nw, c1 = nd * (w + 1) / nw;
     auto free_chunk = [&](const DueEnt& de, uint64_t i) {
@@ -1004,9 +1014,9 @@ __device__ void gather_role(const Dev& d, uint32_t w, uint32_t nw, unsigned char
     const uint64_t m = block_min(cmin, s16);
     const uint64_t nt = block_sum(ntomb, s16);
     if (threadIdx.x == 0) {
-        if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry, (unsigned long long)m);
-        if (rs->ret_b != UINT64_MAX) {
-            const uint32_t rb = (uint32_t)(rs->ret_b % d.R);
+        if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry2[sv.cur ^ 1], (unsigned long long)m);
+        if (sv.ret != UINT64_MAX) {
+            const uint32_t rb = (uint32_t)(sv.ret % d.R);
             if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
             if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)m);
         }
@@ -1324,15 +1334,15 @@ __device__ void reserve_buckets(const Dev& d, uint32_t row, uint32_t x, const ui
 }
 
 // ------------------------------------------------------------ plan ----
-// The end of a round (k_proc's last workgroup, one shard; k_plan, several
-// shards or boot): master_slaveFinishedCurrentRound (master.c:450-480), the
-// next window from the MIN next time m and the discovery minimum j (ms), or,
-// mode 1 with `more`, a drain step of the same window.  The window's due
-// chunks are not listed here: every gather workgroup of the following
-// k_scatter derives them from the bucket words (due_segments).
-struct Window {
-    uint64_t S, E, done, min_jump, next_min_jump;
-};
+// The end of a step is planned by k_scatter itself (step_view): thread 0 of
+// every workgroup reads the round state and the MIN terms the previous
+// kernels left (k_proc's accumulators, or, several shards, the G exchange
+// headers: the MIN all-reduce of scheduler.c:386-408 rides on the
+// all-to-all) and computes master_slaveFinishedCurrentRound
+// (master.c:450-480), so every workgroup routes and gathers for the same new
+// window.  Each workgroup then takes a ticket; the last one publishes the plan
+// for the next kernels (publish_step).  Nothing in the launch writes the
+// state the workgroups read before the last ticket, and nothing waits.
 // The next window from the global MIN and the discovery minimum (ms), given
 // the round state's jump fields (computed in registers; the caller stores).
 __device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uint64_t mj0, uint64_t nmj0) {
@@ -1360,95 +1370,164 @@ __device__ Window next_window(const Dev& d, uint64_t minNext, uint64_t jmin, uin
 __device__ __forceinline__ uint64_t rmw_read(uint64_t* p) {
     return atomicAdd((unsigned long long*)p, 0ull);
 }
-// The bucket words of the NH buckets from the one holding the executed
-// window's end: the new window starts there or later, and the window just
-// executed leaves at most its straddling bucket behind (in the range).  Read
-// with the MIN terms, in the same round trip (one thread); rmw: device-scope
-// reads (other workgroups of the launch reserved slots).
-struct Hint {
-    uint64_t b0;
-    uint32_t hi[NH * XS], lo[NH * XS];
-};
-__device__ __forceinline__ void load_hint(const Dev& d, Hint& h, bool rmw) {
+
+// mode 0: one shard, after k_proc; 1: several shards, after k_count (recv:
+// the exchange blocks); 2: boot (the first window is listed already).  One
+// thread.
+__device__ void step_view(const Dev& d, int mode, const int64_t* recv, StepView& sv) {
     const RoundState* rs = d.rs;
-    const uint32_t R = d.R;
-    h.b0 = rs->E / d.W;
-    const uint32_t nx = (uint32_t)((rs->fold + 1) & 1), r0 = (uint32_t)(h.b0 % R);
-#pragma unroll
-    for (uint32_t k = 0; k < NH; ++k)
-#pragma unroll
-        for (uint32_t x = 0; x < XS; ++x) {
-            const uint32_t rb = r0 + k < R ? r0 + k : r0 + k - R, row = x * R + rb;
-            h.hi[k * XS + x] = rmw ? atomicAdd(&d.bk[row], 0u) : d.bk[row];
-            h.lo[k * XS + x] = d.bw[(size_t)nx * XS * R + row];
-        }
-}
-// One thread.  ovf: the overflow flags to keep; h: load_hint's words.
-__device__ void publish_window(const Dev& d, int mode, uint64_t m, uint64_t j, uint64_t ovf, bool more,
-                               const Hint& h) {
-    RoundState* rs = d.rs;
     const uint64_t W = d.W;
-    const uint64_t S0 = rs->S, E0 = rs->E, rounds0 = rs->rounds, nmj0 = rs->next_min_jump, mj0 = rs->min_jump;
-    const uint64_t bS0 = rs->bS, bL0 = rs->bL, ret0 = rs->ret_b, nfree0 = rs->nfree, tail0 = rs->fl_tail;
-    const uint64_t fold0 = rs->fold;
-    rs->overflow = ovf;
-    rs->fold = fold0 + 1;  // one k_scatter follows every plan
-    if (more) {            // drain step: same window, more exchange
-        rs->phase = 1;
-        rs->listed = 0;
-        rs->rmin_todo = 0;
-        return;
-    }
-    uint64_t S = S0, E = E0, done = 0;
-    if (mode != 2) {
-        rs->phase = 0;
-        rs->jmin = j;
-        const Window w = next_window(d, m, j, mj0, nmj0);
-        if (d.wlog && rounds0 < d.wlog_cap) {  // the window just executed
-            d.wlog[2 * rounds0] = S0;
-            d.wlog[2 * rounds0 + 1] = E0;
+    sv.quit = rs->done != 0;
+    sv.fold = rs->fold;
+    sv.cur = (uint32_t)(sv.fold & 1);
+    sv.S0 = rs->S;
+    sv.E0 = rs->E;
+    sv.rounds0 = rs->rounds;
+    const uint64_t nmj0 = rs->next_min_jump, mj0 = rs->min_jump, jmin0 = rs->jmin;
+    const uint64_t tail0 = rs->fl_tail;
+    sv.nfree0 = rs->nfree2[sv.cur];
+    sv.carry0 = rs->xcarry2[sv.cur];
+    sv.rmin0 = rs->rmin2[sv.cur];
+    sv.ins_S = rs->ins_S;
+    sv.ins_local = (uint32_t)rs->ins_local;
+    // the current window (kept on a drain step and at boot)
+    sv.S = sv.S0;
+    sv.E = sv.E0;
+    sv.bS = rs->bS;
+    sv.bL = rs->bL;
+    sv.ret = rs->ret_b;
+    sv.pbS = rs->pbS;
+    sv.pbL = rs->pbL;
+    sv.pret = rs->pret;
+    sv.tail = tail0;
+    sv.listed = mode == 2 ? (uint32_t)rs->listed : 0u;
+    sv.round_done = 0;
+    sv.more = 0;
+    sv.done = 0;
+    uint64_t m = UINT64_MAX, j = UINT64_MAX, ovf = rs->overflow;
+    if (mode == 0) {
+        // the local MIN terms: carry min, k_proc's emitted and discovery minima
+        // (device-scope atomics, a kernel ago), the buckets beyond the window
+        const uint64_t em = rs->xacc[0], jm = rs->xacc[1];
+        m = sv.carry0 < em ? sv.carry0 : em;
+        m = sv.rmin0 < m ? sv.rmin0 : m;
+        m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
+        j = jmin0 < jm ? jmin0 : jm;
+    } else if (mode == 1) {
+        uint64_t more = 0;
+        for (uint32_t p = 0; p < d.G; ++p) {
+            const int64_t* blk = recv + (size_t)p * d.xrows * 3;
+            more |= (uint64_t)blk[H_MORE];
+            const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
+            m = bm < m ? bm : m;
+            j = bj < j ? bj : j;
+            ovf |= (uint64_t)blk[H_OVF];
+            if ((uint64_t)blk[H_ROUND] != sv.rounds0) ovf |= OV_STEP;  // shards out of step
         }
-        rs->rounds = rounds0 + 1;
-        rs->last_min = m;
-        rs->next_min_jump = w.next_min_jump;
-        rs->min_jump = w.min_jump;
-        S = w.S;
-        E = w.E;
-        done = w.done | (ovf ? 1u : 0u);  // a capacity ran out: stop, the host reports it
-        rs->S = S;
-        rs->E = E;
-        rs->done = done;
-        // the last gather's chunks are in the ring now
-        rs->fl_tail = tail0 + nfree0;
-        // the executed window: its consumed buckets are skipped by rmin until
-        // the next k_proc resets them; its straddling bucket is spent unless
-        // the new window starts in it
-        rs->pbS = bS0;
-        rs->pbL = bL0;
-        rs->pret = ret0;
+        sv.more = more != 0;
     }
-    const bool listing = mode == 2 || !done;
-    uint32_t hint = 0;
-    if (listing) {
-        const uint64_t bS = S / W, bL = (E - 1) / W;
-        rs->bS = bS;
-        rs->bL = bL;
-        rs->ret_b = E < (bL + 1) * W ? bL : UINT64_MAX;
-        rs->rmin_todo = mode != 2;
-        if (mode == 2) rs->rmin = SIMTIME_MAX;  // boot: every event is in bucket 0, the window's
-        const uint64_t pret = mode == 2 ? UINT64_MAX : ret0;
-        hint = bS >= h.b0 && bL < h.b0 + NH && (pret == UINT64_MAX || pret >= bS || pret >= h.b0);
-        if (hint) {
-            rs->hint_b0 = h.b0;
-#pragma unroll
-            for (uint32_t i = 0; i < NH * XS; ++i) {
-                rs->hint_hi[i] = h.hi[i];
-                rs->hint_lo[i] = h.lo[i];
+    sv.m = m;
+    sv.j = j;
+    sv.ovf = ovf;
+    if (mode == 2 || sv.more) return;
+    sv.round_done = 1;
+    const Window w = next_window(d, m, j, mj0, nmj0);
+    sv.w = w;
+    sv.done = (w.done | (ovf ? 1u : 0u)) != 0;  // a capacity ran out: stop, the host reports it
+    sv.S = w.S;
+    sv.E = w.E;
+    sv.tail = tail0 + sv.nfree0;  // the last gather's chunks are in the ring now
+    // the executed window: its consumed buckets are skipped by rmin until the
+    // next k_proc resets them; its straddling bucket is spent unless the new
+    // window starts in it
+    sv.pbS = sv.bS;
+    sv.pbL = sv.bL;
+    sv.pret = sv.ret;
+    if (!sv.done) {
+        sv.listed = 1;
+        sv.bS = w.S / W;
+        sv.bL = (w.E - 1) / W;
+        sv.ret = w.E < (sv.bL + 1) * W ? sv.bL : UINT64_MAX;
+    }
+}
+
+// The last workgroup to read the round state writes the plan (one thread).
+// rmin2 / nfree2 / xcarry2 [cur ^ 1] are written by their producers (the rmin
+// role, gather workgroup 0, the carry atomics); on a step without a new window
+// they carry over here.
+__device__ void publish_step(const Dev& d, int mode, const StepView& sv, const int64_t* recv) {
+    RoundState* rs = d.rs;
+    const uint32_t cur = sv.cur;
+    if (sv.ovf) atomicOr((unsigned long long*)&rs->overflow, (unsigned long long)sv.ovf);
+    rs->fold = sv.fold + 1;
+    rs->splan = 0;
+    if (mode == 1) {
+        if (d.check) {
+            // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in
+            // this shard's headers, from device-scope atomics it read without a
+            // fence, must equal the same terms re-derived here from the
+            // workgroups' plain partials; the own block comes back in recv.
+            // (The carry min and rmin are this step's values, at [cur].)
+            uint64_t lm = sv.carry0, lj = UINT64_MAX;
+            for (uint32_t i = 0; i < d.P; ++i) {
+                const uint64_t x = d.p2min[i], y = d.p2min[d.P + i];
+                lm = x < lm ? x : lm;
+                lj = y < lj ? y : lj;
+            }
+            lm = sv.rmin0 < lm ? sv.rmin0 : lm;
+            lm = lm < SIMTIME_MAX ? lm : SIMTIME_MAX;
+            lj = rs->jmin < lj ? rs->jmin : lj;
+            const int64_t* own = recv + (size_t)d.g * d.xrows * 3;
+            if ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj) flag(d, OV_BUG);
+        }
+        rs->steps += 1;
+        for (uint32_t q = 0; q < d.G; ++q) {
+            if (sv.listed) {  // the next step processes: the outboxes refill
+                d.outn[q] = 0;
+                d.sent[q] = 0;
+            } else {
+                const uint64_t left = d.outn[q] - d.sent[q];
+                d.sent[q] += left < d.xcap ? left : d.xcap;
             }
         }
     }
-    rs->hint_ok = hint;
-    rs->listed = listing ? 1 : 0;  // k_scatter gathers and routes for the new window
+    if (mode == 0) {
+        rs->xacc[0] = UINT64_MAX;  // k_proc's next launch accumulates again
+        rs->xacc[1] = UINT64_MAX;
+    }
+    rs->xcarry2[cur] = UINT64_MAX;  // the next launch's carry atomics go here
+    if (!sv.listed) {               // no gather: nothing new in these
+        rs->xcarry2[cur ^ 1] = sv.carry0;
+        rs->nfree2[cur ^ 1] = sv.nfree0;
+    }
+    if (mode == 2) return;
+    if (sv.more) {  // drain step: same window, more exchange
+        rs->phase = 1;
+        rs->listed = 0;
+        return;
+    }
+    const Window& w = sv.w;
+    rs->phase = 0;
+    rs->jmin = sv.j;
+    if (d.wlog && sv.rounds0 < d.wlog_cap) {  // the window just executed
+        d.wlog[2 * sv.rounds0] = sv.S0;
+        d.wlog[2 * sv.rounds0 + 1] = sv.E0;
+    }
+    rs->rounds = sv.rounds0 + 1;
+    rs->last_min = sv.m;
+    rs->next_min_jump = w.next_min_jump;
+    rs->min_jump = w.min_jump;
+    rs->S = sv.S;
+    rs->E = sv.E;
+    rs->done = sv.done;
+    rs->fl_tail = sv.tail;
+    rs->pbS = sv.pbS;
+    rs->pbL = sv.pbL;
+    rs->pret = sv.pret;
+    rs->bS = sv.bS;
+    rs->bL = sv.bL;
+    rs->ret_b = sv.ret;
+    rs->listed = sv.listed;
 }
 
 // Resets the buckets the window before the current one consumed (fully due,
@@ -1621,7 +1700,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     n = n < d.CAPP ? n : d.CAPP;
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
     const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
-    const uint64_t ring_end = rs->fl_tail + rs->nfree;  // the gather of the listed window freed nfree more
+    const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];  // the last gather freed nfree more
     for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
     for (uint32_t rb = tid; rb < R; rb += K2_T) {
         s_bc[rb] = 0;
@@ -2148,17 +2227,18 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         d.rcnt[p] = nl;
         if (d.remn) d.remn[p] = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
     }
-    {
-        // The last workgroup to finish ends the round: one shard, the next
-        // window (publish_window); several, the exchange block headers.  No
-        // fences (an L2 write-back per workgroup costs more than a launch):
+    if (d.xsend) {
+        // Several shards: the last workgroup to finish writes the exchange
+        // block headers (this shard's MIN terms; one shard, k_scatter plans
+        // the next window from the accumulators after the kernel boundary).
+        // No fences (an L2 write-back per workgroup costs more than a launch):
         // what it reads from the others was performed by device-scope atomics
         // (MIN accumulators, outbox counts), which the issuing wave waits for
         // (vmcnt(0)) before the workgroup takes its ticket: wave 0 for the MIN
-        // accumulators, every wave's outbox reservations returned their value.
-        // An overflow flag another workgroup sets may reach the next round's
-        // plan instead; the run still stops and reports it.  No workgroup waits
-        // for another.
+        // accumulators; every wave's outbox reservations returned their value.
+        // An overflow flag another workgroup sets may reach the next step's
+        // headers instead; the run still stops and reports it.  No workgroup
+        // waits for another.
         __shared__ bool s_lastwg;
         __shared__ uint64_t s_mj[2];
         if (wid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2167,34 +2247,21 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
         __syncthreads();
         if (s_lastwg) {
-            uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
-            if (pst) pst[0] = __builtin_amdgcn_s_memrealtime();
             if (tid == 0) {
-                // the accumulators and the due-list hint in one round trip
+                const uint32_t cur = (uint32_t)(rs->fold & 1);
                 const uint64_t em = rmw_read(&rs->xacc[0]), jm = rmw_read(&rs->xacc[1]);
-                const uint64_t ovf = d.xsend ? 0 : rmw_read(&rs->overflow);
-                Hint h;
-                if (!d.xsend) load_hint(d, h, true);
-                uint64_t m = rs->xcarry;  // carry min (k_scatter's atomics, a kernel ago)
+                uint64_t m = rs->xcarry2[cur];  // carry min (k_scatter's atomics, a kernel ago)
                 m = em < m ? em : m;
-                m = rs->rmin < m ? rs->rmin : m;
+                m = rs->rmin2[cur] < m ? rs->rmin2[cur] : m;
                 m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
-                const uint64_t j = rs->jmin < jm ? rs->jmin : jm;
+                s_mj[0] = m;
+                s_mj[1] = rs->jmin < jm ? rs->jmin : jm;
                 rs->ticket = 0;
                 rs->xacc[0] = UINT64_MAX;
                 rs->xacc[1] = UINT64_MAX;
-                if (!d.xsend) {
-                    rs->xcarry = UINT64_MAX;  // k_scatter's gather and inserts refill it
-                    publish_window(d, 0, m, j, ovf, false, h);
-                }
-                s_mj[0] = m;
-                s_mj[1] = j;
             }
-            if (d.xsend) {
-                __syncthreads();
-                write_headers(d, s_mj[0], s_mj[1]);
-            }
-            if (pst) pst[7] = wait_stamp();
+            __syncthreads();
+            write_headers(d, s_mj[0], s_mj[1]);
         }
     }
     if (stamp && tid == 0) {
@@ -2268,7 +2335,7 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
     const uint32_t R = d.R;
     const uint32_t row = d.P + blockIdx.x;
     const uint32_t stash_id = d.stash[(size_t)row * ST + (threadIdx.x & (ST - 1))], stash_n = d.stn[row];
-    const uint64_t ring_end = rs->fl_tail + rs->nfree;
+    const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];
     if (blockIdx.x == 0 && threadIdx.x == 0) rs->ins_local = rs->phase == 0;
     for (uint32_t b = threadIdx.x; b < R; b += K3_T) {
         s_bc[b] = 0;
@@ -2317,6 +2384,7 @@ constexpr size_t SCAT_LDS = SCAT_LDS0 > REFILL_LDS ? SCAT_LDS0 : REFILL_LDS;
 
 struct Route {
     bool listed;
+    uint32_t cur;         // the step's parity (carry min goes to xcarry2[cur ^ 1])
     uint64_t S, E, ret;   // the new window, its straddling bucket (UINT64_MAX: none)
     uint64_t bS, bSW;     // the window's first bucket and its start: every event inserted is at or
                           // after it and within R buckets of it (k_proc's horizon check)
@@ -2408,45 +2476,73 @@ __device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uin
         const uint32_t rb = (uint32_t)(ro.ret % d.R);
         if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
         if (m != UINT64_MAX) {
-            atomicMin((unsigned long long*)&d.rs->xcarry, (unsigned long long)m);
+            atomicMin((unsigned long long*)&d.rs->xcarry2[ro.cur ^ 1], (unsigned long long)m);
             atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)m);
         }
     }
 }
 
-__global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
+// The planner (one thread) waits until the n other workgroups have read the
+// round state, then publishes.  Every workgroup of the grid runs to its
+// arrival without waiting for anything, so the wait ends; it is bounded all
+// the same (a missed arrival is reported as OV_BUG, never a hang).
+__device__ void plan_when_read(const Dev& d, int mode, const StepView& sv, const int64_t* recv, uint32_t n) {
+    uint64_t* ctr = &d.rs->splan;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+        if (++spins > (1u << 22)) {
+            flag(d, OV_BUG);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    publish_step(d, mode, sv, recv);
+}
+
+// mode: 0 one shard (after k_proc), 1 several shards (after k_count; recv the
+// exchange blocks), 2 boot.  Every workgroup plans the step (step_view) from
+// the state as the previous kernels left it and reports that it has read it
+// (a fire-and-forget arrival); the last workgroup (the rmin role) publishes
+// the plan (publish_step) once every other one has arrived.
+__global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, int mode) {
     RoundState* rs = d.rs;
-    if (rs->done) return;
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
-    const uint32_t R = d.R, blk = blockIdx.x;
+    __shared__ StepView sv;
+    const uint32_t R = d.R, blk = blockIdx.x, tid = threadIdx.x;
+    const bool planner = blk == gridDim.x - 1;
+    if (tid == 0) {
+        step_view(d, mode, recv, sv);
+        if (!sv.quit && !planner) {
+            // every read of the round state has returned before the arrival
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            atomicAdd((unsigned long long*)&rs->splan, 1ull);
+        }
+    }
+    __syncthreads();
+    if (sv.quit) return;  // uniform: the run ended (no workgroup took a ticket)
     const uint32_t g0 = d.P + (recv ? d.G3 : 0);
     Route ro;
-    ro.listed = rs->listed != 0;
-    ro.S = rs->S;
-    ro.E = rs->E;
-    ro.ret = rs->ret_b;
-    ro.bS = rs->bS;
+    ro.listed = sv.listed != 0;
+    ro.cur = sv.cur;
+    ro.S = sv.S;
+    ro.E = sv.E;
+    ro.ret = sv.ret;
+    ro.bS = sv.bS;
     ro.bSW = ro.bS * d.W;
     ro.bSr = (uint32_t)(ro.bS % R);
     // SG_STAMPS: {start, after setup, after the events, end, role, events}
-    uint64_t* st = d.stamps && threadIdx.x == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
+    uint64_t* st = d.stamps && tid == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
     if (st) {
         st[0] = __builtin_amdgcn_s_memrealtime();
         st[4] = blk == gridDim.x - 1 ? 3 : blk == gridDim.x - 2 ? 4 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
         st[1] = st[2] = st[3] = st[6] = st[0];
         st[5] = 0;
     }
-    const uint32_t tid = threadIdx.x;
     if (blk == gridDim.x - 1) {
         uint64_t* s16 = (uint64_t*)lds;
-        if (ro.listed && d.outn && tid < d.G) {  // the next step processes: outboxes refill
-            d.outn[tid] = 0;
-            d.sent[tid] = 0;
-        }
-        if (d.wtime && !recv) {
-            // one shard: the round k_proc just ended; barrier wait
-            // (scheduler.c:380-389): each partition idles from its end to the
-            // round's last partition end
+        if (d.wtime && sv.round_done) {
+            // barrier wait (scheduler.c:380-389): each partition idles from its
+            // end to the round's last partition end
             uint64_t mx = 0;
             for (uint32_t p = tid; p < d.P; p += K3_T) {
                 const uint64_t t = d.wtime[2 * (size_t)d.P + p];
@@ -2455,13 +2551,19 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
             mx = ~block_min(~mx, s16);  // max; barriers inside
             for (uint32_t p = tid; p < d.P; p += K3_T) d.wtime[(size_t)d.P + p] += mx - d.wtime[2 * (size_t)d.P + p];
         }
-        // rmin for the window just listed: the min time of the buckets beyond
-        // it, (bL, bS + R), but those of the window before it (consumed, reset
-        // by the next k_proc).  The rest hold no tombstones or were reset, and
-        // this launch changes only the straddling bucket's minimum, so the
-        // minima read are final.
-        if (!rs->rmin_todo) return;
-        const uint64_t bS = rs->bS, bL = rs->bL, pbS = rs->pbS, pbL = rs->pbL;
+        // rmin for the listed window: the min time of the buckets beyond it,
+        // (bL, bS + R), but those of the window before it (consumed, reset by
+        // the next k_proc).  The rest hold no tombstones or were reset, and this
+        // launch changes only the straddling bucket's minimum, so the minima
+        // read are final.  No new window: the current value carries over.
+        if (!sv.listed) {
+            if (tid == 0) {
+                rs->rmin2[sv.cur ^ 1] = sv.rmin0;
+                plan_when_read(d, mode, sv, recv, gridDim.x - 1);
+            }
+            return;
+        }
+        const uint64_t bS = sv.bS, bL = sv.bL, pbS = sv.pbS, pbL = sv.pbL;
         const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
         uint64_t mn = UINT64_MAX;
         for (uint32_t o = tid + 1; o + span < R; o += K3_T) {
@@ -2473,8 +2575,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         }
         mn = block_min(mn, s16);  // barriers inside
         if (tid == 0) {
-            rs->rmin = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
-            rs->rmin_todo = 0;
+            rs->rmin2[sv.cur ^ 1] = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
+            plan_when_read(d, mode, sv, recv, gridDim.x - 1);
             if (st) st[3] = __builtin_amdgcn_s_memrealtime();
         }
         return;
@@ -2483,7 +2585,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         // fold: every slot reserved so far is written by this launch, so the
         // next step's gather may read them all
         {
-            const uint32_t nx = (uint32_t)((rs->fold & 1) ^ 1);
+            const uint32_t nx = sv.cur ^ 1;
             for (uint32_t i = tid; i < XS * R; i += K3_T) d.bw[(size_t)nx * XS * R + i] = d.bk[i];
         }
         // stash refill: every reserving row back to ST chunk ids, one ring
@@ -2498,7 +2600,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
         uint32_t* s_have = (uint32_t*)(s_hh + 1);  // [PMAX + G3MAX]
         uint32_t* s_roff = s_have + PMAX + G3MAX;  // [PMAX + G3MAX] first list entry of each row
         const uint32_t rows = d.P + (d.outn ? d.G3 : 0u), NCH = d.NCH;
-        const uint64_t avail = rs->fl_tail;
+        const uint64_t avail = sv.tail;
         uint32_t have[RPT];
         uint32_t mine = 0;
 #pragma unroll
@@ -2552,7 +2654,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     }
     const uint32_t gx = gridDim.x - 2;  // gather workgroups [g0, gx)
     if (blk >= g0) {
-        if (ro.listed) gather_role<K3_T>(d, blk - g0, gx - g0, lds, st);
+        if (ro.listed) gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, st);
         if (st) st[3] = wait_stamp();
         return;
     }
@@ -2566,10 +2668,10 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
     if (blk < d.P) {  // partition blk's staged local events
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
         Rec r[SU];
-        if (!rs->ins_local) return;
+        if (!sv.ins_local) return;
         const uint32_t n = d.rcnt[blk];
         if (n == 0) return;  // uniform: nothing routed, nothing to finish
-        const uint64_t S = rs->ins_S;
+        const uint64_t S = sv.ins_S;
         for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
         for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
         __syncthreads();
@@ -2627,7 +2729,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv) {
 // emitted min and discovery min (k_proc), and the buckets beyond the window
 // (rmin).
 __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
-    uint64_t mm = d.rs->xcarry, jj = UINT64_MAX;
+    const uint32_t cur = (uint32_t)(d.rs->fold & 1);
+    uint64_t mm = d.rs->xcarry2[cur], jj = UINT64_MAX;
     for (uint32_t i = threadIdx.x; i < d.P; i += blockDim.x) {
         const uint64_t x = d.p2min[i], y = d.p2min[d.P + i];
         mm = x < mm ? x : mm;
@@ -2636,77 +2739,9 @@ __device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t&
     m = block_min(mm, s16);
     j = block_min(jj, s16);
     const RoundState* rs = d.rs;
-    m = rs->rmin < m ? rs->rmin : m;
+    m = rs->rmin2[cur] < m ? rs->rmin2[cur] : m;
     m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
     j = rs->jmin < j ? rs->jmin : j;
-}
-
-// k_plan: the multi-shard end of a step (mode 1: the next window from the G
-// received headers, the MIN all-reduce of scheduler.c:386-408 carried by the
-// all-to-all, or a drain step) and the boot listing (mode 2).  One workgroup.
-// A single-shard round ends in k_proc's last workgroup instead.
-__global__ __launch_bounds__(PL_T) void k_plan(Dev d, const int64_t* recv, int mode) {
-    RoundState* rs = d.rs;
-    if (rs->done) return;
-    __shared__ uint64_t s16[16];
-    __shared__ uint64_t s_mj[4];
-    const uint32_t tid = threadIdx.x;
-    uint64_t* pst = d.stamps && tid == 0 ? d.stamps + (size_t)d.P * SG_STAMP_W : nullptr;
-    if (pst) pst[0] = __builtin_amdgcn_s_memrealtime();
-    if (mode == 1 && d.check) {
-        // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in this
-        // shard's headers, from device-scope atomics it read without a fence,
-        // must equal the same terms re-derived here from the workgroups' plain
-        // partials (visible after the kernel boundary); the own block comes back
-        // in recv.  On a drain step fill_blocks wrote them from the partials.
-        uint64_t lm, lj;
-        reduce_local(d, s16, lm, lj);  // barriers inside
-        const int64_t* own = recv + (size_t)d.g * d.xrows * 3;
-        if (tid == 0 && ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj)) flag(d, OV_BUG);
-    }
-    if (tid == 0) {
-        uint64_t more = 0, m = UINT64_MAX, j = UINT64_MAX, ovf = rs->overflow;
-        if (mode == 1) {
-            for (uint32_t p = 0; p < d.G; ++p) {
-                const int64_t* blk = recv + (size_t)p * d.xrows * 3;
-                more |= (uint64_t)blk[H_MORE];
-                const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
-                m = bm < m ? bm : m;
-                j = bj < j ? bj : j;
-                ovf |= (uint64_t)blk[H_OVF];
-                if ((uint64_t)blk[H_ROUND] != rs->rounds) ovf |= OV_STEP;  // shards out of step
-            }
-            for (uint32_t q = 0; q < d.G; ++q) {
-                const uint64_t left = d.outn[q] - d.sent[q];
-                d.sent[q] += left < d.xcap ? left : d.xcap;
-            }
-            rs->steps += 1;
-            if (!more) rs->xcarry = UINT64_MAX;  // k_scatter's gather refills it
-        }
-        s_mj[0] = m;
-        s_mj[1] = j;
-        s_mj[2] = ovf;
-        s_mj[3] = more;
-    }
-    __syncthreads();
-    const bool more = s_mj[3] != 0;
-    if (d.wtime && mode == 1 && !more) {
-        // barrier wait (scheduler.c:380-389): each partition idles from its end
-        // to the round's last partition end
-        uint64_t mx = 0;
-        for (uint32_t p = tid; p < d.P; p += PL_T) {
-            const uint64_t t = d.wtime[2 * (size_t)d.P + p];
-            mx = t > mx ? t : mx;
-        }
-        mx = ~block_min(~mx, s16);  // max; barriers inside
-        for (uint32_t p = tid; p < d.P; p += PL_T) d.wtime[(size_t)d.P + p] += mx - d.wtime[2 * (size_t)d.P + p];
-    }
-    if (tid == 0) {
-        Hint h;
-        load_hint(d, h, false);
-        publish_window(d, mode, s_mj[0], s_mj[1], s_mj[2], more, h);
-    }
-    if (pst) pst[7] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Cumulative counters (stats on demand) and pending events.
@@ -3390,11 +3425,9 @@ int sg_engine_boot(sg_engine* e) {
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P + d.G3));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(PL_T), 0, e->stream, d, (const int64_t*)nullptr, 2);
-    HIPCHK(hipGetLastError());
     // the first window's gather (k_scatter's gather role; nothing is staged
     // yet) and the first stash refill
-    hipLaunchKernelGGL(k_scatter, dim3(d.P + d.G1 + 2), dim3(K3_T), 0, e->stream, d, (const int64_t*)nullptr);
+    hipLaunchKernelGGL(k_scatter, dim3(d.P + d.G1 + 2), dim3(K3_T), 0, e->stream, d, (const int64_t*)nullptr, 2);
     HIPCHK(hipGetLastError());
     e->booted = true;
     return SG_OK;
@@ -3411,10 +3444,9 @@ static int enqueue_process(sg_engine* e) {
     });
 }
 
-// k_scatter: the new (and received) events into the calendar and the listed
-// window's gather.  One shard: k_proc's last workgroup already ended the
-// round (window, due list).  Multi-shard (recv): k_count reserves the received
-// events, k_plan (mode 1) ends the step from the headers.
+// k_scatter: the new (and received) events into the calendar, the next
+// window planned and gathered.  Several shards (recv): k_count reserves the
+// received events first.
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
     int rc;
@@ -3423,13 +3455,10 @@ static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
             SG_LAUNCH(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, a, b, d, recv);
         });
         if (rc) return rc;
-        rc = timed_launch(e, SG_K_PLAN, [&](hipEvent_t a, hipEvent_t b) {
-            SG_LAUNCH(k_plan, dim3(1), dim3(PL_T), 0, e->stream, a, b, d, recv, 1);
-        });
-        if (rc) return rc;
     }
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv);
+        SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv,
+                  recv ? 1 : 0);
     });
 }
 

@@ -43,9 +43,6 @@ for r in range(3):
     f = np.diff(st[:, [9, 16, 17, 18, 19]], axis=1) / 100
     print("   light host, lane 0 (median us): pop+draws %.2f  dst loads %.2f  pair loads %.2f  commit %.2f"
           % tuple(np.median(f, axis=0)))
-    # one shard: k_proc's last workgroup ends the round (plan_round), stamps 0 and 7 of row P
-    print("   round end in the last k_proc WG: %.2f us (ticket at %.2f us after the kernel's first start)"
-          % ((pl[7] - pl[0]) / 100, (pl[0] - t0) / 100))
     sc = sc[sc[:, 0] > 0]
     s0 = sc[:, 0].min()
     print(f"   k_scatter: span {(sc[:, 3].max() - s0) / 100:.1f} us, WG start spread {(sc[:, 0].max() - s0) / 100:.1f} us")
