@@ -2214,7 +2214,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint64_t x = s_red[w][i];
             r = i < NCTR ? r + x : (x < r ? x : r);
         }
-        if (i < NCTR) d.pcum[(size_t)i * d.P + p] += r;
+        // the workgroup's own slot: an atomic add needs no load (wave 0 joins
+        // the reservations' barrier without waiting for one)
+        if (i < NCTR) atomicAdd((unsigned long long*)&d.pcum[(size_t)i * d.P + p], (unsigned long long)r);
         else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
         if (i >= NCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
     }
