@@ -603,6 +603,21 @@ __device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
     return base + rank;
 }
 
+// wave_slots: n in {0, 1, 2} consecutive slots for each ACTIVE lane, one
+// atomic per wave (divergent code allowed).
+__device__ __forceinline__ uint32_t wave_slots(uint32_t* ctr, uint32_t n) {
+    const uint64_t m1 = __ballot(n >= 1), m2 = __ballot(n >= 2), act = __ballot(1);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = (1ULL << lane) - 1;
+    const uint32_t rank = (uint32_t)(__builtin_popcountll(m1 & lt) + __builtin_popcountll(m2 & lt));
+    const uint32_t total = (uint32_t)(__builtin_popcountll(m1) + __builtin_popcountll(m2));
+    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+    uint32_t base = 0;
+    if (lane == leader && total) base = atomicAdd(ctr, total);
+    base = __shfl(base, (int)leader, 64);
+    return base + rank;
+}
+
 // event_compare with equal dst (event.c:122-148) on (time, src<<40|seq).
 // Bitwise, not short-circuit, and the running minimum is updated through one
 // select mask: ROCm 7.2 mis-compiled the branchy form inside a selection
@@ -1042,6 +1057,20 @@ struct ProcShared {
     uint32_t peer[MAXG];
 };
 
+// Stage one event for another shard's host (the outbox, several shards only).
+__device__ __forceinline__ void stage_remote(const Dev& d, uint32_t part, ProcShared& sh, Acc& a, uint32_t dst,
+                                             uint64_t tn, uint64_t key) {
+    const uint32_t slot = wave_slot(&sh.nrem);
+    if (slot < d.ECAP) {
+        const size_t so = (size_t)part * d.ECAP + slot;
+        d.rem[so] = Slot{tn, key};
+        d.rem_dst[so] = dst;
+        atomicAdd(&sh.peer[owner_of(d, dst)], 1u);
+    } else {
+        a.overflow = true;
+    }
+}
+
 // Stage one new event (time already bumped) for the calendar (this shard's
 // hosts; k_proc counts them by bucket after phase C) or for the outbox (other
 // shards).
@@ -1055,18 +1084,9 @@ __device__ __forceinline__ bool stage_event(const Dev& d, uint64_t S, uint32_t p
         if (slot < d.ECAP) st_stream(&d.loc[(size_t)part * d.ECAP + slot], Rec{((uint64_t)dl << 40) | (tn - S), key});
         else a.overflow = true;
         return true;
-    } else {
-        const uint32_t slot = wave_slot(&sh.nrem);
-        if (slot < d.ECAP) {
-            const size_t so = (size_t)part * d.ECAP + slot;
-            d.rem[so] = Slot{tn, key};
-            d.rem_dst[so] = dst;
-            atomicAdd(&sh.peer[owner_of(d, dst)], 1u);
-        } else {
-            a.overflow = true;
-        }
-        return false;
     }
+    stage_remote(d, part, sh, a, dst, tn, key);
+    return false;
 }
 
 // Execute one popped event (worker.c:165-176 + the PHOLD body + worker_sendPacket).
@@ -1170,32 +1190,67 @@ __device__ __forceinline__ void execute_event(const Dev& d, uint64_t S, uint64_t
     }
 }
 
-// One resolved send of a host whose sends cannot land in this window at the
-// host itself: reliability test (worker.c:268-273), delivery time
-// (worker.c:275-277), srcHostEventID (event.c:38), endTime drop
-// (scheduler.c:343-346), barrier bump (host_single.c:180-184), staging.
-template <class Count>
-__device__ __forceinline__ void commit_send(const Dev& d, uint64_t S, uint64_t E, uint32_t part, HostCtx& c,
-                                            Acc& a, ProcShared& sh, uint64_t bt, int32_t ch, uint32_t dst,
-                                            uint32_t vd, const PairRec& pr, Count count) {
+// A resolved send of a host whose sends cannot land in this window at the host
+// itself: reliability test (worker.c:268-273), delivery time (worker.c:275-277),
+// srcHostEventID (event.c:38), endTime drop (scheduler.c:343-346), barrier
+// bump (host_single.c:180-184). False when the send is dropped.
+__device__ __forceinline__ bool send_tests(const Dev& d, uint64_t E, HostCtx& c, Acc& a, uint64_t bt, int32_t ch,
+                                           uint32_t dst, uint32_t vd, const PairRec& pr, uint64_t& tn, uint64_t& key) {
     a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // path discovery (topology.c:1374-1385)
-    if (!(bt < d.bootstrap_end || ch <= pr.keep)) {
+    if (!(bt < d.bootstrap_end || ch <= pr.keep)) {  // worker.c:268-273
         ++a.ctr[C_DROPREL];
-        return;
+        return false;
     }
     if (d.pcount) atomicAdd(&d.pcount[(size_t)c.vh * d.V + vd], 1u);  // worker.c:279
-    uint64_t tn = bt + pr.delay;
-    const uint64_t sq = c.s.evc++;
-    if (tn >= d.end_time) {
+    tn = bt + pr.delay;                 // worker.c:275-277
+    const uint64_t sq = c.s.evc++;      // event.c:38
+    if (tn >= d.end_time) {             // scheduler.c:343-346
         ++a.ctr[C_DROPEND];
-        return;
+        return false;
     }
     if (dst == c.sg && tn < E) a.overflow = true;  // excluded by the caller's self-path test
-    if (dst != c.sg && tn < E) {
+    if (dst != c.sg && tn < E) {        // host_single.c:180-184
         tn = E;
         ++a.ctr[C_BUMPED];
     }
-    if (stage_event(d, S, part, sh, a, dst, tn, ((uint64_t)c.h << SRC_SHIFT) | sq)) count(tn);
+    key = ((uint64_t)c.h << SRC_SHIFT) | sq;
+    return true;
+}
+// The light path's two resolved sends (the first nsd are real): the tests for
+// each, then one staging reservation per wave for both local events.
+template <class Count>
+__device__ __forceinline__ void commit_two(const Dev& d, uint64_t S, uint64_t E, uint32_t part, HostCtx& c, Acc& a,
+                                           ProcShared& sh, uint32_t nsd, uint64_t bt0, int32_t ch0, uint32_t dst0,
+                                           uint32_t vd0, const PairRec& pr0, uint64_t bt1, int32_t ch1,
+                                           uint32_t dst1, uint32_t vd1, const PairRec& pr1, Count count) {
+    uint64_t tn0 = 0, tn1 = 0, k0 = 0, k1 = 0;
+    const bool g0 = nsd > 0 && send_tests(d, E, c, a, bt0, ch0, dst0, vd0, pr0, tn0, k0);
+    const bool g1 = nsd > 1 && send_tests(d, E, c, a, bt1, ch1, dst1, vd1, pr1, tn1, k1);
+    const uint32_t dl0 = dst0 - d.lo, dl1 = dst1 - d.lo;
+    const bool l0 = g0 && dl0 < d.L, l1 = g1 && dl1 < d.L;
+    const uint32_t base = wave_slots(&sh.nloc, (uint32_t)l0 + (uint32_t)l1);
+    Rec* loc = d.loc + (size_t)part * d.ECAP;
+    if (l0) {
+        if (base < d.ECAP) st_stream(&loc[base], Rec{((uint64_t)dl0 << 40) | (tn0 - S), k0});
+        else a.overflow = true;
+        count(tn0);
+    }
+    if (l1) {
+        const uint32_t sl = base + (l0 ? 1u : 0u);
+        if (sl < d.ECAP) st_stream(&loc[sl], Rec{((uint64_t)dl1 << 40) | (tn1 - S), k1});
+        else a.overflow = true;
+        count(tn1);
+    }
+    if (g0) {
+        a.emin = tn0 < a.emin ? tn0 : a.emin;
+        ++a.ctr[C_EMIT];
+    }
+    if (g1) {
+        a.emin = tn1 < a.emin ? tn1 : a.emin;
+        ++a.ctr[C_EMIT];
+    }
+    if (g0 && !l0) stage_remote(d, part, sh, a, dst0, tn0, k0);
+    if (g1 && !l1) stage_remote(d, part, sh, a, dst1, tn1, k1);
 }
 
 // Pop a host's sorted segment (worker.c:165-176): trace digest, counters and
@@ -2024,8 +2079,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             const PairRec pr0 = pair_of(c.vh, vd0, want_jump);
                             const PairRec pr1 = pair_of(c.vh, vd1, want_jump);
                             if (st0) stamp[18] = wait_stamp();
-                            if (nsd > 0) commit_send(d, S, E, p, c, a, sh, S + t0, c0, dst0, vd0, pr0, count_local);
-                            if (nsd > 1) commit_send(d, S, E, p, c, a, sh, S + t1, c1, dst1, vd1, pr1, count_local);
+                            commit_two(d, S, E, p, c, a, sh, nsd, S + t0, c0, dst0, vd0, pr0, S + t1, c1, dst1, vd1, pr1,
+                                       count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
                             st_stream2(&hp[0], (uint64_t)c.s.rng, c.s.pops);
                             if (st0) stamp[19] = wait_stamp();
