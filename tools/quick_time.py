@@ -1,6 +1,7 @@
 """Round time of the 1M-host C4 engine without the bench's parity check (for
 experimental variant libraries whose state intentionally differs):
-SG_LIB=libshadowgpu_<v>.so python tools/quick_time.py [rounds]."""
+SG_LIB=libshadowgpu_<v>.so python tools/quick_time.py [rounds] (QT_HOSTS: host count)."""
+import os
 import sys
 import time
 
@@ -9,7 +10,7 @@ from shadow_amd import phold  # noqa: E402
 from shadow_amd.engine import Engine  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-eng = Engine(phold.c4_config(n_hosts=1_000_000))
+eng = Engine(phold.c4_config(n_hosts=int(os.environ.get("QT_HOSTS", 1_000_000))))
 eng.boot()
 eng.run(20)
 eng.set_timing(True, ["process", "insert", "plan"])
