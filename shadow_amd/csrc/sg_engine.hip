@@ -327,7 +327,7 @@ struct Dev {
     uint64_t* outn;           // [G]
     uint64_t* sent;           // [G]
     // debug
-    uint64_t* stamps;         // [P][SG_STAMP_W] k_proc phase stamps + [SG_STAMP_W] k_plan's + one row
+    uint64_t* stamps;         // [P][SG_STAMP_W] k_proc phase stamps + one spare row + one row
                               // per k_scatter workgroup (SG_STAMPS=1), else null
     sg_trace_rec* trace;
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
@@ -3334,7 +3334,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.rs, 1);
     ALLOC(e->d_pend, 1);
     if (D.trace_cap) ALLOC(D.trace, D.trace_cap);
-    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (2 * P + D.G3 + D.G1 + 3) * SG_STAMP_W);  // + k_plan's, k_scatter's
+    if (env_u32("SG_STAMPS", 0)) ALLOC(D.stamps, (2 * P + D.G3 + D.G1 + 3) * SG_STAMP_W);  // + a spare row, k_scatter's
     D.wlog_cap = D.trace_cap ? 1u << 20 : 0;
     if (D.wlog_cap) ALLOC(D.wlog, 2 * D.wlog_cap);
 #undef ALLOC

@@ -184,7 +184,7 @@ class Engine:
 
     def stamps(self) -> np.ndarray:
         """[2P + G3 + G1 + 3, 32] stamps of the last round (SG_STAMPS=1): P rows of
-        k_proc phase stamps, k_plan's row, then one row per k_scatter workgroup
+        k_proc phase stamps, one spare row, then one row per k_scatter workgroup
         {start, setup, events, end, role, n}; or empty."""
         n = C.c_uint64()
         L.check(L.lib().sg_engine_stamps(self.h, None, 0, C.byref(n)))

@@ -1,6 +1,7 @@
-"""GPU: the sharded engine path (k_peer_scan, k_pack, k_fill, k_insert_recv,
-k_window: one all-to-all of fixed-size blocks per step, the window from the
-block headers, drain steps) with several shards on one device.  The
+"""GPU: the sharded engine path (k_proc writing the outbox and exchange
+blocks, k_count and k_scatter reserving and inserting the received events: one
+all-to-all of fixed-size blocks per step, the window from the block headers,
+drain steps) with several shards on one device.  The
 all-to-all is done in-process with block copies on the shards' common stream,
 exactly as shadow_amd.dist does over RCCL; results must equal the unsharded
 oracle."""
