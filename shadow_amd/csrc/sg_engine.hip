@@ -1621,8 +1621,9 @@ __device__ void reset_consumed(const Dev& d) {
 //            here instead (same-round self events, host_single.c:237-267);
 //   phase B  one lane per send, two sends in flight per lane: destination,
 //            path record, reliability test, delivery time;
-//   phase C  per active host, in send order: srcHostEventID, endTime drop,
-//            barrier bump, staging;
+//   phase C  one lane per send record: srcHostEventID, endTime drop, barrier
+//            bump, staging (with delay-only path records every send is kept,
+//            so phases B and C run as one pass without the barrier);
 //   count    the staged local events by calendar bucket (LDS bins over the
 //            dead event image) and one reservation per (partition, bucket).
 constexpr uint32_t HPT = HPMAX / K2_T;     // active hosts per lane, at most
@@ -2131,92 +2132,141 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 
     // ---- phase B: one lane per send, two in flight (header records skipped)
     const uint32_t nsend = s_nsend < d.ECAP ? s_nsend : d.ECAP;
-    for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
-        const uint32_t i1 = i0 + K2_T;
-        const bool v1 = i1 < nsend;
-        const Rec r0 = sget(i0);
-        const Rec r1 = sget(v1 ? i1 : i0);  // an index select, not a conditional load
-        const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
-        const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
-        uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
-        if constexpr (EXACT) {
-            const uint2 a0 = d.nearw[g0], b0 = d.nearw[g0 + 1];
-            const uint2 a1 = d.nearw[g1], b1 = d.nearw[g1 + 1];
-            near_resolve(d, x0, a0, b0, vd0, dst0);
-            near_resolve(d, x1, a1, b1, vd1, dst1);
-        } else {
-            const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
-            dst0 = dst_resolve(d, x0, g0, pb0, vd0);
-            dst1 = dst_resolve(d, x1, g1, pb1, vd1);
+    // Delay-only path records (no loss): every send is kept, so a send's
+    // srcHostEventID is its host's counter plus its place in the host's list
+    // and phases B and C run as one pass (no barrier, no walk back).
+    if (d.pair_fmt == PAIR_DELAY) {
+        if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();  // no phase B of its own
+        for (uint32_t i = tid; i < nsend; i += K2_T) {
+            const Rec r = sget(i);
+            const int32_t x = (int32_t)(uint32_t)r.k;
+            const uint32_t g = dst_guess(d, x);
+            uint32_t vd = 0, dst = 0;
+            if constexpr (EXACT) {
+                const uint2 a0 = d.nearw[g], b0 = d.nearw[g + 1];
+                near_resolve(d, x, a0, b0, vd, dst);
+            } else {
+                const Probe pb = dst_probe(d, g);
+                dst = dst_resolve(d, x, g, pb, vd);
+            }
+            if (r.k & HDR_REC) {
+                if (r.k & PAD_REC) continue;
+                // a host's header: its counter after all its (kept) sends
+                const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
+                uint64_t evc = r.a;
+                for (uint32_t k = i + 1; k <= i + ns; ++k) evc += (sget(k).k & HDR_REC) ? 0u : 1u;
+                d.hs[sbase + s_act[j]].evc = evc;
+                continue;
+            }
+            const uint32_t j = (uint32_t)(r.a >> 52);
+            const PairRec pr = pair_of(s_vh[j] & 0xFFFFu, vd, want_jump);
+            const uint32_t sb = s_sb[j];
+            const Rec hd = sget(sb);
+            a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // topology.c:1374-1385
+            if (d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j] & 0xFFFFu) * d.V + vd], 1u);  // worker.c:279
+            const uint64_t sq = hd.a + (i - sb - 1);   // event.c:38: the host's real sends precede its pads
+            uint64_t tn = S + (r.a & M52) + pr.delay;  // worker.c:275-277
+            if (tn >= d.end_time) {                    // scheduler.c:343-346
+                ++a.ctr[C_DROPEND];
+                continue;
+            }
+            const uint32_t sg = d.lo + sbase + s_act[j];
+            if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
+            if (dst != sg && tn < E) {                   // host_single.c:180-184
+                tn = E;
+                ++a.ctr[C_BUMPED];
+            }
+            const uint32_t h = (uint32_t)hd.k;
+            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
         }
-        asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
-        const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
-        const PairRec pr0 = pair_of(s_vh[j0] & 0xFFFFu, vd0, want_jump);
-        const PairRec pr1 = pair_of(s_vh[j1] & 0xFFFFu, vd1, want_jump);
-        if (!(r0.k & HDR_REC)) {
-            const uint64_t bt = S + (r0.a & M52);
-            const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
-            a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
-            const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
-            if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
-            const uint64_t rel = bt + pr0.delay - S;  // worker.c:275-277
-            if (rel >> 40) a.overflow = true;
-            sput(i0, Rec{((uint64_t)keep << 63) | ((uint64_t)j0 << 40) | rel, dst0});
+    } else {
+        for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
+            const uint32_t i1 = i0 + K2_T;
+            const bool v1 = i1 < nsend;
+            const Rec r0 = sget(i0);
+            const Rec r1 = sget(v1 ? i1 : i0);  // an index select, not a conditional load
+            const int32_t x0 = (int32_t)(uint32_t)r0.k, x1 = (int32_t)(uint32_t)r1.k;
+            const uint32_t g0 = dst_guess(d, x0), g1 = dst_guess(d, x1);
+            uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
+            if constexpr (EXACT) {
+                const uint2 a0 = d.nearw[g0], b0 = d.nearw[g0 + 1];
+                const uint2 a1 = d.nearw[g1], b1 = d.nearw[g1 + 1];
+                near_resolve(d, x0, a0, b0, vd0, dst0);
+                near_resolve(d, x1, a1, b1, vd1, dst1);
+            } else {
+                const Probe pb0 = dst_probe(d, g0), pb1 = dst_probe(d, g1);
+                dst0 = dst_resolve(d, x0, g0, pb0, vd0);
+                dst1 = dst_resolve(d, x1, g1, pb1, vd1);
+            }
+            asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
+            const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
+            const PairRec pr0 = pair_of(s_vh[j0] & 0xFFFFu, vd0, want_jump);
+            const PairRec pr1 = pair_of(s_vh[j1] & 0xFFFFu, vd1, want_jump);
+            if (!(r0.k & HDR_REC)) {
+                const uint64_t bt = S + (r0.a & M52);
+                const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
+                a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
+                const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
+                if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
+                const uint64_t rel = bt + pr0.delay - S;  // worker.c:275-277
+                if (rel >> 40) a.overflow = true;
+                sput(i0, Rec{((uint64_t)keep << 63) | ((uint64_t)j0 << 40) | rel, dst0});
+            }
+            if (v1 && !(r1.k & HDR_REC)) {
+                const uint64_t bt = S + (r1.a & M52);
+                const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
+                a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
+                const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
+                if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1], 1u);
+                const uint64_t rel = bt + pr1.delay - S;
+                if (rel >> 40) a.overflow = true;
+                sput(i1, Rec{((uint64_t)keep << 63) | ((uint64_t)j1 << 40) | rel, dst1});
+            }
         }
-        if (v1 && !(r1.k & HDR_REC)) {
-            const uint64_t bt = S + (r1.a & M52);
-            const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
-            a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
-            const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
-            if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1], 1u);
-            const uint64_t rel = bt + pr1.delay - S;
-            if (rel >> 40) a.overflow = true;
-            sput(i1, Rec{((uint64_t)keep << 63) | ((uint64_t)j1 << 40) | rel, dst1});
-        }
-    }
-    __syncthreads();
-    if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();
+        if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- phase C: one lane per send record.  A send's srcHostEventID is its
-    // host's counter plus the kept sends before it in the host's order
-    // (worker.c:268-279, event.c:38): a short walk back over the host's
-    // records; then endTime drop, barrier bump, staging.
-    for (uint32_t i = tid; i < nsend; i += K2_T) {
-        const Rec r = sget(i);
-        if (r.k & HDR_REC) {
-            if (r.k & PAD_REC) continue;
-            // a host's header: its counter after all its kept sends
-            const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
-            uint64_t evc = r.a;
-            for (uint32_t k = i + 1; k <= i + ns; ++k) evc += sget(k).a >> 63;
-            d.hs[sbase + s_act[j]].evc = evc;
-            continue;
+        // ---- phase C: one lane per send record.  A send's srcHostEventID is its
+        // host's counter plus the kept sends before it in the host's order
+        // (worker.c:268-279, event.c:38): a short walk back over the host's
+        // records; then endTime drop, barrier bump, staging.
+        for (uint32_t i = tid; i < nsend; i += K2_T) {
+            const Rec r = sget(i);
+            if (r.k & HDR_REC) {
+                if (r.k & PAD_REC) continue;
+                // a host's header: its counter after all its kept sends
+                const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
+                uint64_t evc = r.a;
+                for (uint32_t k = i + 1; k <= i + ns; ++k) evc += sget(k).a >> 63;
+                d.hs[sbase + s_act[j]].evc = evc;
+                continue;
+            }
+            const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
+            const uint32_t sb = s_sb[j];
+            const Rec hd = sget(sb);
+            uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
+            for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
+            const bool keep = (r.a >> 63) != 0;
+            if (!keep) {
+                ++a.ctr[C_DROPREL];
+                continue;
+            }
+            const uint64_t sq = evc;                // event.c:38
+            uint64_t tn = S + (r.a & M40);
+            if (tn >= d.end_time) {                 // scheduler.c:343-346
+                ++a.ctr[C_DROPEND];
+                continue;
+            }
+            const uint32_t dst = (uint32_t)r.k;
+            const uint32_t sg = d.lo + sbase + s_act[j];
+            if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
+            if (dst != sg && tn < E) {              // host_single.c:180-184
+                tn = E;
+                ++a.ctr[C_BUMPED];
+            }
+            const uint32_t h = (uint32_t)hd.k;
+            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
         }
-        const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
-        const uint32_t sb = s_sb[j];
-        const Rec hd = sget(sb);
-        uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
-        for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
-        const bool keep = (r.a >> 63) != 0;
-        if (!keep) {
-            ++a.ctr[C_DROPREL];
-            continue;
-        }
-        const uint64_t sq = evc;                // event.c:38
-        uint64_t tn = S + (r.a & M40);
-        if (tn >= d.end_time) {                 // scheduler.c:343-346
-            ++a.ctr[C_DROPEND];
-            continue;
-        }
-        const uint32_t dst = (uint32_t)r.k;
-        const uint32_t sg = d.lo + sbase + s_act[j];
-        if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
-        if (dst != sg && tn < E) {              // host_single.c:180-184
-            tn = E;
-            ++a.ctr[C_BUMPED];
-        }
-        const uint32_t h = (uint32_t)hd.k;
-        if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
     }
     __syncthreads();  // staging done: sh.nloc final, bins complete
     if (d.outn) {
