@@ -276,6 +276,7 @@ struct Dev {
     uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
     bool snd_lds;                // k_proc's send records in LDS while they fit
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
+    uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
@@ -1930,6 +1931,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint64_t W = d.W, bS = rs->bS;
     const uint32_t bSr = (uint32_t)(bS % R);
     const bool self_possible = E - S > d.vself_min;
+    // few due events (a small shard): every host records its sends and the
+    // fused pass resolves them one lane each (shorter than the inline chain)
+    const uint32_t lmax = d.pair_fmt == PAIR_DELAY && n + nact <= d.rec_all ? 0u : d.light_max;
     bool horizon = false;
     const uint64_t bSW = bS * W;
     auto count_local = [&](uint64_t t) {  // one staged local event into the bucket bins
@@ -2041,7 +2045,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             const bool boot = ((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0);
                             ns += boot ? d.load : 1u;
                         }
-                        if (ns <= d.light_max && q < d.light_q) {
+                        if (ns <= lmax && q < d.light_q) {
                             // light host (most hosts in steady state): the whole
                             // body here, both sends' loads in flight together
                             int32_t x0 = 0, x1 = 0, c0 = 0, c1 = 0;
@@ -3313,6 +3317,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // chains then overlap every other lane's instead of running after them
     D.light_q = env_u32z("SG_LIGHT_Q", 1);
     D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
+    D.rec_all = env_u32z("SG_REC_ALL", K2_T);
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
