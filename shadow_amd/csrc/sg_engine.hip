@@ -2119,11 +2119,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
                 sput(k++, Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
             });
+            const uint32_t nreal = k - base - 1;  // sends with a destination
             for (; k <= base + ns; ++k) sput(k, Rec{0, HDR_REC | PAD_REC});  // draws that selected no host
-            // {rng, pops, digest} now; evc after phase C
+            // {rng, pops, digest} now; evc now too when every send is kept, else
+            // after phase C
             HostState* hp = d.hs + lh;
             reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
-            hp->digest = c.s.digest;
+            if (d.pair_fmt == PAIR_DELAY) {  // every send kept: the final counter is known now
+                reinterpret_cast<ulonglong2*>(hp)[1] = make_ulonglong2(c.s.digest, c.s.evc + nreal);
+            } else {
+                hp->digest = c.s.digest;
+            }
             if (st0) stamp[12] = wait_stamp();
             if (stamp && tid == 0 && q == 1) stamp[24] = wait_stamp();
         }
@@ -2153,15 +2159,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 const Probe pb = dst_probe(d, g);
                 dst = dst_resolve(d, x, g, pb, vd);
             }
-            if (r.k & HDR_REC) {
-                if (r.k & PAD_REC) continue;
-                // a host's header: its counter after all its (kept) sends
-                const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
-                uint64_t evc = r.a;
-                for (uint32_t k = i + 1; k <= i + ns; ++k) evc += (sget(k).k & HDR_REC) ? 0u : 1u;
-                d.hs[sbase + s_act[j]].evc = evc;
-                continue;
-            }
+            if (r.k & HDR_REC) continue;  // header and pad records: phase A wrote the counter
             const uint32_t j = (uint32_t)(r.a >> 52);
             const PairRec pr = pair_of(s_vh[j] & 0xFFFFu, vd, want_jump);
             const uint32_t sb = s_sb[j];
