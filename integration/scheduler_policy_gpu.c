@@ -6,15 +6,26 @@
  * policy string, options.c help, CMake source list).  It maps Host* / Event* onto
  * the opaque ids and handles of include/shadowgpu.h §3; the library never
  * dereferences a Shadow pointer.  The vtable it fills is
- * core/scheduler/scheduler_policy.h:31-51.
+ * core/scheduler/scheduler_policy.h:31-51, and the constructor has the same
+ * `(void)` shape as its siblings at scheduler_policy.h:53-58.
  *
- * tests/test_integration_glue.py compiles this file -fsyntax-only against the
- * unmodified reference headers (and conda GLib) whenever /root/reference is
- * present.  Two additions the maintainer makes are therefore declared here:
+ * No other reference file needs an edit beyond the registration lines:
  *   - the enum value SP_PARALLEL_GPU (scheduler_policy.h:12-29): define
  *     SHADOW_HAS_SP_PARALLEL_GPU once it is in the enum;
- *   - event_getSrcHost / event_getSrcHostEventID, two
- *     one-line getters added to core/work/event.{h,c}.
+ *   - srcHostEventID.  Event is opaque outside event.c and event.h has no getter
+ *     for it.  event_compare (event.c:110-153) uses it only to order events of
+ *     the same (src, dst) pair at equal times.  Every event is pushed right after
+ *     event_new_ on the thread executing its source host (worker.c:229-230,
+ *     297-300), so one source's pushes arrive in creation order, minus the
+ *     events scheduler_push drops at endTime (scheduler.c:343-346).  A per-source
+ *     push counter is therefore a monotone relabelling of srcHostEventID and
+ *     gives the same pop order.  A maintainer who adds the one-line getter
+ *     event_getSrcHostEventID to event.{h,c} defines
+ *     SHADOW_HAS_EVENT_SRCID and the exact value is passed instead.
+ *
+ * tests/test_integration_glue.py compiles this file against the unmodified
+ * reference headers (and conda GLib) whenever /root/reference is present, and
+ * runs it under AddressSanitizer through tests/glue_harness.c.
  */
 #include <glib.h>
 #include <pthread.h>
@@ -32,19 +43,20 @@
 #define SG_POLICY_TYPE ((SchedulerPolicyType)(SP_PARALLEL_THREAD_PERHOST + 1))
 #endif
 
-/* added to core/work/event.{h,c} */
-gpointer event_getSrcHost(Event* event);
-guint64 event_getSrcHostEventID(Event* event);
+#ifdef SHADOW_HAS_EVENT_SRCID
+guint64 event_getSrcHostEventID(Event* event); /* INTEGRATION.md §3 */
+#endif
 
-SchedulerPolicy* schedulerpolicygpu_new(guint nWorkers);
+SchedulerPolicy* schedulerpolicygpu_new(void);
 
 typedef struct { GQuark id; pthread_t thread; } PendingHost;
 
 typedef struct {
-    guint nWorkers;
-    GArray* pending;            /* addHost calls, replayed once the host count is known */
+    GArray* pending;            /* addHost calls, replayed once every host is known */
     GHashTable* idToHost;       /* GQuark -> Host* */
-    GHashTable* threadToHosts;  /* pthread_t -> GQueue* (getAssignedHosts result) */
+    GHashTable* idToIndex;      /* GQuark -> registration index + 1 (read-only after create) */
+    guint64* pushCount;         /* per source host: pushes so far (srcHostEventID order) */
+    GHashTable* threadToHosts;  /* pthread_t -> GQueue* (getAssignedHosts result; owns it) */
     GMutex lock;
     GOnce once;
     sg_policy* p;
@@ -53,14 +65,25 @@ typedef struct {
 #define SGCHK(x) do { int _rc = (x); if (_rc != SG_OK) error("gpu policy: %s", sg_last_error()); } while (0)
 
 /* addHost runs single-threaded from scheduler_start (scheduler.c:488-531); the
- * device policy is created at the first call after it, when every host is known. */
+ * device policy is created at the first call after it, when every host and every
+ * worker thread is known (the worker count is the number of distinct threads
+ * hosts were assigned to, scheduler.c:437-486). */
 static gpointer _gpu_create(gpointer arg) {
     GpuPolicyData* d = arg;
-    sg_policy_params prm = {.n_threads = d->nWorkers, .max_hosts = d->pending->len,
-                            .queue_cap = 0, .device = 0};
-    SGCHK(sg_policy_create(&prm, &d->p));
+    GHashTable* threads = g_hash_table_new(g_direct_hash, g_direct_equal);
     for (guint i = 0; i < d->pending->len; i++) {
         PendingHost* ph = &g_array_index(d->pending, PendingHost, i);
+        g_hash_table_add(threads, GSIZE_TO_POINTER((gsize)ph->thread));
+    }
+    guint nThreads = g_hash_table_size(threads);
+    g_hash_table_destroy(threads);
+    sg_policy_params prm = {.n_threads = nThreads ? nThreads : 1, .max_hosts = d->pending->len,
+                            .queue_cap = 0, .device = 0};
+    SGCHK(sg_policy_create(&prm, &d->p));
+    d->pushCount = g_new0(guint64, d->pending->len ? d->pending->len : 1);
+    for (guint i = 0; i < d->pending->len; i++) {
+        PendingHost* ph = &g_array_index(d->pending, PendingHost, i);
+        g_hash_table_insert(d->idToIndex, GUINT_TO_POINTER(ph->id), GUINT_TO_POINTER(i + 1));
         SGCHK(sg_policy_add_host(d->p, ph->id, (uint64_t)ph->thread));
     }
     return d->p;
@@ -77,7 +100,10 @@ static void _gpu_addHost(SchedulerPolicy* policy, Host* host, pthread_t thread) 
     g_hash_table_insert(d->idToHost, GUINT_TO_POINTER(ph.id), host);
 }
 
-static GQueue* _gpu_getAssignedHosts(SchedulerPolicy* policy) {   /* host_single.c:146-165 */
+/* host_single.c:146-165.  Called on each worker at boot and again at shutdown
+ * (scheduler.c:78-113); the queue returned last time is freed by the hash
+ * table's value-destroy function when the new one replaces it. */
+static GQueue* _gpu_getAssignedHosts(SchedulerPolicy* policy) {
     GpuPolicyData* d = policy->data;
     sg_policy* p = _gpu(policy);
     pthread_t self = pthread_self();
@@ -90,21 +116,36 @@ static GQueue* _gpu_getAssignedHosts(SchedulerPolicy* policy) {   /* host_single
         g_queue_push_tail(q, g_hash_table_lookup(d->idToHost, GUINT_TO_POINTER(ids[i])));
     g_free(ids);
     g_mutex_lock(&d->lock);
-    GQueue* old = g_hash_table_lookup(d->threadToHosts, GUINT_TO_POINTER(self));
-    g_hash_table_insert(d->threadToHosts, GUINT_TO_POINTER(self), q);
+    g_hash_table_insert(d->threadToHosts, GSIZE_TO_POINTER((gsize)self), q);
     g_mutex_unlock(&d->lock);
-    if (old) g_queue_free(old);
     return q;
+}
+
+static guint64 _gpu_srcEventID(GpuPolicyData* d, Event* event, GQuark src) {
+#ifdef SHADOW_HAS_EVENT_SRCID
+    (void)d; (void)src;
+    return event_getSrcHostEventID(event);
+#else
+    (void)event;
+    guint idx = GPOINTER_TO_UINT(g_hash_table_lookup(d->idToIndex, GUINT_TO_POINTER(src)));
+    utility_assert(idx != 0);
+    /* one source host runs on one thread at a time; the atomic only keeps a
+     * host that migrates between rounds (host_steal-style) well defined */
+    return __atomic_fetch_add(&d->pushCount[idx - 1], 1, __ATOMIC_RELAXED);
+#endif
 }
 
 /* push takes the caller's reference (scheduler.c:354); the bumped time is written
  * back into the event as host_single.c:181 does. */
 static void _gpu_push(SchedulerPolicy* policy, Event* event, Host* srcHost, Host* dstHost,
                       SimulationTime barrier) {
+    GpuPolicyData* d = policy->data;
+    sg_policy* p = _gpu(policy);
+    GQuark src = host_getID(srcHost);
     SimulationTime t = 0;
-    SGCHK(sg_policy_push(_gpu(policy), (uint64_t)pthread_self(), (uint64_t)(uintptr_t)event,
-                         event_getTime(event), host_getID(srcHost), host_getID(dstHost),
-                         event_getSrcHostEventID(event), barrier, &t));
+    SGCHK(sg_policy_push(p, (uint64_t)pthread_self(), (uint64_t)(uintptr_t)event,
+                         event_getTime(event), src, host_getID(dstHost),
+                         _gpu_srcEventID(d, event, src), barrier, &t));
     event_setTime(event, t);
 }
 
@@ -134,20 +175,22 @@ static void _gpu_free(SchedulerPolicy* policy) {                      /* schedul
         g_free(hs);
         sg_policy_destroy(d->p);
     }
+    g_free(d->pushCount);
     g_array_free(d->pending, TRUE);
     g_hash_table_destroy(d->idToHost);
-    g_hash_table_destroy(d->threadToHosts);
+    g_hash_table_destroy(d->idToIndex);
+    g_hash_table_destroy(d->threadToHosts); /* frees every queue still held */
     g_mutex_clear(&d->lock);
     g_free(d);
     MAGIC_CLEAR(policy);
     g_free(policy);
 }
 
-SchedulerPolicy* schedulerpolicygpu_new(guint nWorkers) {
+SchedulerPolicy* schedulerpolicygpu_new(void) {
     GpuPolicyData* d = g_new0(GpuPolicyData, 1);
-    d->nWorkers = nWorkers;
     d->pending = g_array_new(FALSE, FALSE, sizeof(PendingHost));
     d->idToHost = g_hash_table_new(g_direct_hash, g_direct_equal);
+    d->idToIndex = g_hash_table_new(g_direct_hash, g_direct_equal);
     d->threadToHosts = g_hash_table_new_full(g_direct_hash, g_direct_equal, NULL,
                                              (GDestroyNotify)g_queue_free);
     g_mutex_init(&d->lock);

@@ -33,3 +33,33 @@ def test_glue_compiles_against_reference_headers(tmp_path, registered):
     for sym in ("sg_policy_create", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
                 "sg_policy_remaining", "sg_policy_thread_hosts", "sg_policy_add_host"):
         assert f" U {sym}" in nm, sym
+
+
+@pytest.mark.skipif(not os.path.isdir(REF) or not all(os.path.isdir(g) for g in GLIB),
+                    reason="reference sources or conda GLib headers absent")
+@pytest.mark.parametrize("exact_id", [False, True])
+def test_glue_runs_under_asan(tmp_path, exact_id):
+    """The glue's own logic under AddressSanitizer (tests/glue_harness.c: test
+    doubles for the Shadow functions it calls and for sg_policy_*): each worker
+    calls getAssignedHosts twice as at boot and shutdown (scheduler.c:78-113),
+    pops return a thread's own hosts in event_compare order with the per-source
+    srcHostEventID relabelling, free unrefs what is left."""
+    src = os.path.join(ROOT, "integration", "scheduler_policy_gpu.c")
+    harness = os.path.join(ROOT, "tests", "glue_harness.c")
+    exe = str(tmp_path / "glue")
+    flags = ["-std=gnu99", "-D_GNU_SOURCE", "-g", "-O1", "-fsanitize=address",
+             "-fno-omit-frame-pointer", "-I" + REF, "-I" + os.path.join(ROOT, "include")] + \
+            ["-I" + g for g in GLIB]
+    if exact_id:
+        # the maintainer's getter variant: the harness supplies event_getSrcHostEventID
+        flags += ["-DSHADOW_HAS_EVENT_SRCID", "-DHARNESS_EXACT_ID"]
+    r = subprocess.run(["gcc", src, harness, "-o", exe] + flags +
+                       ["-L/opt/conda/lib", "-Wl,-rpath,/opt/conda/lib", "-lglib-2.0", "-lpthread"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               G_SLICE="always-malloc")  # GLib slices through malloc, so ASan sees them
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "glue harness ok" in r.stdout
