@@ -60,6 +60,7 @@ class EngineShard:
             exchange_cap = default_exchange_cap(n_local, world)
         self.world = world
         self.rank = rank
+        self.comm = None  # the native step loop's communicator (enable_native)
         self.eng = Engine(cfg, device=device, shard_index=rank, shard_count=world,
                           queue_cap=queue_cap, exchange_cap=exchange_cap,
                           trace_capacity=trace_capacity, stream=self.stream.cuda_stream)
@@ -85,13 +86,18 @@ class EngineShard:
         default process group; graph_batch > 0 replays captured hipGraphs.
 
         Every decision is collective, so all ranks take the native loop or none:
-        each rank probes RCCL first (no collective), the flags are AND-reduced,
-        rank 0's id is broadcast with its own flag, and after the collective
-        ncclCommInitRank a second AND-reduce confirms every rank got a
+        each rank's local checks (RCCL opens and exports its symbols, the device
+        index is valid) come first with no collective, the flags are
+        AND-reduced, rank 0's id is broadcast with its own flag, and after the
+        collective ncclCommInitRank a second AND-reduce confirms every rank got a
         communicator (a rank that did not releases nothing, the others close
-        theirs).  Raises on every rank when the native loop is unavailable."""
+        theirs).  Raises on every rank when the native loop is unavailable.
+        A rank whose ncclCommInitRank itself fails after the others entered it
+        can still leave them blocked inside RCCL's init: that failure is
+        RCCL's, after every check this side can make locally."""
         from .engine import Comm
-        if not self._all_ok(Comm.available()):
+        local_ok = Comm.available() and 0 <= self.dev.index < torch.cuda.device_count()
+        if not self._all_ok(local_ok):
             raise RuntimeError("RCCL cannot be opened on every rank")
         uid = torch.zeros(129, dtype=torch.uint8)  # [0]: rank 0 made an id; [1:]: the id
         if self.rank == 0:
@@ -223,14 +229,37 @@ def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16) -> i
     return n
 
 
+def _any_rank(flag: bool, dev) -> bool:
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64)
+    if _backend() == "nccl":
+        t = t.to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(int(t.item()))
+
+
 def run_until_round(shard, world: int, rounds: int, check_every: int = 8) -> int:
-    """Run steps until the shard has completed `rounds` windows (or is done)."""
+    """Run steps until every shard has completed `rounds` windows (or is done),
+    in batches of check_every steps (so it may run past `rounds`).  The decision
+    is collective: every rank runs the same number of steps."""
     n = 0
+    dev = getattr(shard, "dev", None)
     while True:
         st = shard.stats()
-        if st["done"] or st["rounds"] >= rounds:
+        if not _any_rank(not (st["done"] or st["rounds"] >= rounds), dev):
             return n
         n += run(shard, world, check_every, check_every=1 << 30)
+
+
+def finish_round(shard, world: int, max_steps: int = 1 << 16) -> dict:
+    """Run single steps until every rank is at a round boundary (phase 0) or
+    done; returns this shard's stats there."""
+    dev = getattr(shard, "dev", None)
+    for _ in range(max_steps):
+        st = shard.stats()
+        if not _any_rank(not (st["phase"] == 0 or st["done"]), dev):
+            return st
+        run(shard, world, 1, check_every=1 << 30)
+    raise RuntimeError("no round boundary within max_steps drain steps")
 
 
 # ------------------------------------------------------------------ bench ----
@@ -247,10 +276,16 @@ def _gather_rows(vals, dev):
     return [o.tolist() for o in out]
 
 
-def bench(args):
+def _cuda_sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def bench(args, make_shard=None):
     """bench.py --gpus N under torch.distributed.run: the 1M-host PHOLD over N
     GPUs (strong scaling: the host count stays 1M).  Returns the JSON dict on
-    rank 0, None elsewhere."""
+    rank 0, None elsewhere.  make_shard(cfg, rank, world, device) builds the
+    rank's shard: EngineShard (the product) unless a CPU test passes its own."""
     from . import phold
     from ._lib import KERNEL_CLASSES
     rank, world, local = _env_rank()
@@ -258,13 +293,17 @@ def bench(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with "
                          "torch.distributed.run --nproc-per-node N")
     dev = 0 if args.same_device else local
-    torch.cuda.set_device(dev)
+    if make_shard is None:
+        make_shard = EngineShard
+        torch.cuda.set_device(dev)
     if args.dist_backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-    else:  # rehearsal of the multi-rank path on one GPU
+    else:  # rehearsal of the multi-rank path on one GPU (or a CPU test)
         dist.init_process_group(args.dist_backend)
+    # small collectives live where the backend wants them
+    cdev = torch.device("cuda", dev) if args.dist_backend == "nccl" else torch.device("cpu")
     cfg = phold.c4_config(n_hosts=args.hosts)
-    shard = EngineShard(cfg, rank, world, dev)
+    shard = make_shard(cfg, rank, world, dev)
     if args.dist_backend == "nccl" and not args.py_steps:
         try:
             shard.enable_native(args.graph)
@@ -280,7 +319,7 @@ def bench(args):
     run_until_round(shard, world, 2)
     shard.exchange_peak(reset=True)
     run_until_round(shard, world, 2 + max(args.warmup, 8))
-    peak = torch.tensor([shard.exchange_peak()], dtype=torch.int64, device=shard.dev)
+    peak = torch.tensor([shard.exchange_peak()], dtype=torch.int64, device=cdev)
     dist.all_reduce(peak, op=dist.ReduceOp.MAX)
     cap = -(-(int(peak.item()) * 5 // 4 + 256) // 256) * 256
     shard.set_exchange_cap(cap)
@@ -289,26 +328,31 @@ def bench(args):
     s0 = shard.stats()
     dist.barrier()
     shard.sync()
-    torch.cuda.synchronize()
+    _cuda_sync()
     t0 = time.perf_counter()
     run(shard, world, args.steps, check_every=1 << 30)
     shard.sync()
-    torch.cuda.synchronize()
+    _cuda_sync()
     dt = time.perf_counter() - t0
     dist.barrier()
     s1 = shard.stats()
-    t = torch.tensor([dt], dtype=torch.float64, device=shard.dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=cdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # the parity point: a step boundary where the round is complete on every
+    # rank.  A drain step (phase 1) has popped the next window's events before
+    # `rounds` counts it, so finish it first (untimed; the drain decision is the
+    # same on every rank, the check is collective all the same)
+    end = finish_round(shard, world)
     fp = shard.fingerprint()  # this shard's term of the end-of-region state fingerprint
     tot = torch.tensor([s1["pops"] - s0["pops"], s1["rounds"] - s0["rounds"],
-                        s1["exchange_steps"] - s0["exchange_steps"], s1["overflow"],
+                        s1["exchange_steps"] - s0["exchange_steps"], end["overflow"],
                         int(s1["done"]), fp - (1 << 64 if fp >= 1 << 63 else 0)],
-                       dtype=torch.int64, device=shard.dev)
+                       dtype=torch.int64, device=cdev)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     tmax = float(t.item())
     total, rounds_sum, steps_sum, ovf, done_sum, fp = (int(x) for x in tot.tolist())
     fp &= (1 << 64) - 1
-    end_round = s1["rounds"]
+    end_round = end["rounds"]
     # per-rank kernel times over the next steps (HIP events on the engine stream;
     # the exchange class is this rank's RCCL all-to-all: its wait for the slowest
     # rank plus the transfer, the barrier idle time of scheduler.c:380-389)
@@ -318,7 +362,7 @@ def bench(args):
         run(shard, world, kr, check_every=1 << 30)
         kt = shard.eng.kernel_times()
         shard.eng.set_timing(False)
-        rows = _gather_rows([kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES], shard.dev)
+        rows = _gather_rows([kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES], cdev)
     else:
         rows = None
     shard.close_native()

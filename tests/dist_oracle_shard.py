@@ -38,6 +38,10 @@ class OracleShard:
         self.loc_min = (1 << 64) - 2
         self.loc_jmin = M64
         self.steps = 0
+        self.peak = 0
+        # the EngineShard surface dist.bench uses
+        self.dev = None
+        self.comm = None
 
     def boot(self):
         self.sim.boot()
@@ -62,6 +66,7 @@ class OracleShard:
                                          ev["dst"].astype(np.int64)], 1) if len(ev) else \
                     np.zeros((0, 3), np.int64)
             self.sent = [0] * self.world
+            self.peak = max([self.peak] + [len(self.outq[p]) for p in range(self.world) if p != self.rank])
             m = self.sim.local_min()
             if len(out):
                 m = min(m, int(out["time"].min()))
@@ -115,4 +120,29 @@ class OracleShard:
     def stats(self):
         st = self.sim.stats()
         st["exchange_steps"] = self.steps
+        st["phase"] = self.phase
+        st.setdefault("overflow", 0)
         return st
+
+    # ---- the rest of EngineShard's surface (dist.bench)
+    def exchange_peak(self, reset=False):
+        v = self.peak
+        if reset:
+            self.peak = 0
+        return v
+
+    def set_exchange_cap(self, cap):
+        self.xcap = cap
+        self.rows = HDR + cap
+        self.recv = torch.zeros((self.world, self.rows, 3), dtype=torch.int64)
+
+    def sync(self):
+        pass
+
+    def close_native(self):
+        pass
+
+    def fingerprint(self):
+        from shadow_amd.trace import state_fingerprint
+        hs = self.sim.host_state()
+        return state_fingerprint(self.bounds[self.rank], hs["digest"], hs["pops"], hs["rng"], hs["ev"])

@@ -1,0 +1,132 @@
+"""GPU, two processes: the multi-rank engine path of shadow_amd.dist with real
+EngineShards, the way the N > 1 bench runs it (one process per rank, the step
+protocol driven by dist.run / run_until_round / finish_round, one all-to-all per
+step).  Both ranks share GPU 0, so the exchange goes over gloo through host
+memory (RCCL needs one GPU per rank; the RCCL native loop is covered at world 1
+in test_gpu_sharded.py).  This replaces the execute barrier and MIN of
+scheduler.c:386-398 and master.c:450-480 with the header-carried window.
+
+  configs[3] at 1M hosts, 2 x 500k, against the oracle's per-round fixture
+  configs[4] gossip, 100k hosts, the whole run, against its whole-run fixture
+  bench.py --gpus 2 --same-device --dist-backend gloo: parity.match true
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_fixtures.json")))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kind, xcap, stop_round, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from shadow_amd import dist as D
+    from shadow_amd import phold
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        cfg = phold.c4_config(n_hosts=1_000_000) if kind == "c4" else phold.c5_config()
+        sh = D.EngineShard(cfg, rank, world, 0, exchange_cap=xcap)
+        sh.boot()
+        if stop_round:
+            D.run_until_round(sh, world, stop_round, check_every=4)
+            st = D.finish_round(sh, world)
+        else:
+            D.run(sh, world, check_every=8)
+            st = sh.stats()
+        fp = sh.fingerprint()
+        q.put((rank, None, st, fp))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as exc:  # reported by the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+        raise
+
+
+def _run(kind, world, xcap, stop_round=0, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, xcap, stop_round, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=timeout) for _ in range(world)]
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    errs = [r[1] for r in res if r[1]]
+    assert not errs, errs[0]
+    for p in ps:
+        assert p.exitcode == 0
+    return sorted(res, key=lambda x: x[0])
+
+
+@pytest.mark.parametrize("xcap", [None, 8192])
+def test_c4_1m_two_processes(xcap):
+    """configs[3]: 1M hosts as 2 ranks of 500k; default blocks and 8192-row
+    blocks (drain steps); the state at the round boundary after round 24
+    against the oracle's fixture for that round."""
+    res = _run("c4", 2, xcap, stop_round=24)
+    st = [r[2] for r in res]
+    r = st[0]["rounds"]
+    assert r >= 24 and all(x["rounds"] == r and x["phase"] == 0 for x in st)
+    assert all(x["overflow"] == 0 for x in st), [hex(x["overflow"]) for x in st]
+    rows = {row[0]: row for row in FIX["c4_1m"]["rounds"]}
+    assert sum(x["pops"] for x in st) == rows[r][1]
+    assert (sum(x[3] for x in res) & ((1 << 64) - 1)) == rows[r][2]
+    for x in st:
+        assert (x["window_start"], x["window_end"]) == (rows[r][3], rows[r][4])
+    if xcap:
+        assert st[0]["exchange_steps"] > r  # drain steps happened
+
+
+def test_c5_gossip_two_processes():
+    res = _run("c5", 2, 8192)
+    st = [r[2] for r in res]
+    fx = FIX["c5"]["stats"]
+    assert all(x["overflow"] == 0 for x in st)
+    for k in ("pops", "boots", "sends", "drop_reliability", "drop_endtime", "bumped", "same_round"):
+        assert sum(x[k] for x in st) == fx[k], k
+    for x in st:
+        assert x["rounds"] == fx["rounds"] and x["done"]
+    assert (sum(x[3] for x in res) & ((1 << 64) - 1)) == FIX["c5"]["fingerprint"]
+
+
+def test_bench_two_ranks_self_launched():
+    """`python bench.py --gpus 2` with no launcher of its own (bench.py starts
+    torch.distributed.run), ranks on GPU 0 over gloo: one JSON line with the
+    two ranks' events and parity.match true."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--warmup", "10", "--same-device", "--dist-backend", "gloo"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["parity"]["match"] is True, res["parity"]
+    assert res["metric"].endswith("; bit-exact")
