@@ -14,7 +14,9 @@ Also reported:
   roofline     dominant kernel (k_proc): algorithmic bytes (64 B per
                committed event + 24 B per active host-round)
                per launch / its average launch time (HIP events on the engine
-               stream), against 8 TB/s HBM.
+               stream), against 8 TB/s HBM; roofline.per_kernel gives the same
+               for every kernel of the round (k_scatter: 32 B per record it
+               moves).
   cpu_baseline the CPU reference policy (oracle/host_steal.c, the host_steal
                restatement) on the same workload, timed on this machine's host
                cores over a bounded sample of rounds (rank 0, N=1).
@@ -39,18 +41,36 @@ PMC_JSON = os.path.join(ROOT, "profiles", "r02", "bench_k2", "pmc.json")
 DOMINANT = "k_proc"
 
 
-def pmc_traffic(n_hosts):
-    """(corrected PMC bytes per launch of the dominant kernel, source) from the
-    committed profile of this workload, or (None, None)."""
+def pmc_traffic(n_hosts, kernel=DOMINANT):
+    """(corrected PMC bytes per launch of `kernel`, the bytes with FETCH_SIZE as
+    counted, source) from the committed profile of this workload, or Nones."""
     if n_hosts != 1_000_000 or not os.path.exists(PMC_JSON):
         return None, None, None
     ks = json.load(open(PMC_JSON))["kernels"]
-    k = next((v for n, v in ks.items() if n == DOMINANT or n.startswith(DOMINANT + "<")), None)
+    k = next((v for n, v in ks.items() if n == kernel or n.startswith(kernel + "<")), None)
     if not k:
         return None, None, None
     return k["traffic_bytes"], k.get("traffic_bytes_lower"), os.path.relpath(PMC_JSON, ROOT)
+
+
 ALG_BYTES_PER_EVENT = 64
 ALG_BYTES_PER_ACTIVE_HOST = 24
+# k_scatter (DESIGN.md §3): every record it moves is read once and written once,
+# 16 B each way: staged events into the calendar (insert role, due ones routed
+# straight to their partition) and the new window's calendar events into the
+# host partitions (gather role); the rmin and refill roles' few KB are not counted
+ALG_BYTES_PER_MOVE = 32
+
+
+def kernel_roofline(name, alg_bytes, avg_s, n_hosts):
+    """One kernel's line of roofline.per_kernel: algorithmic bytes per launch
+    over its average launch time against HBM peak, beside the committed PMC
+    traffic per launch."""
+    traffic, lower, src = pmc_traffic(n_hosts, name)
+    ach = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"avg_us": avg_s * 1e6, "alg_bytes_per_launch": alg_bytes, "achieved": ach,
+            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": lower,
+            "traffic_gbs": traffic / avg_s / 1e9 if traffic and avg_s else None, "traffic_source": src}
 
 
 def parse():
@@ -169,6 +189,7 @@ def run_single(args):
     # (hipExtLaunchKernelGGL) on the engine stream — kept out of the headline
     # region all the same
     a1, _ = eng.active_hosts()
+    mv1 = eng.event_moves()
     kr = max(1, min(args.steps, args.kernel_rounds))
     eng.set_timing(True)
     eng.run(kr, batch=args.batch)
@@ -177,6 +198,7 @@ def run_single(args):
     proc_ms, proc_n = kt["process"]
     s2 = eng.stats()
     a2, _ = eng.active_hosts()
+    mv2 = eng.event_moves()
     kpops = s2["pops"] - s1["pops"]
     alg_bytes = ALG_BYTES_PER_EVENT * kpops + ALG_BYTES_PER_ACTIVE_HOST * (a2 - a1)
     per_launch_bytes = alg_bytes / max(proc_n, 1)
@@ -184,6 +206,13 @@ def run_single(args):
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic, traffic_lower, traffic_src = pmc_traffic(args.hosts)
     kus = {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]}
+    ins_ms, ins_n = kt["insert"]
+    moves = (mv2["emitted"] - mv1["emitted"]) + (mv2["gathered"] - mv1["gathered"])
+    per_kernel = {
+        DOMINANT: kernel_roofline(DOMINANT, per_launch_bytes, avg_launch_s, args.hosts),
+        "k_scatter": kernel_roofline("k_scatter", ALG_BYTES_PER_MOVE * moves / max(ins_n, 1),
+                                     ins_ms / 1e3 / max(ins_n, 1), args.hosts),
+    }
     res = {
         "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
         "value": pops / dt,
@@ -213,6 +242,7 @@ def run_single(args):
                      "alg_bytes_per_launch": per_launch_bytes,
                      "timing_rounds": kr,
                      "kernel_us_per_round": kus,
+                     "per_kernel": per_kernel,
                      "gaps_us_per_round": dt * 1e6 / args.steps - sum(kus.values()),
                      "timing_method": "HIP events as each launch's dispatch-packet timestamps "
                                       "(hipExtLaunchKernelGGL), rounds after the timed region; "

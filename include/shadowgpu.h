@@ -12,12 +12,14 @@
  *      tables (glibc rand_r streams, the seed chain, host attachment, direct-path
  *      delay/reliability resolution, PHOLD destination weights, window logic).
  *   2. The device engine: an HBM-resident calendar of time buckets; one
- *      conservative round = gather (the window's due events, counting-sorted by
- *      host partition) → process (per host, pop every event before the barrier
- *      in event_compare order, run the PHOLD body, resolve delivery times and
- *      drops, barrier bump) → insert (new events into their time buckets) →
- *      plan (MIN next-event time + min-latency runahead → next [start, end),
- *      the next window's due chunks).
+ *      conservative round is two kernels.  k_proc: every host pops its events
+ *      before the barrier in event_compare order, the PHOLD body runs, delivery
+ *      times and drops are resolved, inter-host events get the barrier bump, and
+ *      the new events are reserved in their time buckets.  k_scatter: the new
+ *      events are written into the buckets, the next window is planned (MIN
+ *      next-event time + min-latency runahead → next [start, end)) and its due
+ *      events are gathered into the host partitions.  Several shards add one
+ *      all-to-all per step (k_count reserves the received events).
  */
 #ifndef SHADOWGPU_H
 #define SHADOWGPU_H
@@ -302,7 +304,7 @@ int sg_engine_boot(sg_engine* e);
 /* Single shard: runs up to max_rounds windows without host round-trips, in
  * batches of `batch` rounds per host synchronisation; stops when done. */
 int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch);
-/* Enqueue one round (gather + process + insert + plan) without synchronising. */
+/* Enqueue one round (k_proc + k_scatter) without synchronising. */
 int sg_engine_enqueue_round(sg_engine* e);
 /* n rounds without reading the round state back (graph-batched when
  * sg_engine_set_graph is on); at most two batches stay queued on the stream. */
@@ -315,6 +317,11 @@ int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops,
 int sg_engine_host_range(sg_engine* e, uint32_t* first_host, uint32_t* n_local);
 /* Cumulative hosts-with-pops per round (active host-rounds) and staged events. */
 int sg_engine_active_hosts(sg_engine* e, uint64_t* active_host_rounds, uint64_t* emitted);
+/* Cumulative record moves of the insert kernels (the per-kernel roofline's
+ * algorithmic bytes): events k_proc staged, events k_scatter's gather moved from
+ * the calendar into host partitions, received events k_scatter wrote (several
+ * shards). */
+int sg_engine_event_moves(sg_engine* e, uint64_t* emitted, uint64_t* gathered, uint64_t* received);
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
 /* Executed windows {start, end} per round (recorded when trace_capacity > 0). */
 int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);
@@ -335,7 +342,8 @@ int sg_engine_geometry(sg_engine* e, sg_engine_geom* out);
 /* Profiling hook: with SG_STAMPS=1 in the environment at create, k_proc records
  * per workgroup {start, sorted, phase A, phase B, end} s_memrealtime ticks
  * (100 MHz), {due events, active hosts, sends} and finer phase stamps of the
- * last round in a row of 32 u64 per partition, plus one row for k_plan;
+ * last round in a row of 32 u64 per partition, then one spare row and one row
+ * per k_scatter workgroup (role, start, setup, events, end);
  * *n_out = 0 when the hook is off. */
 int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n_out);
 
@@ -390,9 +398,10 @@ int sg_engine_set_graph(sg_engine* e, uint32_t batch);
 /* Kernel timing since sg_engine_set_timing(e, 1) (HIP events on the engine
  * stream): total ms and launches per kernel class, arrays of SG_KCLASSES. */
 enum sg_kernel_class {
-    SG_K_PROCESS = 0,  /* k_proc: per-host pops + PHOLD body + send resolution */
-    SG_K_INSERT = 1,   /* k_ins: new / received events into time buckets */
-    SG_K_PLAN = 2,     /* k_plan (+ k_fill when sharded) */
+    SG_K_PROCESS = 0,  /* k_proc: pops + PHOLD body + send resolution + bucket reservations */
+    SG_K_INSERT = 1,   /* k_scatter (+ k_count when sharded): events into their buckets,
+                          the next window planned and gathered */
+    SG_K_PLAN = 2,     /* unused: planning is a k_scatter role now (class kept for ABI stability) */
     SG_K_GATHER = 3,   /* unused: the gather is a k_scatter role now (class kept for ABI stability) */
     SG_K_EXCHANGE = 4, /* the step's RCCL all-to-all (sg_engine_run_steps): this shard's
                           wait for the slowest shard plus the transfer — the barrier
@@ -424,7 +433,7 @@ int sg_engine_path_counts(sg_engine* e, uint64_t* out, uint64_t capacity, uint64
  * start to its last store, idle = from there to the end of the round's last
  * partition, summed over the rounds since enable (a multi-shard step's wait
  * in the collective is not included).  enable != 0 zeroes them; they cost
- * one extra barrier per partition and a P-entry pass in k_plan, so they are
+ * one extra barrier per partition and a P-entry pass in k_scatter, so they are
  * off by default.  barrier_times copies P entries (n_out = P, or 0 while off). */
 int sg_engine_barrier_timers(sg_engine* e, int enable);
 int sg_engine_barrier_times(sg_engine* e, uint64_t* busy_ns, uint64_t* idle_ns, uint64_t capacity,
@@ -443,11 +452,11 @@ int sg_engine_barrier_times(sg_engine* e, uint64_t* busy_ns, uint64_t* idle_ns, 
  * Per round: push stages inter-host (and future self) events per thread with
  * no lock; self events before the barrier go to a per-host CPU heap (they must
  * be popped in this round, host_single.c:237-267).  The last worker to call
- * next_time flushes the staged events to HBM (k_pol_insert) and reduces the
- * MIN next time on the device.  The first pop of the next round extracts, on
+ * next_time flushes the staged events to HBM (k_pins) and reduces the MIN next
+ * time on the device (k_pmin).  The first pop of the next round extracts, on
  * the device, every queued event before the new barrier sorted per host in
- * event_compare order (k_pol_extract); pops merge that run with the host's CPU
- * heap. */
+ * event_compare order (k_pcount / k_pscan / k_pwrite); pops merge that run with
+ * the host's CPU heap. */
 typedef struct sg_policy sg_policy;
 
 typedef struct sg_policy_params {

@@ -6,39 +6,32 @@
 //   events      live in time buckets of width W (a ring of R buckets), each a
 //               list of 1024-event chunks.  A round reads only the buckets its
 //               window [S, E) covers, never a host's whole queue.
-//   k_gather    streams the due buckets' chunks and counting-sorts the events
-//               with t < E by host partition (HP consecutive hosts; LDS
-//               histogram, one reservation per workgroup and partition).  The
-//               window's last bucket may straddle E: its due events are
-//               tombstoned in place, the rest stay (their MIN is the carry min).
-//   k_proc      one workgroup per partition: LDS counting sort of the
-//               partition's due events by host, compaction of the active hosts,
-//               then one lane per active host pops its events in event_compare
-//               order (core/work/event.c:110-153), same-round self events
-//               included (host_single.c:237-267), and runs the PHOLD body:
-//               destination draw (test_phold.c:160-178), reliability draw +
-//               ceil delay (worker.c:243-304), srcHostEventID (event.c:38),
-//               endTime drop (scheduler.c:343), barrier bump
-//               (host_single.c:180-184).  New events are staged per partition.
-//   k_count     staged (and, multi-shard, received) events → bucket counts:
-//               LDS histogram by bucket, one atomic reservation per
-//               (workgroup, bucket); the reserved bases are kept for k_scatter.
-//   k_plan      one workgroup: frees the consumed chunks, gives every bucket
-//               the chunks its new count needs (free ring), MIN next time
-//               (host_single.c:273-305, scheduler.c:393-398: the per-workgroup
-//               minima plus the first non-empty bucket beyond the window),
-//               discovery minimum (topology.c:1374-1385), next window
-//               (master.c:450-480), and lists the next window's due chunks.
-//   k_scatter   the counted events into their reserved chunk slots.
-// Chunk tables are written only by k_boot / k_plan and read by later kernels,
-// so no workgroup ever waits on another inside a launch.
+//   k_proc      one workgroup per host partition (HP consecutive slots): LDS
+//               counting sort of the partition's due events by host, then the
+//               flat pass, one lane per due event: its place in the host's
+//               event_compare order (core/work/event.c:110-153), the host's
+//               earlier draws replayed, trace digest term, PHOLD destination
+//               draw (test_phold.c:160-178), reliability draw + ceil delay
+//               (worker.c:243-304), srcHostEventID (event.c:38), endTime drop
+//               (scheduler.c:343), barrier bump (host_single.c:180-184).  Hosts
+//               the flat pass cannot take (boot events, same-round self events
+//               host_single.c:237-267, lossy multi-event hosts, gossip) run
+//               phase A, one lane per host, and phases B/C.  New events are
+//               staged per partition, counted by bucket in LDS and reserved in
+//               the calendar (one atomic per partition and bucket; chunk ids
+//               from the partition's stash).
+//   k_scatter   the staged events into their reserved slots (due ones routed
+//               straight to their partition), the next window planned from the
+//               MIN terms (host_single.c:273-305, master.c:450-480) by every
+//               workgroup, the new window's due chunks gathered into the host
+//               partitions, the minimum beyond the window, the stashes refilled.
 //   multi-shard k_proc also writes the events for other shards into per-peer
-//               outbox regions (one reservation per peer and partition);
-//               The first xcap rows of each peer's outbox are the exchange
-//               block itself; the last k_proc workgroup to finish writes the
-//               block headers (the shard's MIN terms).  On a drain step k_proc
-//               only copies outbox leftovers into the blocks.  k_plan reads the
-//               G headers back instead of the local minima.
+//               outbox regions; the first xcap rows of each peer's outbox are the
+//               exchange block itself, and the last k_proc workgroup to finish
+//               writes the block headers (the shard's MIN terms).  After the
+//               all-to-all, k_count reserves the received events and k_scatter
+//               plans from the G headers.  On a drain step k_proc only copies
+//               outbox leftovers into the blocks.
 //
 // HBM layout: 16-B records everywhere.
 //   bucket record     {dst_local << 40 | (t - b*W),  src << 40 | srcHostEventID}
@@ -108,7 +101,11 @@ enum Ovf : uint64_t {
 
 enum Ctr {
     C_POPS = 0, C_BOOTS, C_SENDS, C_NULL, C_DROPREL, C_DROPEND, C_BUMPED, C_SAME,
-    C_ACTIVE, C_EMIT, NCTR
+    C_ACTIVE, C_EMIT,
+    NPCTR,                  // counters k_proc accumulates; k_scatter's follow
+    C_GATHER = NPCTR,       // events the gather role moved from the calendar into partitions
+    C_RECV,                 // received events the insert role wrote (several shards)
+    NCTR
 };
 
 struct Rec {
@@ -194,12 +191,22 @@ struct PairRec {
 // 8 or 4 bytes, so the V*V table stays in an XCD's L2.
 enum PairFmt : uint32_t { PAIR_WIDE = 0, PAIR_NARROW = 1, PAIR_DELAY = 2 };
 
+// A host's 32-B record: its state and, so that k_proc reads one record per
+// host, its identity (registration index h, attachment vertex, both fixed).
 struct HostState {
     uint32_t rng;     // host Random (host.c:176)
-    uint32_t pad;
-    uint64_t pops;
+    uint32_t h;       // registration index (its id in event keys and traces)
+    uint64_t pv;      // pops (low 48 bits) | vertex << 48
     uint64_t digest;
     uint64_t evc;     // eventIDCounter (host.c:397-400); k_proc writes it last (phase C)
+};
+constexpr uint64_t M48 = (1ULL << 48) - 1;
+__device__ __forceinline__ uint64_t hs_w0(uint32_t rng, uint32_t h) { return rng | ((uint64_t)h << 32); }
+__device__ __forceinline__ uint64_t hs_w1(uint64_t pops, uint32_t vh) { return pops | ((uint64_t)vh << 48); }
+// A host's state while k_proc executes its events.
+struct HostWork {
+    uint32_t rng;
+    uint64_t pops, digest, evc;
 };
 
 // Unsigned 32-bit division by a launch constant without a divide:
@@ -277,9 +284,10 @@ struct Dev {
     bool snd_lds;                // k_proc's send records in LDS while they fit
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
+    uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
-    uint32_t check;           // SG_CHECK=1: k_plan re-derives the sent headers' MIN terms (debug)
+    uint32_t check;           // SG_CHECK=1: k_scatter's planner re-derives the sent headers' MIN terms (debug)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
     const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
@@ -652,7 +660,7 @@ __global__ void k_boot(Dev d) {
         d.pool[i] = Rec{(uint64_t)i << 40, (uint64_t)h << SRC_SHIFT};
         HostState s = d.hs[i];
         s.evc = 1;
-        s.pops = 0;
+        s.pv &= ~M48;  // pops 0, the vertex stays
         s.digest = 0;
         d.hs[i] = s;
     }
@@ -729,7 +737,7 @@ constexpr int GUNR = 4;          // events in flight per thread (two-pass path)
 template <bool SCATTER, int GT>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
                                             uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
-                                            uint64_t& cmin, uint64_t& ntomb) {
+                                            uint64_t& cmin, uint64_t& ntomb, uint64_t& ng) {
     const uint32_t tot = nb * CH;
     for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += GT * GUNR) {
         Rec r[GUNR];
@@ -762,6 +770,7 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
                 continue;
             }
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            ++ng;
             if (slot < d.CAPP)
                 st_stream(&d.part[(size_t)p * d.CAPP + slot], Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k});
             if (de.nflags & RETAINED) {
@@ -936,7 +945,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
         s_cnt[p] = 0;
         s_cur[p] = 0;
     }
-    uint64_t cmin = UINT64_MAX, ntomb = 0;
+    uint64_t cmin = UINT64_MAX, ntomb = 0, ng = 0;  // ng: events moved (C_GATHER)
     auto reserve = [&]() {  // one reservation per partition this workgroup feeds
         for (uint32_t p = threadIdx.x; p < P; p += GT) {
             const uint32_t c = s_cnt[p];
@@ -996,6 +1005,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             if (pp[q] == UINT32_MAX) continue;
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            ++ng;
             if (slot < d.CAPP) st_stream(&d.part[(size_t)p * d.CAPP + slot], r[q]);
             const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
@@ -1011,7 +1021,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             __syncthreads();
             if (threadIdx.x < nb) s_de[threadIdx.x] = due_entry(d, dl, s_start, s_lo, (uint32_t)(cb + threadIdx.x));
             __syncthreads();
-            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
         __syncthreads();
         reserve();
@@ -1024,12 +1034,14 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
                 free_chunk(de, cb + threadIdx.x);
             }
             __syncthreads();
-            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb);
+            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
     }
     const uint64_t m = block_min(cmin, s16);
     const uint64_t nt = block_sum(ntomb, s16);
+    const uint64_t gn = block_sum(ng, s16);
     if (threadIdx.x == 0) {
+        if (gn) atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GATHER * d.P + w % d.P], (unsigned long long)gn);
         if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry2[sv.cur ^ 1], (unsigned long long)m);
         if (sv.ret != UINT64_MAX) {
             const uint32_t rb = (uint32_t)(sv.ret % d.R);
@@ -1041,7 +1053,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
 
 // ----------------------------------------------------------------- proc ----
 struct Acc {
-    uint32_t ctr[NCTR];
+    uint32_t ctr[NPCTR];
     uint64_t jmin;   // min truncated latency of attempted sends
     uint64_t emin;   // min time of staged (emitted) events
     bool overflow;
@@ -1050,8 +1062,16 @@ struct Acc {
 struct HostCtx {
     uint32_t h, vh;   // registration index, vertex
     uint32_t sg;      // global slot (destinations are slots)
-    HostState s;
+    HostWork s;
 };
+__device__ __forceinline__ void host_load(HostCtx& c, ulonglong2 w01, ulonglong2 w23) {
+    c.s.rng = (uint32_t)w01.x;
+    c.h = (uint32_t)(w01.x >> 32);
+    c.s.pops = w01.y & M48;
+    c.vh = (uint32_t)(w01.y >> 48);
+    c.s.digest = w23.x;
+    c.s.evc = w23.y;
+}
 
 struct ProcShared {
     uint32_t nloc, nrem;
@@ -1315,6 +1335,42 @@ __device__ __forceinline__ void sort_segment(Rec* seg, uint32_t cnt) {
     }
 }
 
+// Flat pass (k_proc): one lane per due event instead of one per host.  A
+// lane finds its event's place in the host's pop order by comparing it with
+// the host's other due events (seg, cnt records in LDS, any order): rank,
+// the host's earliest time and whether a boot event is among them.
+struct SegScan {
+    uint32_t rank;
+    uint64_t tmin;
+    bool boot;  // srcHostEventID 0: only a boot event carries it (event.c:38, worker_bootHosts)
+};
+__device__ __forceinline__ SegScan seg_scan(const Rec* seg, uint32_t cnt, uint64_t et, uint64_t ek) {
+    SegScan s{0, et, (ek & SEQ_MASK) == 0};
+    if (cnt > 1) {
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const Rec r = seg[k];
+            const uint64_t rt = r.a & M52;
+            s.rank += key_less(rt, r.k, et, ek) ? 1u : 0u;
+            s.tmin = rt < s.tmin ? rt : s.tmin;
+            s.boot |= (r.k & SEQ_MASK) == 0;
+        }
+    }
+    return s;
+}
+// A host the flat pass executes: every event is a PHOLD message event with one
+// send (no boot event: test_phold.c:310-312), so an event's draws follow the
+// draws of the events before it; every send kept unless the host has one event
+// (lossy records: a send's srcHostEventID counts the kept sends before it,
+// event.c:38 after worker.c:268-273); no self event can land inside the window
+// (host_single.c:237-267 would pop it this round).  Every lane of the host
+// computes the same answer; the others run phase A.
+constexpr uint32_t FLAT_CMAX = 16;
+__device__ __forceinline__ bool flat_ok(const Dev& d, uint32_t cnt, const SegScan& s, bool self_possible, uint64_t S,
+                                        uint64_t E, uint32_t vh) {
+    if (s.boot || cnt > FLAT_CMAX || (cnt > 1 && d.pair_fmt != PAIR_DELAY)) return false;
+    return !self_possible || S + s.tmin + d.vself[vh] >= E;
+}
+
 // Diagnostics (SG_STAMPS): a timestamp once this wave's outstanding memory
 // operations have landed.
 constexpr uint32_t SG_STAMP_W = 32;  // stamp slots per workgroup row
@@ -1334,7 +1390,7 @@ __device__ __forceinline__ uint64_t wait_stamp() {
 // writes the events into the reserved slots and refills the stashes.  Every
 // thread of the block (T threads) calls it.
 template <int T>
-__device__ void reserve_buckets(const Dev& d, uint32_t row, uint32_t x, const uint32_t* s_bc, const uint32_t* s_bm,
+__device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint32_t x, const uint32_t* s_bc, const uint32_t* s_bm,
                                 uint64_t bS, uint32_t bSr, uint32_t sid, uint32_t sn, uint64_t avail,
                                 uint32_t* s_ids, uint64_t* s_h, uint64_t* s16) {
     constexpr uint32_t PER = RMAX / T;
@@ -1591,7 +1647,7 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
 // reach them (new events are at or after the current window's start), and
 // k_scatter's gather and rmin of the previous step are done with them.
 // Threads [0, XS * nb) of one workgroup at launch.
-__device__ void reset_consumed(const Dev& d) {
+__device__ __forceinline__ void reset_consumed(const Dev& d) {
     const RoundState* rs = d.rs;
     const uint64_t pbS = rs->pbS, pbL = rs->pbL, pret = rs->pret, bS = rs->bS;
     if (pbS == UINT64_MAX) return;
@@ -1636,13 +1692,13 @@ constexpr uint32_t EPT = EVLMAX / K2_T;    // of them per lane
 // min jump, overflow, round} then up to xcap outbox rows.  The MIN terms are
 // this shard's reduce_local of the step's process partials (unchanged on drain
 // steps, so a drain step repeats them).  One workgroup (every thread calls it).
-__device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j);
+__device__ __forceinline__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j);
 __device__ __forceinline__ uint64_t atomic_read(uint64_t* a) {
     return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // outn / overflow are read atomically: the last k_proc workgroup reads what
 // the others' device-scope atomics performed (their L2 lines may be stale here).
-__device__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
+__device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
     RoundState* rs = d.rs;
     if (threadIdx.x < d.G) {
         const uint32_t p = threadIdx.x;
@@ -1667,7 +1723,7 @@ __device__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
 }
 // Drain step: the next xcap leftovers of every peer's outbox into its block,
 // spread over nblk workgroups; workgroup 0 also writes the headers.
-__device__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t nblk, uint64_t* s16) {
+__device__ __forceinline__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t nblk, uint64_t* s16) {
     for (uint32_t p = 0; p < d.G; ++p) {
         const uint64_t left = d.outn[p] - d.sent[p];
         const uint64_t n = left < d.xcap ? left : d.xcap;
@@ -1713,7 +1769,10 @@ __device__ __forceinline__ void near_resolve(const Dev& d, int32_t x, uint2 a, u
 // EXACT: d.dst_near (a destination is two adjacent 8-byte records per send);
 // the other instantiation resolves destinations through the weight probes
 // (and bisection).  ROWS: d.lds_rows (path records from the partition's LDS rows).
-template <bool EXACT, bool ROWS>
+// FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
+// the flat pass; its event image holds only those (EPTF registers per lane), a
+// bigger one sorts through part2 and runs phase A.
+template <bool EXACT, bool ROWS, bool FLAT>
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
     if (rs->done) return;
@@ -1737,7 +1796,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ int32_t s_last;         // last weight threshold: x above it selects no host
     __shared__ ProcShared sh;
     __shared__ uint64_t s16[16];
-    __shared__ uint64_t s_red[K2_T / 64][NCTR + 2];
+    __shared__ uint64_t s_red[K2_T / 64][NPCTR + 2];
     __shared__ uint32_t s_obase[MAXG], s_oslot[MAXG];
     const uint64_t S = rs->S, E = rs->E;
     const bool want_jump = rs->jmin > d.gjmin;  // discovery can still lower the window's jump
@@ -1750,7 +1809,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // the first SPEC records per lane are loaded before the count arrives
     // (CAPP >= SPEC * K2_T; records past the count are ignored)
     constexpr uint32_t SPEC = 2;
-    Rec rr[EPT];
+    constexpr uint32_t EPTF = FLAT ? SPEC : EPT;
+    Rec rr[EPTF];
 #pragma unroll
     for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
     uint32_t n = d.pcnt[p];
@@ -1775,10 +1835,18 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (tid < MAXG) sh.peer[tid] = 0;
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
-    const bool in_lds = n <= d.EVL;
+    const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T);
+    // Flat pass (PHOLD, events in LDS, at most SPEC per lane; see below): the
+    // states of the hosts of the lane's two due events are loaded as soon as
+    // the records arrive.  Every lane's state reads have returned before the
+    // barrier after the scatter (vmcnt(0)) and every state write comes after
+    // it, so a host's last event cannot overwrite the state its other events
+    // read.
+    const bool flat = FLAT && in_lds;
+    ulonglong2 pre_a0, pre_b0, pre_a1 = make_ulonglong2(0, 0), pre_b1 = make_ulonglong2(0, 0);
     if (in_lds) {
 #pragma unroll
-        for (uint32_t q = SPEC; q < EPT; ++q) {
+        for (uint32_t q = SPEC; q < EPTF; ++q) {
             const uint32_t i = tid + q * K2_T;
             rr[q] = i < n ? ld_stream(&part[i]) : Rec{0, 0};
         }
@@ -1812,16 +1880,28 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __syncthreads();
     if (in_lds) {
 #pragma unroll
-        for (uint32_t q = 0; q < EPT; ++q) {
+        for (uint32_t q = 0; q < EPTF; ++q) {
             if (tid + q * K2_T >= n) continue;
             const uint32_t hl = (uint32_t)(rr[q].a >> 52);
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
         }
+        if (flat) {  // uniform
+            const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
+            uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
+            l0 = l0 < d.L ? l0 : d.L - 1;  // a record past the count: any valid slot
+            l1 = l1 < d.L ? l1 : d.L - 1;
+            pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
+            pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
+            if (tid + K2_T < n) {  // most lanes have one event
+                pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
+                pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
+            }
+        }
         // the records are in registers now: re-defining them through asm keeps
         // the scatter below from waiting on the state prefetch (vmcnt(0))
 #pragma unroll
-        for (uint32_t q = 0; q < EPT; ++q) {
+        for (uint32_t q = 0; q < EPTF; ++q) {
             rr[q].a = opaque(rr[q].a);
             rr[q].k = opaque(rr[q].k);
         }
@@ -1866,22 +1946,18 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // the lane's first host only (the second is rare), loaded unconditionally
     // from a clamped slot: a conditional load is waited for where it is issued
     constexpr uint32_t NPRE = 1;
-    ulonglong2 pre_a0, pre_b0, pre_a1 = make_ulonglong2(0, 0), pre_b1 = pre_a1;
-    uint2 pre_s0, pre_s1 = make_uint2(0, 0);
-    {
+    if (!flat) {  // uniform
         const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
-        const uint2* siw = reinterpret_cast<const uint2*>(d.sinfo);
         uint32_t l0 = sbase + s_act[tid < nact ? tid : 0u];
         l0 = l0 < d.L ? l0 : d.L - 1;
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-        pre_s0 = siw[l0];
     }
-    if (tid == 0) d.pcnt[p] = 0;  // consumed; k_gather of the next round refills it
+    if (tid == 0) d.pcnt[p] = 0;  // consumed; the next k_scatter's gather refills it
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
 #pragma unroll
-        for (uint32_t q = 0; q < EPT; ++q) {
+        for (uint32_t q = 0; q < EPTF; ++q) {
             if (tid + q * K2_T >= n) continue;
             const uint32_t hl = (uint32_t)(rr[q].a >> 52);
             if (hl >= HP) continue;
@@ -1904,12 +1980,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (i < nwords) reinterpret_cast<uint32_t*>(dyn + d.row_off)[i] = rw[q];
         }
     }
+    if (flat) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flat pass's state reads have returned
     __syncthreads();  // the grouped events (and rows) are read back by other lanes
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
     Acc a;
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) a.ctr[i] = 0;
+    for (int i = 0; i < NPCTR; ++i) a.ctr[i] = 0;
     a.jmin = UINT64_MAX;
     a.emin = SIMTIME_MAX;
     a.overflow = false;
@@ -1960,19 +2037,20 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         atomicAdd(&s_bc[rb], 1u);
         atomicMin(&s_bm[rb], off);
     };
+    uint32_t nacta = nact;  // the hosts phase A takes: s_act[0, nacta)
     auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
         Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
 #pragma unroll 1
         for (uint32_t q = 0; q < HPT; ++q) {
             const uint32_t j = tid + q * K2_T;
-            if (__builtin_amdgcn_readfirstlane(tid & ~63u) + q * K2_T >= nact) break;  // wave-uniform
+            if (__builtin_amdgcn_readfirstlane(tid & ~63u) + q * K2_T >= nacta) break;  // wave-uniform
             bool go = false;  // this lane records sends (phase B/C path)
             uint32_t ns = 0, cnt = 0, lh = 0;
             Rec* seg = nullptr;
             HostCtx c;
             const bool st0 = stamp && tid == 0 && q == 0;
             if (stamp && tid == 0 && q == 1) stamp[23] = __builtin_amdgcn_s_memrealtime();
-            if (j < nact) {
+            if (j < nacta) {
                 s_sb[j] = UINT32_MAX;
                 const uint32_t hl = s_act[j];
                 cnt = s_n[hl];
@@ -1982,30 +2060,23 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 if (lh >= d.L) {
                     a.overflow = true;
                 } else {
-                    if (q < NPRE) {  // selects of values, not of addresses
-                        c.s.rng = (uint32_t)opaque(q == 0 ? pre_a0.x : pre_a1.x);
-                        c.s.pad = 0;
-                        c.s.pops = opaque(q == 0 ? pre_a0.y : pre_a1.y);
-                        c.s.digest = opaque(q == 0 ? pre_b0.x : pre_b1.x);
-                        c.s.evc = opaque(q == 0 ? pre_b0.y : pre_b1.y);
-                        c.h = opaque(q == 0 ? pre_s0.x : pre_s1.x);
-                        c.vh = opaque(q == 0 ? pre_s0.y : pre_s1.y);
+                    if (q < NPRE && !flat) {  // selects of values, not of addresses
+                        host_load(c, make_ulonglong2(opaque(pre_a0.x), opaque(pre_a0.y)),
+                                  make_ulonglong2(opaque(pre_b0.x), opaque(pre_b0.y)));
                     } else {
-                        c.s = d.hs[lh];
-                        const SlotInfo si = d.sinfo[lh];
-                        c.h = si.h;
-                        c.vh = si.v;
+                        const ulonglong2* hw = reinterpret_cast<const ulonglong2*>(d.hs + lh);
+                        host_load(c, hw[0], hw[1]);
                     }
                     s_vh[j] = c.vh;
-                    ++a.ctr[C_ACTIVE];
                     // the vertex's self delay only when some vertex's could land
                     // inside this window (uniform; never in steady C4 rounds)
                     const uint64_t self_delay = self_possible ? d.vself[c.vh] : 0;
+                    ++a.ctr[C_ACTIVE];
                     if (st0) stamp[8] = wait_stamp();
                     sort_segment(seg, cnt);  // pop order
                     if (st0) stamp[9] = wait_stamp();
                     if (d.workload != SG_WORKLOAD_PHOLD ||
-                        (self_possible && S + (seg[0].a & M52) + self_delay < E)) {
+                               (self_possible && S + (seg[0].a & M52) + self_delay < E)) {
                         // sequential body: a self event may land inside this window
                         uint32_t nx = 0;
                         auto append = [&](uint64_t trel, uint64_t key) -> bool {
@@ -2035,7 +2106,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             }
                             execute_event(d, S, E, p, c, a, S + b.t, b.k, sh, append, count_local);
                         }
-                        d.hs[lh] = c.s;
+                        reinterpret_cast<ulonglong2*>(d.hs + lh)[0] =
+                            make_ulonglong2(hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
+                        reinterpret_cast<ulonglong2*>(d.hs + lh)[1] = make_ulonglong2(c.s.digest, c.s.evc);
                     } else {
                         // this host's sends, at most: a draw that selects no host
                         // (test_phold.c:176-177) sends nothing, so the path is
@@ -2087,7 +2160,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             commit_two(d, S, E, p, c, a, sh, nsd, S + t0, c0, dst0, vd0, pr0, S + t1, c1, dst1, vd1, pr1,
                                        count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
-                            st_stream2(&hp[0], (uint64_t)c.s.rng, c.s.pops);
+                            st_stream2(&hp[0], hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
                             if (st0) stamp[19] = wait_stamp();
                             st_stream2(&hp[1], c.s.digest, c.s.evc);
                             ns = 0;
@@ -2124,7 +2197,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             // {rng, pops, digest} now; evc now too when every send is kept, else
             // after phase C
             HostState* hp = d.hs + lh;
-            reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2((uint64_t)c.s.rng, c.s.pops);
+            reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2(hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
             if (d.pair_fmt == PAIR_DELAY) {  // every send kept: the final counter is known now
                 reinterpret_cast<ulonglong2*>(hp)[1] = make_ulonglong2(c.s.digest, c.s.evc + nreal);
             } else {
@@ -2134,7 +2207,178 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (stamp && tid == 0 && q == 1) stamp[24] = wait_stamp();
         }
     };
-    if (in_lds) phase_a(std::true_type{});
+    // ---- flat pass: one lane per due event (the lane's own records, still in
+    // registers).  A host's events are independent once each knows its rank
+    // in the host's pop order: the rand_r draws of the events before it are
+    // replayed (pure arithmetic, one send per event, test_phold.c:310-312;
+    // a draw selecting no host consumes one draw, not two), its trace digest
+    // term is additive given its position, and its srcHostEventID is the
+    // host's counter plus the kept sends before it.  The host's last event
+    // writes the state; a host with several events adds the digest terms
+    // with atomics.  Hosts flat_ok rejects are listed (their rank-0 event's
+    // lane appends them to s_act, which only phase A reads from here on) and
+    // run phase A.  A lane's two events are resolved together: both
+    // destination loads in flight at once.
+    __shared__ uint32_t s_nser;
+    bool ser = !flat;
+    if (flat) {
+        if (tid == 0) s_nser = 0;
+        __syncthreads();
+        // what stage 3 needs of an event, kept small (two are live at once)
+        enum : uint32_t { F_OK = 1, F_SND = 2, F_LAST = 4, F_MULTI = 8 };
+        struct FlatEv {
+            uint32_t hl, h, vh, rng, g, flags;
+            int32_t x, ch;
+            uint64_t bt;
+            uint64_t pops_end;  // the host's pops after the round (its last event writes it)
+            uint64_t sq;        // this send's srcHostEventID
+            uint64_t term;      // digest term; one-event host: the new digest
+        };
+        // stage 1: place in the host's order, replay, draws (LDS and ALU only)
+        auto flat_draw = [&](const Rec& ev, bool valid, ulonglong2 w01, ulonglong2 w23)
+            __attribute__((always_inline)) {
+            FlatEv f;
+            f.hl = (uint32_t)(ev.a >> 52);
+            f.flags = 0;
+            f.x = 0;
+            f.g = 0;
+            f.vh = 0;
+            if (!valid || f.hl >= HP) return f;  // past the count / flagged by the histogram
+            const uint32_t cnt = s_n[f.hl];
+            const uint64_t et = ev.a & M52;
+            const SegScan sc = seg_scan(s_ev + (s_c[f.hl] - cnt), cnt, et, ev.k);
+            f.h = (uint32_t)(w01.x >> 32);
+            f.vh = (uint32_t)(w01.y >> 48);
+            if (!flat_ok(d, cnt, sc, self_possible, S, E, f.vh)) {
+                if (sc.rank == 0) s_act[atomicAdd(&s_nser, 1u)] = (uint16_t)f.hl;  // phase A takes it
+                return f;
+            }
+            f.flags = F_OK | (sc.rank + 1 == cnt ? F_LAST : 0u) | (cnt > 1 ? F_MULTI : 0u);
+            uint32_t rng = (uint32_t)w01.x;
+            const uint64_t pops0 = w01.y & M48;
+            f.pops_end = pops0 + cnt;
+            uint32_t before = 0;  // sends of the host's earlier events (all kept: flat_ok)
+            for (uint32_t k = 0; k < sc.rank; ++k) {
+                if (dev_rand_r(rng) <= last) {
+                    (void)dev_rand_r(rng);
+                    ++before;
+                }
+            }
+            f.sq = w23.y + before;  // event.c:38: the counter plus the kept sends before
+            f.bt = S + et;
+            const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
+            const uint64_t bseq = ev.k & SEQ_MASK;
+            f.term = digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
+            if (cnt == 1) f.term += w23.x;  // the host's new digest
+            if (d.trace) {
+                const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
+                if (ts < d.trace_cap) {
+                    sg_trace_rec tr;
+                    tr.time = f.bt;
+                    tr.seq = bseq;
+                    tr.host = f.h;
+                    tr.src = bsrc;
+                    tr.pos = pops0 + sc.rank;
+                    d.trace[ts] = tr;
+                } else {
+                    a.overflow = true;
+                }
+            }
+            ++a.ctr[C_POPS];
+            a.ctr[C_ACTIVE] += sc.rank == 0 ? 1u : 0u;
+            f.x = dev_rand_r(rng);
+            const bool snd = f.x <= last;  // test_phold.c:176-177
+            f.flags |= snd ? F_SND : 0u;
+            f.ch = 0;
+            if (snd) f.ch = dev_rand_r(rng);  // worker.c:268-269
+            f.rng = rng;
+            f.g = dst_guess(d, f.x);
+            return f;
+        };
+        // stage 3: the send's tests and staging, the host's state (stores and
+        // LDS atomics only: nothing after it waits for a global load)
+        auto flat_send = [&](const FlatEv& f, uint32_t vd, uint32_t dst, const PairRec& pr)
+            __attribute__((always_inline)) {
+            if (!(f.flags & F_OK)) return;
+            bool kept = false;
+            if (f.flags & F_SND) {
+                ++a.ctr[C_SENDS];
+                kept = f.bt < d.bootstrap_end || f.ch <= pr.keep;  // worker.c:268-273
+                if (!kept) {
+                    ++a.ctr[C_DROPREL];
+                } else {
+                    if (d.pcount) atomicAdd(&d.pcount[(size_t)f.vh * d.V + vd], 1u);  // worker.c:279
+                    uint64_t tn = f.bt + pr.delay;        // worker.c:275-277
+                    const uint64_t sq = f.sq;             // event.c:38
+                    if (sq >> SRC_SHIFT) a.overflow = true;
+                    if (tn >= d.end_time) {               // scheduler.c:343-346
+                        ++a.ctr[C_DROPEND];
+                    } else {
+                        const uint32_t sg = d.lo + sbase + f.hl;
+                        if (dst == sg && tn < E) a.overflow = true;  // excluded by flat_ok
+                        if (dst != sg && tn < E) {                   // host_single.c:180-184
+                            tn = E;
+                            ++a.ctr[C_BUMPED];
+                        }
+                        if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)f.h << SRC_SHIFT) | sq)) count_local(tn);
+                    }
+                }
+            } else {
+                ++a.ctr[C_NULL];
+            }
+            HostState* hp = d.hs + sbase + f.hl;
+            if (f.flags & F_LAST) {  // the host's last event: its state after the round
+                const uint64_t evc = f.sq + (kept ? 1u : 0u);
+                ulonglong2* hw = reinterpret_cast<ulonglong2*>(hp);
+                st_stream2(&hw[0], hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
+                if (!(f.flags & F_MULTI)) st_stream2(&hw[1], f.term, evc);
+                else hp->evc = evc;
+            }
+            if (f.flags & F_MULTI) atomicAdd((unsigned long long*)&hp->digest, (unsigned long long)f.term);
+        };
+        const bool stf = stamp && tid == 0;
+        if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
+        const FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
+        const FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
+        if (stf) stamp[17] = wait_stamp();
+        // stage 2: both events' destination records in flight together
+        // (unconditional loads; an unused one reads record 0's line), resolved
+        // and pinned here: a value resolved after the first store would wait
+        // for that store too (vmcnt counts in order)
+        uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
+        if constexpr (EXACT) {
+            const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
+            const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
+            near_resolve(d, f0.x, a0, b0, vd0, dst0);
+            near_resolve(d, f1.x, a1, b1, vd1, dst1);
+        } else {
+            const Probe pb0 = dst_probe(d, f0.g), pb1 = dst_probe(d, f1.g);
+            dst0 = (f0.flags & F_OK) && (f0.flags & F_SND) ? dst_resolve(d, f0.x, f0.g, pb0, vd0) : 0u;
+            dst1 = (f1.flags & F_OK) && (f1.flags & F_SND) ? dst_resolve(d, f1.x, f1.g, pb1, vd1) : 0u;
+        }
+        vd0 = opaque(vd0);
+        vd1 = opaque(vd1);
+        dst0 = opaque(dst0);
+        dst1 = opaque(dst1);
+        const PairRec pr0 = pair_of(f0.vh, vd0, want_jump), pr1 = pair_of(f1.vh, vd1, want_jump);
+        // path discovery (topology.c:1374-1385) folded here, before the stores
+        // (the discovered-ms loads run only while the minimum can still fall)
+        constexpr uint32_t F_SENDS = F_OK | F_SND;
+        if ((f0.flags & F_SENDS) == F_SENDS) a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;
+        if ((f1.flags & F_SENDS) == F_SENDS) a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
+        a.jmin = opaque(a.jmin);
+        if (stf) stamp[18] = wait_stamp();
+        flat_send(f0, vd0, dst0, pr0);
+        flat_send(f1, vd1, dst1, pr1);
+        if (stf) stamp[19] = wait_stamp();
+        if (stamp && (tid & 255) == 0) stamp[26 + (tid >> 8)] = __builtin_amdgcn_s_memrealtime();  // waves 0, 4, 8, 12
+        __syncthreads();
+        nacta = s_nser;
+        ser = nacta != 0;
+        if (stf) stamp[30] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (!ser) {
+    } else if (in_lds) phase_a(std::true_type{});
     else phase_a(std::false_type{});
     if (stamp && (tid & 63) == 0) stamp[26 + (tid >> 8)] = wait_stamp();  // waves 0, 4, 8, 12 done
     __syncthreads();
@@ -2300,32 +2544,32 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 
     // workgroup partials: cumulative counters, this round's two minima
     const int lane = tid & 63, wid = tid >> 6;
-    uint64_t v[NCTR + 2];
+    uint64_t v[NPCTR + 2];
 #pragma unroll
-    for (int i = 0; i < NCTR; ++i) v[i] = wave_sum_u32(a.ctr[i]);
-    v[NCTR] = wave_min(a.emin);
-    v[NCTR + 1] = wave_min(a.jmin);
+    for (int i = 0; i < NPCTR; ++i) v[i] = wave_sum_u32(a.ctr[i]);
+    v[NPCTR] = wave_min(a.emin);
+    v[NPCTR + 1] = wave_min(a.jmin);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < NCTR + 2; ++i) s_red[wid][i] = v[i];
+        for (int i = 0; i < NPCTR + 2; ++i) s_red[wid][i] = v[i];
     }
     if (a.overflow) flag(d, OV_PROC);
     __syncthreads();
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     // wave 0: the partials and the MIN accumulators (the last workgroup reads
     // them), issued before the reservations
-    if (tid < NCTR + 2) {
+    if (tid < NPCTR + 2) {
         const int i = tid;
         uint64_t r = s_red[0][i];
         for (int w = 1; w < K2_T / 64; ++w) {
             const uint64_t x = s_red[w][i];
-            r = i < NCTR ? r + x : (x < r ? x : r);
+            r = i < NPCTR ? r + x : (x < r ? x : r);
         }
         // the workgroup's own slot: an atomic add needs no load (wave 0 joins
         // the reservations' barrier without waiting for one)
-        if (i < NCTR) atomicAdd((unsigned long long*)&d.pcum[(size_t)i * d.P + p], (unsigned long long)r);
-        else d.p2min[(size_t)(i - NCTR) * d.P + p] = r;
-        if (i >= NCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NCTR], (unsigned long long)r);
+        if (i < NPCTR) atomicAdd((unsigned long long*)&d.pcum[(size_t)i * d.P + p], (unsigned long long)r);
+        else d.p2min[(size_t)(i - NPCTR) * d.P + p] = r;
+        if (i >= NPCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NPCTR], (unsigned long long)r);
     }
     __shared__ uint32_t s_ids[ST];
     __shared__ uint64_t s_h;
@@ -2379,7 +2623,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         stamp[6] = nact;
         stamp[7] = s_nsend;
     }
-    if (d.wtime) {  // this partition's busy time; k_plan charges the wait for the last one
+    if (d.wtime) {  // this partition's busy time; k_scatter's rmin workgroup charges the wait for the last one
         __syncthreads();
         if (tid == 0) {
             const uint64_t t_end = wait_stamp();
@@ -2393,7 +2637,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 // Events → calendar buckets.  Local events were counted and reserved per
 // (partition, bucket) by k_proc; received exchange blocks (multi-shard) are
 // counted here by k_count, split evenly over its grid.  k_scatter writes both
-// into the chunks k_plan allocated: one workgroup per partition, then the
+// into the chunks the reserving rows allocated: one workgroup per partition, then the
 // received-block split (wbase rows P + workgroup).
 
 // Exclusive offsets of the received blocks' event counts (own block: 0).
@@ -2474,14 +2718,14 @@ __global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
 }
 
 // k_scatter: new (and received) events into the calendar, fused with the
-// gather of the window k_plan just listed.  Workgroup roles:
+// gather of the window it plans.  Workgroup roles:
 //   [0, P)          partition blk's staged local events (process step)
 //   [P, P + G3)     the received blocks' events (multi-shard), split evenly
 //   [g0, g0 + G1)   gather: the listed due chunks into the host partitions
 //   last            rmin: first live bucket beyond the new window, its min
 // An inserted event due in the new window (t < E) is routed straight to its
 // host partition instead: its slot stays empty in a fully due bucket (whose
-// chunks k_plan did not grow and k_scatter's gather returns to the ring) or
+// chunks were not grown and k_scatter's gather returns to the ring) or
 // becomes a tombstone in the straddling bucket.  Events that stay in the
 // straddling bucket add to the carry min (the next MIN term), as the
 // gather's leftovers do.
@@ -2502,7 +2746,7 @@ struct Route {
 
 // One batch of up to SU events per thread (every thread of the workgroup
 // calls it): slot from the (partition, bucket) reservation cursor, chunk
-// from k_plan's allocation; due events routed.  Returns nothing; carry min
+// from the reserving row's allocation; due events routed.  Returns nothing; carry min
 // and tombstones accumulate in smin / ntomb.
 __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t x, uint32_t* s_cur, uint32_t* s_pc,
                                              uint32_t* s_pk, const bool (&v)[SU], const uint64_t (&t)[SU],
@@ -2817,6 +3061,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
     const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
+    if (tid == 0 && hi > lo)  // C_RECV: the received events this workgroup writes
+        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_RECV * d.P + w % d.P], (unsigned long long)(hi - lo));
     for (uint64_t i0 = lo; i0 < hi; i0 += K3_T * SU) {
         bool v[SU];
         uint64_t t[SU], k[SU];
@@ -2837,7 +3083,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
 // The local MIN terms of a round: carry min (k_scatter's gather and inserts),
 // emitted min and discovery min (k_proc), and the buckets beyond the window
 // (rmin).
-__device__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
+__device__ __forceinline__ void reduce_local(const Dev& d, uint64_t* s16, uint64_t& m, uint64_t& j) {
     const uint32_t cur = (uint32_t)(d.rs->fold & 1);
     uint64_t mm = d.rs->xcarry2[cur], jj = UINT64_MAX;
     for (uint32_t i = threadIdx.x; i < d.P; i += blockDim.x) {
@@ -3316,6 +3562,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.light_q = env_u32z("SG_LIGHT_Q", 1);
     D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
     D.rec_all = env_u32z("SG_REC_ALL", 2 * K2_T);
+    D.flat = env_u32z("SG_FLAT", 0) != 0 && D.workload == SG_WORKLOAD_PHOLD;
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
@@ -3436,7 +3683,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     std::vector<SlotInfo> si(L);
     for (size_t i = 0; i < L; ++i) {
         const uint32_t h = host_of_slot[i];
-        hs[i] = HostState{t->host_rng[h], 0, 0, 0, 0};  // evc 0 until boot
+        hs[i] = HostState{t->host_rng[h], h, (uint64_t)t->host_vertex[h] << 48, 0, 0};  // evc 0 until boot
         si[i] = SlotInfo{h, t->host_vertex[h]};
     }
     hipError_t err = hipSuccess;
@@ -3527,10 +3774,14 @@ int sg_engine_boot(sg_engine* e) {
     }
     HIPCHK(hipSetDevice(e->device));
     const Dev& d = e->d;
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P + d.G3));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
@@ -3547,10 +3798,17 @@ static int enqueue_process(sg_engine* e) {
     const Dev& d = e->d;
     return timed_launch(e, SG_K_PROCESS, [&](hipEvent_t a, hipEvent_t b) {
         const dim3 g(d.P), t(K2_T);
-        if (d.dst_near && d.lds_rows) SG_LAUNCH((k_proc<true, true>), g, t, d.proc_lds, e->stream, a, b, d);
-        else if (d.dst_near) SG_LAUNCH((k_proc<true, false>), g, t, d.proc_lds, e->stream, a, b, d);
-        else if (d.lds_rows) SG_LAUNCH((k_proc<false, true>), g, t, d.proc_lds, e->stream, a, b, d);
-        else SG_LAUNCH((k_proc<false, false>), g, t, d.proc_lds, e->stream, a, b, d);
+        if (d.flat) {
+            if (d.dst_near && d.lds_rows) SG_LAUNCH((k_proc<true, true, true>), g, t, d.proc_lds, e->stream, a, b, d);
+            else if (d.dst_near) SG_LAUNCH((k_proc<true, false, true>), g, t, d.proc_lds, e->stream, a, b, d);
+            else if (d.lds_rows) SG_LAUNCH((k_proc<false, true, true>), g, t, d.proc_lds, e->stream, a, b, d);
+            else SG_LAUNCH((k_proc<false, false, true>), g, t, d.proc_lds, e->stream, a, b, d);
+        } else {
+            if (d.dst_near && d.lds_rows) SG_LAUNCH((k_proc<true, true, false>), g, t, d.proc_lds, e->stream, a, b, d);
+            else if (d.dst_near) SG_LAUNCH((k_proc<true, false, false>), g, t, d.proc_lds, e->stream, a, b, d);
+            else if (d.lds_rows) SG_LAUNCH((k_proc<false, true, false>), g, t, d.proc_lds, e->stream, a, b, d);
+            else SG_LAUNCH((k_proc<false, false, false>), g, t, d.proc_lds, e->stream, a, b, d);
+        }
     });
 }
 
@@ -3731,6 +3989,17 @@ int sg_engine_active_hosts(sg_engine* e, uint64_t* active, uint64_t* emitted) {
     return SG_OK;
 }
 
+int sg_engine_event_moves(sg_engine* e, uint64_t* emitted, uint64_t* gathered, uint64_t* received) {
+    if (!e) return SG_ERR_INVAL;
+    sg_round_stats s;
+    int rc = sg_engine_stats(e, &s);
+    if (rc) return rc;
+    if (emitted) *emitted = e->h_rs->ctr[C_EMIT];
+    if (gathered) *gathered = e->h_rs->ctr[C_GATHER];
+    if (received) *received = e->h_rs->ctr[C_RECV];
+    return SG_OK;
+}
+
 int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops, uint32_t* rng,
                          uint64_t* event_counter) {
     if (!e) return SG_ERR_INVAL;
@@ -3742,7 +4011,7 @@ int sg_engine_host_state(sg_engine* e, uint64_t* digest, uint64_t* pops, uint32_
     for (size_t sl = 0; sl < L; ++sl) {  // slots back to registration order
         const size_t i = e->host_of_slot[sl] - e->d.lo;
         if (digest) digest[i] = hs[sl].digest;
-        if (pops) pops[i] = hs[sl].pops;
+        if (pops) pops[i] = hs[sl].pv & ((1ull << 48) - 1);
         if (rng) rng[i] = hs[sl].rng;
         if (event_counter) event_counter[i] = hs[sl].evc;
     }

@@ -96,6 +96,13 @@ class Engine:
         L.check(L.lib().sg_engine_active_hosts(self.h, C.byref(a), C.byref(e)))
         return a.value, e.value
 
+    def event_moves(self) -> dict:
+        """Cumulative events staged by k_proc, gathered by k_scatter from the
+        calendar into partitions, and received events k_scatter wrote."""
+        v = [C.c_uint64() for _ in range(3)]
+        L.check(L.lib().sg_engine_event_moves(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(("emitted", "gathered", "received"), (x.value for x in v)))
+
     def host_state(self) -> dict:
         n = self.n_local
         d, p, e = (np.zeros(n, np.uint64) for _ in range(3))

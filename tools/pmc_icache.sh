@@ -15,7 +15,7 @@ for f in sorted(glob.glob("gpurun_out/ic/p*/**/*counter_collection.csv", recursi
     rows = list(csv.DictReader(open(f)))
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in rows:
-        per[r["Kernel_Name"].split("(")[0][-12:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        per[r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in per.items():
         if "k_" not in k:
             continue

@@ -19,10 +19,10 @@ for g in ("mix", "act"):
     f = glob.glob(f"gpurun_out/pmc_issue/{g}/**/*counter_collection.csv", recursive=True)[0]
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
-        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         per[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for n, cs in per.items():
-        if not n.startswith(("k_proc", "k_scatter", "k_plan")):
+        if not n.startswith(("k_proc", "k_scatter", "k_count")):
             continue
         print(g, n, {c: round(sum(v[-8:]) / len(v[-8:])) for c, v in cs.items()})
 PY

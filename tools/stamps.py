@@ -34,6 +34,15 @@ for r in range(3):
     r_s = "%.2f" % np.median((st[rec, 12] - st[rec, 11]) / 100) if rec.any() else "n/a"
     print("   phase A, lane 0 of wave 0, first host (median us): state loads %.2f  sort %.2f  count draws %.2f  "
           "reserve %.2f" % tuple(np.median(a, axis=0)) + f"  record+store {r_s} ({int(rec.sum())} WGs)")
+    fl = st[:, 30] >= st[:, 1]
+    if fl.any():  # k_proc's flat pass ran (stamp 30 at its end)
+        print("   flat pass (median us): %.2f in %d WGs; phase A after it %.2f"
+              % (np.median(st[fl, 30] - st[fl, 1]) / 100, int(fl.sum()), np.median(st[fl, 2] - st[fl, 30]) / 100))
+        x = np.diff(st[fl][:, [1, 16, 17, 18, 19, 30]], axis=1) / 100
+        print("   flat pass, lane 0 (median us): start %.2f  draws %.2f  dst loads %.2f  sends %.2f  barrier %.2f"
+              % tuple(np.median(x, axis=0)))
+        w = (st[fl][:, 26:30] - st[fl][:, [1]]) / 100
+        print("   flat pass end per wave 0/4/8/12 (median us after its start):", np.round(np.median(w, axis=0), 2))
     t = np.diff(st[:, [3, 13, 14, 15, 4]], axis=1) / 100
     print("   after phase B (median us): phase C %.2f  partials %.2f  reservations %.2f  tail %.2f"
           % tuple(np.median(t, axis=0)))
