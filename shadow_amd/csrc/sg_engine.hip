@@ -1769,6 +1769,12 @@ __device__ __forceinline__ void near_resolve(const Dev& d, int32_t x, uint2 a, u
 // EXACT: d.dst_near (a destination is two adjacent 8-byte records per send);
 // the other instantiation resolves destinations through the weight probes
 // (and bisection).  ROWS: d.lds_rows (path records from the partition's LDS rows).
+// SG_ABL (timing experiments only; results are wrong with any bit set): 1 no
+// digest atomics, 2 no host-state stores, 4 no destination loads, 8 no staging
+// stores, 16 no bucket bins, 32 no digest hash
+#ifndef SG_ABL
+#define SG_ABL 0
+#endif
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
@@ -1818,7 +1824,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
     const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
     const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];  // the last gather freed nfree more
-    for (uint32_t h = tid; h < HP; h += K2_T) s_n[h] = 0;
+    // flat pass: a host's digest terms of its events but the last, summed in
+    // LDS over s_vh / s_sb (phase A's arrays, free until phase A runs)
+    unsigned long long* s_dig = reinterpret_cast<unsigned long long*>(s_vh);
+    for (uint32_t h = tid; h < HP; h += K2_T) {
+        s_n[h] = 0;
+        if constexpr (FLAT) s_dig[h] = 0;
+    }
     for (uint32_t rb = tid; rb < R; rb += K2_T) {
         s_bc[rb] = 0;
         s_bm[rb] = UINT32_MAX;
@@ -2268,8 +2280,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.bt = S + et;
             const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
             const uint64_t bseq = ev.k & SEQ_MASK;
-            f.term = digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
-            if (cnt == 1) f.term += w23.x;  // the host's new digest
+            f.term = (SG_ABL & 32) ? f.bt ^ bseq : digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
+            if (sc.rank + 1 == cnt) f.term += w23.x;  // the last event: the old digest + its term
             if (d.trace) {
                 const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
                 if (ts < d.trace_cap) {
@@ -2320,21 +2332,27 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             tn = E;
                             ++a.ctr[C_BUMPED];
                         }
-                        if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)f.h << SRC_SHIFT) | sq)) count_local(tn);
+                        if (SG_ABL & 8) {
+                            a.emin = tn < a.emin ? tn : a.emin;
+                            if (!(SG_ABL & 16)) count_local(tn);
+                        } else if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)f.h << SRC_SHIFT) | sq)) {
+                            if (!(SG_ABL & 16)) count_local(tn);
+                        }
                     }
                 }
             } else {
                 ++a.ctr[C_NULL];
             }
             HostState* hp = d.hs + sbase + f.hl;
-            if (f.flags & F_LAST) {  // the host's last event: its state after the round
+            if ((f.flags & F_LAST) && !(SG_ABL & 2)) {  // the host's last event: its state after the round
                 const uint64_t evc = f.sq + (kept ? 1u : 0u);
                 ulonglong2* hw = reinterpret_cast<ulonglong2*>(hp);
                 st_stream2(&hw[0], hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
                 if (!(f.flags & F_MULTI)) st_stream2(&hw[1], f.term, evc);
-                else hp->evc = evc;
+                else hp->evc = evc;  // the digest after the barrier below
+            } else if (!(SG_ABL & 1)) {  // an earlier event of a multi-event host (ok: F_MULTI)
+                atomicAdd(&s_dig[f.hl], (unsigned long long)f.term);
             }
-            if (f.flags & F_MULTI) atomicAdd((unsigned long long*)&hp->digest, (unsigned long long)f.term);
         };
         const bool stf = stamp && tid == 0;
         if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
@@ -2347,10 +2365,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         // for that store too (vmcnt counts in order)
         uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
         if constexpr (EXACT) {
-            const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
-            const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
-            near_resolve(d, f0.x, a0, b0, vd0, dst0);
-            near_resolve(d, f1.x, a1, b1, vd1, dst1);
+            if (SG_ABL & 4) {
+                dst0 = f0.g;
+                dst1 = f1.g;
+                vd0 = f0.g & 1023;
+                vd1 = f1.g & 1023;
+            } else {
+                const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
+                const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
+                near_resolve(d, f0.x, a0, b0, vd0, dst0);
+                near_resolve(d, f1.x, a1, b1, vd1, dst1);
+            }
         } else {
             const Probe pb0 = dst_probe(d, f0.g), pb1 = dst_probe(d, f1.g);
             dst0 = (f0.flags & F_OK) && (f0.flags & F_SND) ? dst_resolve(d, f0.x, f0.g, pb0, vd0) : 0u;
@@ -2371,10 +2396,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         flat_send(f0, vd0, dst0, pr0);
         flat_send(f1, vd1, dst1, pr1);
         if (stf) stamp[19] = wait_stamp();
-        if (stamp && (tid & 255) == 0) stamp[26 + (tid >> 8)] = __builtin_amdgcn_s_memrealtime();  // waves 0, 4, 8, 12
         __syncthreads();
+        // a multi-event host's digest: the last event's lane adds the others'
+        // terms (LDS; global atomics on the state's line next to the state
+        // stores cost about 10 us per round, profiles/r03/flat)
+        if ((f0.flags & (F_LAST | F_MULTI)) == (F_LAST | F_MULTI))
+            d.hs[sbase + f0.hl].digest = f0.term + s_dig[f0.hl];
+        if ((f1.flags & (F_LAST | F_MULTI)) == (F_LAST | F_MULTI))
+            d.hs[sbase + f1.hl].digest = f1.term + s_dig[f1.hl];
         nacta = s_nser;
         ser = nacta != 0;
+        if (ser) __syncthreads();  // phase A reuses s_vh / s_sb
         if (stf) stamp[30] = __builtin_amdgcn_s_memrealtime();
     }
     if (!ser) {
