@@ -3594,7 +3594,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.light_q = env_u32z("SG_LIGHT_Q", 1);
     D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
     D.rec_all = env_u32z("SG_REC_ALL", 2 * K2_T);
-    D.flat = env_u32z("SG_FLAT", 0) != 0 && D.workload == SG_WORKLOAD_PHOLD;
+    D.flat = env_u32z("SG_FLAT", 1) != 0 && D.workload == SG_WORKLOAD_PHOLD;
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
