@@ -2903,6 +2903,22 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             atomicAdd((unsigned long long*)&rs->splan, 1ull);
         }
     }
+    // Insert role: what does not depend on the window is loaded while thread 0
+    // plans (waves 1.. at once; wave 0 after its plan): the partition's count,
+    // its first SU staged events per thread and its reservation bases.
+    Rec pre[SU];
+    uint32_t pre_n = 0;
+    if (blk < d.P) {  // uniform
+        const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
+        pre_n = d.rcnt[blk];
+#pragma unroll
+        for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[threadIdx.x + q * K3_T]);
+        uint32_t* s_cur = (uint32_t*)lds;
+        uint32_t* s_pc = s_cur + RMAX;
+        const uint32_t* wb = d.wbase + (size_t)blk * R;
+        for (uint32_t rb = tid; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+        for (uint32_t p = tid; p < d.P; p += K3_T) s_pc[p] = 0;
+    }
     __syncthreads();
     if (sv.quit) return;  // uniform: the run ended (no workgroup took a ticket)
     const uint32_t g0 = d.P + (recv ? d.G3 : 0);
@@ -3050,25 +3066,27 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     uint32_t* s_off = (uint32_t*)(s16 + 16);  // [MAXG] received blocks' offsets
     const uint32_t* wb = d.wbase + (size_t)blk * R;
     uint64_t smin = UINT64_MAX, ntomb = 0;
-    if (blk < d.P) {  // partition blk's staged local events
+    if (blk < d.P) {  // partition blk's staged local events (bases and first batch loaded above)
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
         Rec r[SU];
         if (!sv.ins_local) return;
-        const uint32_t n = d.rcnt[blk];
+        const uint32_t n = pre_n;
         if (n == 0) return;  // uniform: nothing routed, nothing to finish
         const uint64_t S = sv.ins_S;
-        for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
-        for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
-        __syncthreads();
         if (st) {
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[5] = n;
         }
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+            if (i0 == 0) {  // uniform
 #pragma unroll
-            for (int q = 0; q < SU; ++q) {
-                const uint32_t i = i0 + threadIdx.x + q * K3_T;
-                r[q] = ld_stream(&src[i < n ? i : 0]);
+                for (int q = 0; q < SU; ++q) r[q] = pre[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < SU; ++q) {
+                    const uint32_t i = i0 + threadIdx.x + q * K3_T;
+                    r[q] = ld_stream(&src[i < n ? i : 0]);
+                }
             }
             bool v[SU];
             uint64_t t[SU], k[SU];
