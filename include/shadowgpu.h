@@ -19,7 +19,7 @@
  *      events are written into the buckets, the next window is planned (MIN
  *      next-event time + min-latency runahead → next [start, end)) and its due
  *      events are gathered into the host partitions.  Several shards add one
- *      all-to-all per step (k_count reserves the received events).
+ *      all-to-all per step (the next k_proc queues the received events).
  */
 #ifndef SHADOWGPU_H
 #define SHADOWGPU_H
@@ -357,13 +357,19 @@ int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n
  *       overflow flags, round} then n triples {time, src << 40 | srcHostEventID,
  *       dst};
  *   (caller) all_to_all of send → recv, equal [rows][3] blocks per peer;
- *   step_recv(e, recv) — local new events + received triples into the queues;
- *       the next window from the G received headers (the MIN all-reduce of
+ *   step_recv(e, recv) — local new events into the queues, received triples
+ *       due in the new window straight into their hosts' partitions; the next
+ *       window from the G received headers (the MIN all-reduce of
  *       scheduler.c:386-408 / master.c:450-480, carried by the all-to-all).
- *       When any sender still has outbox leftovers the next step is a drain
- *       step (same window, no processing). */
+ *       The other received triples are queued by the next step_send's kernel,
+ *       so recv must stay intact until the next step_send has been enqueued
+ *       (the next all-to-all overwrites it only after that).  When any sender
+ *       still has outbox leftovers the next step is a drain step (same window,
+ *       no processing). */
 int sg_engine_exchange_rows(sg_engine* e, uint64_t* rows);
-/* Change exchange_cap between steps (every shard must use the same value). */
+/* Change exchange_cap between steps (every shard must use the same value).  The
+ * caller may then reallocate its send / receive buffers: the engine keeps a
+ * copy of the last received blocks for the next step_send. */
 int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap);
 /* Largest per-peer outbox of a process step since the last reset. */
 int sg_engine_exchange_peak(sg_engine* e, uint64_t* peak, int reset);
@@ -399,8 +405,8 @@ int sg_engine_set_graph(sg_engine* e, uint32_t batch);
  * stream): total ms and launches per kernel class, arrays of SG_KCLASSES. */
 enum sg_kernel_class {
     SG_K_PROCESS = 0,  /* k_proc: pops + PHOLD body + send resolution + bucket reservations */
-    SG_K_INSERT = 1,   /* k_scatter (+ k_count when sharded): events into their buckets,
-                          the next window planned and gathered */
+    SG_K_INSERT = 1,   /* k_scatter: events into their buckets, the next window planned
+                          and gathered (sharded: received events due in it routed) */
     SG_K_PLAN = 2,     /* unused: planning is a k_scatter role now (class kept for ABI stability) */
     SG_K_GATHER = 3,   /* unused: the gather is a k_scatter role now (class kept for ABI stability) */
     SG_K_EXCHANGE = 4, /* the step's RCCL all-to-all (sg_engine_run_steps): this shard's

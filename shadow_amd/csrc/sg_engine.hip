@@ -29,9 +29,11 @@
 //               outbox regions; the first xcap rows of each peer's outbox are the
 //               exchange block itself, and the last k_proc workgroup to finish
 //               writes the block headers (the shard's MIN terms).  After the
-//               all-to-all, k_count reserves the received events and k_scatter
-//               plans from the G headers.  On a drain step k_proc only copies
-//               outbox leftovers into the blocks.
+//               all-to-all, k_scatter plans from the G headers and routes the
+//               received events due in the new window to their partitions; the
+//               next k_proc stages the rest with its own new events
+//               (stage_received).  On a drain step k_proc copies outbox
+//               leftovers into the blocks and stages the received events.
 //
 // HBM layout: 16-B records everywhere.
 //   bucket record     {dst_local << 40 | (t - b*W),  src << 40 | srcHostEventID}
@@ -69,7 +71,7 @@ constexpr uint64_t TOMB = ~0ULL;
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 constexpr int CH_SHIFT = 10;
 constexpr uint32_t CH = 1u << CH_SHIFT;  // events per chunk (16 KB)
-constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
+constexpr uint32_t RMAX = 4096;          // ring buckets (LDS bucket bins)
 // Bucket sub-lists: a reserving row appends to sub-list (row mod XS) of a
 // bucket, so about P / XS rows contend per counter.  XS = 1 measured fastest
 // since the reservations moved into k_proc (profiles/r02/knobs/xs_ab.log:
@@ -81,9 +83,9 @@ constexpr uint32_t RMAX = 4096;          // ring buckets (k_count LDS bins)
 constexpr uint32_t XS = SG_XS;
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
-constexpr uint32_t G3MAX = 512;          // k_count workgroups (received-block split)
+constexpr uint32_t G3MAX = 512;          // k_scatter receive-role workgroups (received-block split)
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
-constexpr int K1_T = 256, K2_T = 1024, K3_T = 512, K3_E = 8, PL_T = 1024;
+constexpr int K2_T = 1024, K3_T = 512;
 constexpr uint32_t RETAINED = 1u << 31;
 constexpr uint32_t ST = 16;           // chunk ids in a reserving row's stash
 constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (bucket width set to fit)
@@ -247,7 +249,7 @@ struct RoundState {
     uint64_t splan;          // k_scatter workgroups that read the round state this launch: the
                              // last one publishes the next (SG step plan, k_scatter)
     uint64_t fl_head, fl_tail;
-    uint64_t ins_local;      // k_count took the staged local events (process step)
+    uint64_t ins_local;      // k_proc staged events for k_scatter's insert role this step
     uint64_t ins_S;          // their window start (staged times are relative to it)
     // multi-shard step protocol
     uint64_t phase;      // 0: process step, 1: drain step (outbox leftovers only)
@@ -255,6 +257,7 @@ struct RoundState {
     uint64_t peak_peer;  // largest per-peer outbox of a process step (since reset)
     uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
     uint64_t xacc[2];    // emitted min, discovery min of k_proc's workgroups (atomics)
+    uint64_t recv_ok;    // a several-shard k_scatter read the receive buffer: the next k_proc stages it
 };
 
 struct Dev {
@@ -301,11 +304,11 @@ struct Dev {
     uint64_t* wtime;          // [3][P] barrier timers (scheduler.c:380-389), or null: busy ticks,
                               // idle ticks (waiting for the round's last partition), this round's end
     HostState* hs;            // [L]
-    // calendar: bucket rb is XS sub-lists; a reserving row (k_proc partition p,
-    // k_count workgroup w) appends to sub-list p % XS (w % XS)
+    // calendar: bucket rb is XS sub-lists; a reserving row (k_proc partition p)
+    // appends to sub-list p % XS
     Rec* pool;                // [NCH][CH]
     uint32_t* btab;           // [XS][R][NCH] chunk ids of each sub-list
-    uint32_t* bk;             // [XS][R] slots reserved (k_proc / k_count atomics)
+    uint32_t* bk;             // [XS][R] slots reserved (k_proc atomics)
     uint32_t* bw;             // [2][XS][R] slots written before the step: k_scatter reads
                               // bw[fold & 1] and copies bk into the other half for the next step
     uint32_t* btomb;          // [R] tombstones
@@ -330,6 +333,9 @@ struct Dev {
     Slot* rem;                // [P][ECAP]
     uint32_t* rem_dst;        // [P][ECAP]
     int64_t* xsend;           // [G][xrows][3] this step's exchange blocks (set by step_send)
+    const int64_t* xrecv;     // [G][xrows_in][3] the previous step's received blocks (k_proc stages
+                              // what k_scatter did not route), or null
+    uint64_t xrows_in, xcap_in;  // their layout (the exchange cap may have changed since)
     int64_t* outq;            // [G][oreg][3] per-peer outbox regions (rows < xcap go
                               // straight into xsend on a process step)
     uint64_t oreg;            // rows per peer region (P * ECAP: every staged event fits)
@@ -482,10 +488,12 @@ __device__ __forceinline__ uint32_t choose_dst(const Dev& d, int32_t x, HostInfo
     info.vertex = v;
     return r;
 }
+// The shard that owns global slot h: shard g holds [floor(g*N/G), floor((g+1)*N/G)),
+// so the owner is the largest g with floor(g*N/G) <= h, i.e. floor(((h+1)*G - 1)/N).
+// (Arithmetic, not a search over d.bounds: a dynamic index into the by-value
+// kernel argument would make the compiler copy all of Dev to scratch.)
 __device__ __forceinline__ uint32_t owner_of(const Dev& d, uint32_t h) {
-    uint32_t p = 0;
-    while (p + 1 < d.G && h >= d.bounds[p + 1]) ++p;
-    return p;
+    return (uint32_t)((((uint64_t)h + 1) * d.G - 1) / d.N);
 }
 
 template <typename T>
@@ -719,6 +727,7 @@ __global__ void k_boot(Dev d) {
         rs->ticket = 0;
         rs->xacc[0] = UINT64_MAX;
         rs->xacc[1] = UINT64_MAX;
+        rs->recv_ok = 0;
     }
     if (i < d.G && d.outn) {
         d.outn[i] = 0;
@@ -1483,7 +1492,7 @@ __device__ __forceinline__ uint64_t rmw_read(uint64_t* p) {
     return atomicAdd((unsigned long long*)p, 0ull);
 }
 
-// mode 0: one shard, after k_proc; 1: several shards, after k_count (recv:
+// mode 0: one shard, after k_proc; 1: several shards, after the all-to-all (recv:
 // the exchange blocks); 2: boot (the first window is listed already).  One
 // thread.
 __device__ void step_view(const Dev& d, int mode, const int64_t* recv, StepView& sv) {
@@ -1574,6 +1583,7 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     rs->fold = sv.fold + 1;
     rs->splan = 0;
     if (mode == 1) {
+        rs->recv_ok = 1;  // the next k_proc stages what this launch did not route
         if (d.check) {
             // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in
             // this shard's headers, from device-scope atomics it read without a
@@ -1769,6 +1779,102 @@ __device__ __forceinline__ void near_resolve(const Dev& d, int32_t x, uint2 a, u
 // EXACT: d.dst_near (a destination is two adjacent 8-byte records per send);
 // the other instantiation resolves destinations through the weight probes
 // (and bisection).  ROWS: d.lds_rows (path records from the partition's LDS rows).
+// Exclusive offsets of the received blocks' event counts (own block: 0).
+// rows / cap: the blocks' layout (HDR + cap rows per peer).
+__device__ __forceinline__ uint64_t recv_offsets(const Dev& d, const int64_t* recv, uint64_t rows, uint64_t cap,
+                                                 uint32_t* s_off, uint64_t* s16,
+                                 bool check) {
+    const uint32_t s = threadIdx.x;
+    uint64_t c = 0;
+    if (s < d.G && s != d.g) {
+        const uint64_t n = (uint64_t)recv[(size_t)s * rows * 3 + H_N];
+        if (n <= cap) c = n;
+        else if (check) flag(d, OV_XCHG);
+    }
+    uint64_t total;
+    const uint64_t run = block_excl_scan(c, s16, &total);
+    if (s < d.G) s_off[s] = (uint32_t)run;
+    __syncthreads();
+    return total;
+}
+
+// Received event `idx` of the concatenated blocks: t, key, dst_local.
+__device__ __forceinline__ bool recv_event(const Dev& d, const int64_t* recv, uint64_t rows, const uint32_t* s_off,
+                                           uint32_t idx, uint64_t& t, uint64_t& k, uint32_t& dl) {
+    uint32_t lo = 0, hi = d.G - 1;  // last block with s_off <= idx
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= idx) lo = mid; else hi = mid - 1;
+    }
+    const int64_t* row = recv + ((size_t)lo * rows + HDR + (idx - s_off[lo])) * 3;
+    t = (uint64_t)row[0];
+    k = (uint64_t)row[1];
+    dl = (uint32_t)row[2] - d.lo;
+    return dl < d.L;
+}
+
+// A staged event at time t into a reserving row's LDS bucket bins (bucket bS
+// + o is ring slot (bSr + o) % R): count and min offset in the bucket.  False
+// (and no bin) when t lies outside the calendar's horizon.
+__device__ __forceinline__ bool bin_time(const Dev& d, uint64_t t, uint64_t bS, uint64_t bSW, uint32_t bSr,
+                                         uint32_t* s_bc, uint32_t* s_bm) {
+    const uint32_t R = d.R;
+    const uint64_t W = d.W;
+    uint32_t o, off;
+    if (d.ring32) {  // launch-uniform: no 64-bit division
+        const uint64_t rel = t - bSW;
+        o = wdiv(d, (uint32_t)rel);
+        off = (uint32_t)rel - o * (uint32_t)W;
+        if (t < bSW || (rel >> 32) || o >= R) return false;
+    } else {
+        const uint64_t b = t / W;
+        if (b < bS || b - bS >= R) return false;
+        o = (uint32_t)(b - bS);
+        off = (uint32_t)(t - b * W);
+    }
+    uint32_t rb = bSr + o;
+    rb = rb >= R ? rb - R : rb;
+    atomicAdd(&s_bc[rb], 1u);
+    atomicMin(&s_bm[rb], off);
+    return true;
+}
+
+// Several shards: k_proc stages its share of the events the previous step
+// received (recv: that step's blocks, intact until this step's all-to-all)
+// like local events — into loc and the bucket bins, reserved with them —
+// except those k_scatter already routed into this window's partitions
+// (routed: it planned this window, and t < E).  This is the insert of
+// received events (scheduler_push on the receiving side, scheduler.c:339-357):
+// no kernel of its own.  Every thread calls it (barrier inside).  Returns the
+// minimum time staged (UINT64_MAX: none).
+template <class Count>
+__device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* recv, uint32_t part, uint32_t nparts,
+                                                   bool routed, uint64_t S, uint64_t E, ProcShared& sh, bool& ovf,
+                                                   uint32_t* s_off, uint64_t* s16, Count count) {
+    const uint64_t total = recv_offsets(d, recv, d.xrows_in, d.xcap_in, s_off, s16, true);  // barrier inside
+    const uint64_t lo = total * part / nparts, hi = total * (part + 1) / nparts;
+    uint64_t mn = UINT64_MAX;
+    for (uint64_t i0 = lo; i0 < hi; i0 += blockDim.x) {
+        const uint64_t idx = i0 + threadIdx.x;
+        uint64_t t = 0, k = 0;
+        uint32_t dl = 0;
+        bool v = idx < hi;
+        if (v && !recv_event(d, recv, d.xrows_in, s_off, (uint32_t)idx, t, k, dl)) {
+            flag(d, OV_XCHG);
+            v = false;
+        }
+        if (v && routed && t < E) v = false;  // k_scatter put it in its partition
+        if (v) {
+            const uint32_t slot = wave_slot(&sh.nloc);
+            if (slot < d.ECAP) st_stream(&d.loc[(size_t)part * d.ECAP + slot], Rec{((uint64_t)dl << 40) | (t - S), k});
+            else ovf = true;
+            count(t);
+            mn = t < mn ? t : mn;
+        }
+    }
+    return mn;
+}
+
 // SG_ABL (timing experiments only; results are wrong with any bit set): 1 no
 // digest atomics, 2 no host-state stores, 4 no destination loads, 8 no staging
 // stores, 16 no bucket bins, 32 no digest hash
@@ -1782,11 +1888,6 @@ template <bool EXACT, bool ROWS, bool FLAT>
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
     if (rs->done) return;
-    if (rs->phase) {  // drain step: outbox leftovers into the exchange blocks
-        __shared__ uint64_t s16d[16];
-        if (d.xsend) fill_blocks(d, blockIdx.x, gridDim.x, s16d);
-        return;
-    }
     extern __shared__ __align__(16) unsigned char dyn[];
     const uint32_t HP = d.HP, R = d.R;
     uint32_t* s_n = (uint32_t*)dyn;             // [HP] events per host
@@ -1804,10 +1905,55 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ uint64_t s16[16];
     __shared__ uint64_t s_red[K2_T / 64][NPCTR + 2];
     __shared__ uint32_t s_obase[MAXG], s_oslot[MAXG];
+    __shared__ uint32_t s_roff[MAXG];  // received blocks' offsets (stage_received)
+    __shared__ uint32_t s_ids[ST];
+    __shared__ uint64_t s_h;
     const uint64_t S = rs->S, E = rs->E;
+    // several shards: stage the previous step's received events this step
+    // (k_scatter routed those due in this window when it planned it: listed)
+    const bool stage_recv = d.xrecv && rs->recv_ok;
+    const bool recv_routed = rs->listed != 0;
     const bool want_jump = rs->jmin > d.gjmin;  // discovery can still lower the window's jump
     const uint32_t p = blockIdx.x;
     const uint32_t tid = threadIdx.x;
+    if (rs->phase) {
+        // drain step: outbox leftovers into the exchange blocks; the previous
+        // step's received events staged and reserved (no window was planned,
+        // so none was routed).  The headers repeat the process step's MIN
+        // terms, whose emitted minima cover the staged events.
+        if (d.xsend) fill_blocks(d, p, gridDim.x, s16);
+        if (tid == 0 && p == 0) {
+            rs->ins_local = stage_recv ? 1 : 0;
+            rs->ins_S = S;
+        }
+        if (!stage_recv) return;  // uniform
+        const uint32_t R = d.R;
+        const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
+        const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];
+        const uint64_t bS = rs->bS, bSW = bS * d.W;
+        const uint32_t bSr = (uint32_t)(bS % R);
+        uint32_t* s_bc = (uint32_t*)(dyn + d.bin_off);
+        uint32_t* s_bm = s_bc + R;
+        for (uint32_t rb = tid; rb < R; rb += K2_T) {
+            s_bc[rb] = 0;
+            s_bm[rb] = UINT32_MAX;
+        }
+        if (tid == 0) sh.nloc = 0;
+        __syncthreads();
+        bool ovf = false, hz = false;
+        (void)stage_received(d, d.xrecv, p, gridDim.x, false, S, E, sh, ovf, s_roff, s16, [&](uint64_t t) {
+            if (!bin_time(d, t, bS, bSW, bSr, s_bc, s_bm)) hz = true;
+        });
+        if (ovf) flag(d, OV_PROC);
+        if (hz) flag(d, OV_HORIZON);
+        __syncthreads();
+        reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
+        if (tid == 0) {
+            if (sh.nloc > d.ECAP) flag(d, OV_PROC);
+            d.rcnt[p] = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
+        }
+        return;
+    }
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -2026,28 +2172,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     bool horizon = false;
     const uint64_t bSW = bS * W;
     auto count_local = [&](uint64_t t) {  // one staged local event into the bucket bins
-        uint32_t o, off;  // bucket bS + o, the offset in it
-        if (d.ring32) {   // launch-uniform: no 64-bit division
-            const uint64_t rel = t - bSW;
-            o = wdiv(d, (uint32_t)rel);
-            off = (uint32_t)rel - o * (uint32_t)W;
-            if (t < bSW || (rel >> 32) || o >= R) {
-                horizon = true;
-                return;
-            }
-        } else {
-            const uint64_t b = t / W;
-            if (b < bS || b - bS >= R) {
-                horizon = true;
-                return;
-            }
-            o = (uint32_t)(b - bS);
-            off = (uint32_t)(t - b * W);
-        }
-        uint32_t rb = bSr + o;
-        rb = rb >= R ? rb - R : rb;
-        atomicAdd(&s_bc[rb], 1u);
-        atomicMin(&s_bm[rb], off);
+        if (!bin_time(d, t, bS, bSW, bSr, s_bc, s_bm)) horizon = true;
     };
     uint32_t nacta = nact;  // the hosts phase A takes: s_act[0, nacta)
     auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
@@ -2546,6 +2671,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
         }
     }
+    if (stage_recv) {  // uniform; a barrier inside
+        const uint64_t m = stage_received(d, d.xrecv, p, gridDim.x, recv_routed, S, E, sh, a.overflow, s_roff, s16,
+                                          count_local);
+        a.emin = m < a.emin ? m : a.emin;  // in this shard's MIN terms from now on
+    }
     __syncthreads();  // staging done: sh.nloc final, bins complete
     if (d.outn) {
         // multi-shard: the partition's events for other shards into their peers'
@@ -2603,8 +2733,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         else d.p2min[(size_t)(i - NPCTR) * d.P + p] = r;
         if (i >= NPCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NPCTR], (unsigned long long)r);
     }
-    __shared__ uint32_t s_ids[ST];
-    __shared__ uint64_t s_h;
     reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
     if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid == 0) {
@@ -2666,88 +2794,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 }
 
 // --------------------------------------------------------------- insert ----
-// Events → calendar buckets.  Local events were counted and reserved per
-// (partition, bucket) by k_proc; received exchange blocks (multi-shard) are
-// counted here by k_count, split evenly over its grid.  k_scatter writes both
-// into the chunks the reserving rows allocated: one workgroup per partition, then the
-// received-block split (wbase rows P + workgroup).
-
-// Exclusive offsets of the received blocks' event counts (own block: 0).
-__device__ uint64_t recv_offsets(const Dev& d, const int64_t* recv, uint32_t* s_off, uint64_t* s16,
-                                 bool check) {
-    const uint32_t s = threadIdx.x;
-    uint64_t c = 0;
-    if (s < d.G && s != d.g) {
-        const uint64_t n = (uint64_t)recv[(size_t)s * d.xrows * 3 + H_N];
-        if (n <= d.xcap) c = n;
-        else if (check) flag(d, OV_XCHG);
-    }
-    uint64_t total;
-    const uint64_t run = block_excl_scan(c, s16, &total);
-    if (s < d.G) s_off[s] = (uint32_t)run;
-    __syncthreads();
-    return total;
-}
-
-// Received event `idx` of the concatenated blocks: t, key, dst_local.
-__device__ __forceinline__ bool recv_event(const Dev& d, const int64_t* recv, const uint32_t* s_off,
-                                           uint32_t idx, uint64_t& t, uint64_t& k, uint32_t& dl) {
-    uint32_t lo = 0, hi = d.G - 1;  // last block with s_off <= idx
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (s_off[mid] <= idx) lo = mid; else hi = mid - 1;
-    }
-    const int64_t* row = recv + ((size_t)lo * d.xrows + HDR + (idx - s_off[lo])) * 3;
-    t = (uint64_t)row[0];
-    k = (uint64_t)row[1];
-    dl = (uint32_t)row[2] - d.lo;
-    return dl < d.L;
-}
-
-// Multi-shard only: received events → bucket counts, one reservation per
-// (workgroup, bucket).  Every step runs it; it records whether this step's
-// k_scatter also takes the staged local events (process steps only).
-__global__ __launch_bounds__(K3_T) void k_count(Dev d, const int64_t* recv) {
-    RoundState* rs = d.rs;
-    if (rs->done) return;
-    __shared__ uint32_t s_off[MAXG];
-    __shared__ uint32_t s_bc[RMAX];  // per bucket: events of this workgroup
-    __shared__ uint32_t s_bm[RMAX];  // per bucket: min time offset within the bucket
-    __shared__ uint64_t s16[16];
-    __shared__ uint32_t s_ids[ST];
-    __shared__ uint64_t s_h;
-    const uint64_t W = d.W, bS = rs->bS;
-    const uint32_t R = d.R;
-    const uint32_t row = d.P + blockIdx.x;
-    const uint32_t stash_id = d.stash[(size_t)row * ST + (threadIdx.x & (ST - 1))], stash_n = d.stn[row];
-    const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) rs->ins_local = rs->phase == 0;
-    for (uint32_t b = threadIdx.x; b < R; b += K3_T) {
-        s_bc[b] = 0;
-        s_bm[b] = UINT32_MAX;
-    }
-    const uint64_t total = recv_offsets(d, recv, s_off, s16, true);
-    const uint64_t lo = total * blockIdx.x / gridDim.x, hi = total * (blockIdx.x + 1) / gridDim.x;
-    for (uint64_t idx = lo + threadIdx.x; idx < hi; idx += K3_T) {
-        uint64_t t, k;
-        uint32_t dl;
-        if (!recv_event(d, recv, s_off, (uint32_t)idx, t, k, dl)) {
-            flag(d, OV_XCHG);
-            continue;
-        }
-        const uint64_t b = t / W;
-        if (b < bS || b - bS >= R) {
-            flag(d, OV_HORIZON);
-            continue;
-        }
-        const uint32_t rb = (uint32_t)(b % R);
-        atomicAdd(&s_bc[rb], 1u);
-        atomicMin(&s_bm[rb], (uint32_t)(t - b * W));
-    }
-    __syncthreads();
-    reserve_buckets<K3_T>(d, row, blockIdx.x % XS, s_bc, s_bm, bS, (uint32_t)(bS % R), stash_id, stash_n, ring_end,
-                          s_ids, &s_h, s16);
-}
+// Events → calendar buckets.  Staged events (a partition's new events and,
+// several shards, its share of the previous step's received events) were
+// counted and reserved per (partition, bucket) by k_proc; k_scatter writes
+// them into the chunks the reserving rows allocated, one workgroup per
+// partition.
 
 // k_scatter: new (and received) events into the calendar, fused with the
 // gather of the window it plans.  Workgroup roles:
@@ -2884,7 +2935,7 @@ __device__ void plan_when_read(const Dev& d, int mode, const StepView& sv, const
     publish_step(d, mode, sv, recv);
 }
 
-// mode: 0 one shard (after k_proc), 1 several shards (after k_count; recv the
+// mode: 0 one shard (after k_proc), 1 several shards (after the all-to-all; recv the
 // exchange blocks), 2 boot.  Every workgroup plans the step (step_view) from
 // the state as the previous kernels left it and reports that it has read it
 // (a fire-and-forget arrival); the last workgroup (the rmin role) publishes
@@ -3000,7 +3051,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         uint64_t* s_hh = s16 + 16;
         uint32_t* s_have = (uint32_t*)(s_hh + 1);  // [PMAX + G3MAX]
         uint32_t* s_roff = s_have + PMAX + G3MAX;  // [PMAX + G3MAX] first list entry of each row
-        const uint32_t rows = d.P + (d.outn ? d.G3 : 0u), NCH = d.NCH;
+        const uint32_t rows = d.P, NCH = d.NCH;  // the reserving rows: k_proc's partitions
         const uint64_t avail = sv.tail;
         uint32_t have[RPT];
         uint32_t mine = 0;
@@ -3064,7 +3115,6 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     uint32_t* s_pk = s_pc + PMAX;        // [PMAX] cursor within it
     uint64_t* s16 = (uint64_t*)(s_pk + PMAX);
     uint32_t* s_off = (uint32_t*)(s16 + 16);  // [MAXG] received blocks' offsets
-    const uint32_t* wb = d.wbase + (size_t)blk * R;
     uint64_t smin = UINT64_MAX, ntomb = 0;
     if (blk < d.P) {  // partition blk's staged local events (bases and first batch loaded above)
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
@@ -3105,28 +3155,43 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (st) st[3] = wait_stamp();
         return;
     }
-    // the received blocks' events, split evenly over G3 workgroups
+    // the received blocks' events due in the new window, split evenly over G3
+    // workgroups, routed straight to their host partitions (one reservation
+    // per (workgroup, partition)); the next k_proc stages the rest
+    // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
-    for (uint32_t rb = threadIdx.x; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
-    for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) s_pc[p] = 0;
-    const uint64_t total = recv_offsets(d, recv, s_off, s16, false);  // barrier inside
-    const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
-    if (tid == 0 && hi > lo)  // C_RECV: the received events this workgroup writes
-        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_RECV * d.P + w % d.P], (unsigned long long)(hi - lo));
-    for (uint64_t i0 = lo; i0 < hi; i0 += K3_T * SU) {
-        bool v[SU];
-        uint64_t t[SU], k[SU];
-        uint32_t dl[SU];
-#pragma unroll
-        for (int q = 0; q < SU; ++q) {
-            const uint64_t idx = i0 + threadIdx.x + q * K3_T;
-            t[q] = k[q] = 0;
-            dl[q] = 0;
-            v[q] = idx < hi && recv_event(d, recv, s_off, (uint32_t)idx, t[q], k[q], dl[q]);
-        }
-        insert_batch(d, ro, w % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+    for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
+        s_pc[p] = 0;
+        s_pk[p] = 0;
     }
-    insert_finish(d, ro, smin, ntomb, s16);
+    const uint64_t total = recv_offsets(d, recv, d.xrows, d.xcap, s_off, s16, false);  // barrier inside
+    const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
+    if (tid == 0 && hi > lo)  // C_RECV: the received events this workgroup looks at
+        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_RECV * d.P + w % d.P], (unsigned long long)(hi - lo));
+    if (!ro.listed) return;  // uniform: no new window, nothing is due
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
+        uint64_t t, k;
+        uint32_t dl;
+        if (recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) && t < ro.E) atomicAdd(&s_pc[part_of(d, dl)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
+        const uint32_t c = s_pc[p];
+        if (c) {
+            const uint32_t base = atomicAdd(&d.pcnt[p], c);
+            if (base + c > d.CAPP) flag(d, OV_PART);
+            s_pc[p] = base;
+        }
+    }
+    __syncthreads();
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
+        uint64_t t, k;
+        uint32_t dl;
+        if (!recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
+        const uint32_t p = part_of(d, dl);
+        const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
+        if (slot < d.CAPP) d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k};
+    }
 }
 
 // ----------------------------------------------------------------- plan ----
@@ -3217,12 +3282,18 @@ struct sg_engine {
     uint64_t gen = 0;  // bumped whenever a kernel argument captured in a graph changes
     hipGraphExec_t gexec = nullptr;
     hipEvent_t batch_ev[2] = {nullptr, nullptr};  // sg_engine_enqueue_rounds' queue bound
+    const int64_t* last_recv = nullptr;  // the last step_recv's buffer (read by the next k_proc)
+    uint64_t last_rows = 0, last_cap = 0;  // its layout
+    int64_t* recv_hold = nullptr;          // a copy of it kept across set_exchange_cap
+    size_t recv_hold_bytes = 0;
     struct GraphKey {
         uint64_t gen;
         const void *send, *recv, *comm;
+        const void* staged;  // the receive buffer the batch's first k_proc stages from
         uint32_t n;
         bool operator==(const GraphKey& o) const {
-            return gen == o.gen && send == o.send && recv == o.recv && comm == o.comm && n == o.n;
+            return gen == o.gen && send == o.send && recv == o.recv && comm == o.comm && staged == o.staged &&
+                   n == o.n;
         }
     } gkey{};
 };
@@ -3306,12 +3377,6 @@ static void harvest_timing(sg_engine* e) {
         e->free_ev.push_back(pr.b);
     }
     e->pending_ev.clear();
-}
-
-static uint32_t next_pow2(uint64_t x) {
-    uint32_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
 }
 
 static uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -3786,6 +3851,7 @@ int sg_engine_destroy(sg_engine* e) {
     for (auto ev : e->free_ev) (void)hipEventDestroy(ev);
     if (e->h_rs) (void)hipHostFree(e->h_rs);
     if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+    if (e->recv_hold) (void)hipFree(e->recv_hold);
     for (hipEvent_t ev : e->batch_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
@@ -3862,18 +3928,10 @@ static int enqueue_process(sg_engine* e) {
     });
 }
 
-// k_scatter: the new (and received) events into the calendar, the next
-// window planned and gathered.  Several shards (recv): k_count reserves the
-// received events first.
+// k_scatter: the staged events into the calendar, the next window planned and
+// gathered; several shards (recv): the received events due in it routed.
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
-    int rc;
-    if (recv) {
-        rc = timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
-            SG_LAUNCH(k_count, dim3(d.G3), dim3(K3_T), 0, e->stream, a, b, d, recv);
-        });
-        if (rc) return rc;
-    }
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
         SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv,
                   recv ? 1 : 0);
@@ -3947,7 +4005,7 @@ int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds) {
     int rc;
     for (uint32_t k = 0; n_rounds; ++k) {
         const uint32_t n = n_rounds < b ? (uint32_t)n_rounds : b;
-        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, n};
+        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, nullptr, n};
         if ((rc = enqueue_batch(e, key, n, [&] { return sg_engine_enqueue_round(e); }))) return rc;
         n_rounds -= n;
         // at most two batches queued: wait for the one before this
@@ -3982,7 +4040,7 @@ int sg_engine_run(sg_engine* e, uint64_t max_rounds, uint32_t batch) {
     while (done_rounds < max_rounds && !e->h_rs->done) {
         uint64_t n = max_rounds - done_rounds;
         if (n > batch) n = batch;
-        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, (uint32_t)n};
+        const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, nullptr, (uint32_t)n};
         if ((rc = enqueue_batch(e, key, (uint32_t)n, [&] { return sg_engine_enqueue_round(e); })))
             return rc;
         done_rounds += n;
@@ -4118,6 +4176,22 @@ int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap) {
         sg_set_error("sg_engine_set_exchange_cap: exchange_cap must be > 0");
         return SG_ERR_INVAL;
     }
+    // the last step's received blocks are still to be staged by the next
+    // k_proc, and the caller reallocates its buffers for the new cap: keep a
+    // copy (in the old layout, which the next k_proc decodes)
+    if (e->last_recv && e->last_recv != e->recv_hold) {
+        const size_t bytes = (size_t)e->d.G * e->last_rows * 3 * sizeof(int64_t);
+        if (bytes > e->recv_hold_bytes) {
+            if (e->recv_hold) HIPCHK(hipFree(e->recv_hold));
+            e->recv_hold = nullptr;
+            e->recv_hold_bytes = 0;
+            HIPCHK(hipMalloc(&e->recv_hold, bytes));
+            e->recv_hold_bytes = bytes;
+        }
+        HIPCHK(hipMemcpyAsync(e->recv_hold, e->last_recv, bytes, hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->last_recv = e->recv_hold;
+    }
     e->d.xcap = exchange_cap;
     e->d.xrows = HDR + exchange_cap;
     e->gen++;
@@ -4141,8 +4215,12 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
         return SG_ERR_INVAL;
     }
     e->d.xsend = send;  // k_proc writes the exchange blocks (launch argument)
+    e->d.xrecv = e->last_recv;  // and stages what the last step received but did not route
+    e->d.xrows_in = e->last_rows;
+    e->d.xcap_in = e->last_cap;
     rc = enqueue_process(e);
     e->d.xsend = nullptr;
+    e->d.xrecv = nullptr;
     return rc;
 }
 
@@ -4153,6 +4231,9 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv) {
         sg_set_error("sg_engine_step_recv: NULL receive buffer");
         return SG_ERR_INVAL;
     }
+    e->last_recv = recv;  // the next step_send's k_proc stages its non-due events
+    e->last_rows = e->d.xrows;
+    e->last_cap = e->d.xcap;
     return enqueue_insert_plan(e, recv);
 }
 
@@ -4401,7 +4482,7 @@ int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, 
     const uint32_t b = e->graph_batch ? e->graph_batch : 32;
     while (n_steps) {
         const uint32_t n = n_steps < b ? (uint32_t)n_steps : b;
-        const sg_engine::GraphKey key{e->gen, send, recv, c, n};
+        const sg_engine::GraphKey key{e->gen, send, recv, c, e->last_recv, n};
         if ((rc = enqueue_batch(e, key, n, step))) return rc;
         n_steps -= n;
     }

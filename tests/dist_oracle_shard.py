@@ -3,7 +3,7 @@ interface (pre / post around one all-to-all), so the distributed step protocol
 of shadow_amd.dist — fixed-size exchange blocks with headers, drain steps when
 an outbox exceeds exchange_cap, the window from the received headers — can be
 exercised on CPU with gloo.  Mirrors sg_engine.hip's exchange-block writes
-(k_proc), received-event insertion (k_count / k_scatter) and the window from the
+(k_proc), received-event insertion (the next k_proc / k_scatter) and the window from the
 headers (step_view).  Never used by the product path."""
 import numpy as np
 import torch

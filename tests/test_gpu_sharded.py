@@ -1,5 +1,6 @@
 """GPU: the sharded engine path (k_proc writing the outbox and exchange
-blocks, k_count and k_scatter reserving and inserting the received events: one
+blocks and queueing the previous step's received events, k_scatter routing the
+received events due in the new window: one
 all-to-all of fixed-size blocks per step, the window from the block headers,
 drain steps) with several shards on one device.  The
 all-to-all is done in-process with block copies on the shards' common stream,
