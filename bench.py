@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = os.path.join(ROOT, "profiles", "r02", "bench_k2", "pmc.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r03", "bench", "pmc.json")
 DOMINANT = "k_proc"
 
 
