@@ -458,17 +458,19 @@ int sg_engine_barrier_times(sg_engine* e, uint64_t* busy_ns, uint64_t* idle_ns, 
  * Per round: push stages inter-host (and future self) events per thread with
  * no lock; self events before the barrier go to a per-host CPU heap (they must
  * be popped in this round, host_single.c:237-267).  The last worker to call
- * next_time flushes the staged events to HBM (k_pins) and reduces the MIN next
- * time on the device (k_pmin).  The first pop of the next round extracts, on
- * the device, every queued event before the new barrier sorted per host in
- * event_compare order (k_pcount / k_pscan / k_pwrite); pops merge that run with
- * the host's CPU heap. */
+ * next_time flushes the staged events into the device calendar (time buckets
+ * of 2^SG_PBUCKET_SHIFT ns, default 2^18; k_cins1 / k_cneed / k_calloc /
+ * k_cins2) and reduces the MIN next time on the device (k_cmin).  The first pop
+ * of the next round extracts, on the device, every queued event before the new
+ * barrier sorted per host in event_compare order, reading only the due buckets
+ * (k_xplan / k_hist / k_mscan / k_part / k_local / k_xfinish); pops merge that
+ * run with the host's CPU heap. */
 typedef struct sg_policy sg_policy;
 
 typedef struct sg_policy_params {
     uint32_t n_threads;   /* worker threads that call push/pop/next_time (nWorkers) */
     uint32_t max_hosts;   /* hosts that will be added */
-    uint32_t queue_cap;   /* initial HBM event slots per host (0 = 64; grows on demand) */
+    uint32_t queue_cap;   /* initial calendar pool, in events per host (0 = 16; grows on demand) */
     int device;           /* HIP device */
 } sg_policy_params;
 

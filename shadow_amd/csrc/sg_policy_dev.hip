@@ -1,23 +1,39 @@
 // sg_policy_dev.hip — device half of the `gpu` SchedulerPolicy (Mode P).
 //
-// Per-host event queues live in HBM (slot-major SoA, as in sg_engine.hip) and
-// carry an opaque 64-bit handle (the Shadow Event*) next to the event_compare
-// key (time, src host id, srcHostEventID; the destination is the queue).
-//   k_pins      staged events → destination queues; overflowing records are
-//               listed so the host can grow the queues and re-deliver them
-//   extraction  three passes over the hosts whose earliest event is before
-//               the barrier (every other host is one 8-byte read):
-//     k_pcount    due events per host, block sums
-//     k_pscan     exclusive scan of the block sums (one workgroup)
-//     k_pwrite    per host: its due events' slots gathered in registers,
-//                 ranked among themselves in event_compare order
-//                 (event.c:110-153), written as one contiguous run at the
-//                 host-ordered offset; the rest compacted in place
-//     The runs are in host order, so off[h + 1] - off[h] is host h's count:
-//     one N + 1 offset array crosses PCIe, no count array.
-//   k_pmin      MIN over the hosts' earliest times (host_single.c:273-305)
+// The queued events of every host live in one HBM calendar: a ring of RB time
+// buckets of width 2^shift ns (bucket b holds times [b << shift, (b + 1) << shift),
+// ring slot b mod RB), each an array of 32-B records spread over fixed-size
+// chunks of a shared pool (a per-bucket chunk table, a stack of free chunks).
+// Events beyond the ring's horizon, or beyond a bucket's capacity, go to a flat
+// "far" list, which is read only when it holds a due event.  So an extraction
+// reads the due buckets and nothing else: its cost follows the events of the
+// round, not the events queued (host_single.c:210-271 pops every event before
+// the barrier, per host in event_compare order).
+//
+//   insert   k_cins1   slots reserved per (workgroup, bucket) through an LDS
+//                      hash (one global atomic per distinct bucket), far
+//                      records appended
+//            k_cneed   chunks the new slots need; the host grows the pool if
+//                      the free stack is short (the one sync of an insert)
+//            k_calloc  chunks popped from the free stack into the tables
+//            k_cins2   records stored, bucket minima
+//   extract  k_xplan   one work item per due chunk (and far piece)
+//            k_hist / k_mscan / k_part   level 1 of a two-level host sort:
+//                      due records partitioned by host block (4096 hosts)
+//                      through per-unit LDS histograms and one scan, no global
+//                      atomics; extracted records of the straddling bucket and
+//                      the far list tombstoned
+//            k_local   level 2, one workgroup per host block: LDS counting
+//                      sort by host, the block's run offsets off[]
+//            k_xrank   each record ranked in its host's run in event_compare
+//                      order (event.c:110-153)
+//            k_xfinish spent buckets reset and their chunks freed; minima of
+//                      the straddling bucket and the far list updated
+//   MIN      k_cmin    over the RB bucket minima and the far minimum
+//                      (host_single.c:273-305)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -29,60 +45,72 @@ namespace {
 
 constexpr int BLOCK = 256;
 constexpr uint64_t SIMTIME_MAX = UINT64_MAX - 1;
+constexpr uint64_t TOMB = UINT64_MAX;  // an extracted record left in place
+constexpr uint32_t CH = 1024;          // records per chunk (32 KB)
+constexpr uint32_t RB = 16384;         // ring buckets
+constexpr uint32_t FAR = 0xFFFFFFFFu;  // rslot: the record went to the far list
+constexpr uint32_t FARBIT = 0x80000000u;
+constexpr uint32_t IPW = 4 * BLOCK;    // records per workgroup in k_cins1 / k_cins2
+constexpr uint32_t HT = 2048;          // k_cins1 LDS hash entries (load <= 1/2)
+constexpr uint32_t XG = 2048;          // grid of the item-driven extraction kernels
+constexpr uint32_t PIECE = BLOCK;      // records per workgroup step of an item
+constexpr uint32_t PPI = CH / PIECE;   // pieces per item
+constexpr uint32_t HB = 12;            // host block = dst >> HB (level 1 of the host sort)
+constexpr uint32_t HPB = 1u << HB;     // hosts per block
+constexpr uint32_t MAXP2 = 4096;       // host blocks: up to 16M hosts
+constexpr uint32_t UI = 4;             // items per level-1 unit (4096 records)
+constexpr uint32_t XU = 512;           // grid of the level-1 kernels
 
-struct Q {
-    uint32_t n, cap;
-    uint64_t* time;
-    uint64_t* seq;
-    uint64_t* handle;
-    uint32_t* src;
-    uint32_t* cnt;
-    uint64_t* hmin;
+struct Scal {
+    uint32_t ftop;                 // chunks on the free stack
+    uint32_t need;                 // chunks the pending insert needs
+    uint32_t nitems;               // work items of the current plan
+    uint32_t farscan;              // the plan includes the far list
+    unsigned long long nfar;       // far records, tombstones included
+    unsigned long long farmin;     // earliest live far time
+    unsigned long long farlive;    // live far records
+    unsigned long long total;      // records of the current extraction
+    unsigned long long smin;       // earliest remaining time of the last due bucket
+    unsigned long long fmin;       // earliest remaining far time (scan)
+    unsigned long long flive;      // remaining far records (scan)
+    unsigned long long pmin[RB / 1024];  // k_cmin's partial minima
+    unsigned long long nall;       // k_call's count
 };
 
-__global__ void k_pinit(Q q) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h < q.n) {
-        q.cnt[h] = 0;
-        q.hmin[h] = SIMTIME_MAX;
+// One cache line per bucket: the insert's atomics on neighbouring buckets do
+// not queue behind each other.
+struct BH {
+    uint32_t cnt;      // slots reserved (beyond cap: those went far)
+    uint32_t chk;      // chunks attached
+    uint64_t min;      // earliest stored time (SIMTIME_MAX: none)
+    uint32_t pad[12];
+};
+
+struct Cal {
+    uint32_t n;        // hosts
+    uint32_t shift;    // bucket = time >> shift
+    uint32_t nchb;     // chunk-table entries per bucket
+    uint32_t cap;      // records per bucket = nchb * CH
+    sgp_rec* pool;     // nchunks * CH records
+    uint32_t* btab;    // [RB][nchb] chunk ids
+    BH* bh;            // [RB]
+    uint32_t* fst;     // free chunk stack
+    sgp_rec* far;      // far list
+    uint4* items;      // plan: {chunk id | FARBIT piece, records, ring slot, last-bucket flag}
+    Scal* sc;
+};
+
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
     }
+    return v;
 }
 
-__global__ void k_pins(Q q, const sgp_rec* r, uint64_t n, uint32_t* fail, uint32_t* nfail) {
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
-        const sgp_rec e = r[i];
-        const uint32_t slot = atomicAdd(&q.cnt[e.dst], 1u);
-        if (slot >= q.cap) {
-            fail[atomicAdd(nfail, 1u)] = (uint32_t)i;
-            continue;
-        }
-        const size_t k = (size_t)slot * q.n + e.dst;
-        q.time[k] = e.time;
-        q.seq[k] = e.seq;
-        q.handle[k] = e.handle;
-        q.src[k] = e.src_id;
-        atomicMin((unsigned long long*)&q.hmin[e.dst], (unsigned long long)e.time);
-    }
-}
-
-__global__ void k_pclamp(Q q, uint32_t oldcap) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h < q.n && q.cnt[h] > oldcap) q.cnt[h] = oldcap;
-}
-
-__global__ void k_pcopy(Q to, Q from) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h >= from.n) return;
-    const uint32_t c = from.cnt[h];
-    for (uint32_t j = 0; j < c; ++j) {
-        const size_t a = (size_t)j * from.n + h, b = (size_t)j * to.n + h;
-        to.time[b] = from.time[a];
-        to.seq[b] = from.seq[a];
-        to.handle[b] = from.handle[a];
-        to.src[b] = from.src[a];
-    }
-    to.cnt[h] = c;
-    to.hmin[h] = from.hmin[h];
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 __device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uint64_t bt, uint32_t bs,
@@ -91,188 +119,487 @@ __device__ __forceinline__ bool key_less(uint64_t t, uint32_t s, uint64_t q, uin
     return (t < bt) | ((t == bt) & ((s < bs) | ((s == bs) & (q < bq))));
 }
 
-// Due events of host h (time < barrier) and the earliest time after it.
-__global__ __launch_bounds__(BLOCK) void k_pcount(Q q, uint64_t barrier, uint32_t* kcnt, uint32_t* bsum) {
-    __shared__ uint32_t s_w[BLOCK / 64];
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t k = 0;
-    if (h < q.n && q.hmin[h] < barrier) {
-        const uint32_t c = q.cnt[h];
-        for (uint32_t j = 0; j < c; ++j) k += q.time[(size_t)j * q.n + h] < barrier;
+__global__ void k_cinit(Cal c, uint32_t nchunks) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < RB) {
+        c.bh[i].cnt = 0;
+        c.bh[i].chk = 0;
+        c.bh[i].min = SIMTIME_MAX;
     }
-    if (h < q.n) kcnt[h] = k;
-    uint32_t w = k;
-    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = w;
+    if (i < nchunks) c.fst[i] = i;
+}
+
+// Free-stack entries [at, at + k) = chunk ids first.. (a grown pool's new chunks)
+__global__ void k_fpush(uint32_t* fst, uint32_t at, uint32_t first, uint32_t k) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < k) fst[at + i] = first + i;
+}
+
+// Slots for up to IPW staged records per workgroup: an LDS hash groups them by
+// bucket so each distinct bucket costs one global atomic.  Records outside the
+// ring [cur, cur + RB) or past their bucket's capacity are appended to the far
+// list (the host sized it for every record of this insert).
+__global__ __launch_bounds__(BLOCK) void k_cins1(Cal c, uint64_t cur, const sgp_rec* in, uint64_t n,
+                                                 uint32_t* rslot) {
+    __shared__ unsigned long long s_key[HT];  // bucket + 1, 0 = empty
+    __shared__ uint32_t s_cnt[HT];
+    __shared__ uint32_t s_base[HT];
+    __shared__ unsigned long long s_min[HT];
+    __shared__ uint32_t s_nfar;
+    __shared__ unsigned long long s_fbase, s_fmin;
+    for (uint32_t e = threadIdx.x; e < HT; e += BLOCK) {
+        s_key[e] = 0;
+        s_cnt[e] = 0;
+        s_min[e] = SIMTIME_MAX;
+    }
+    if (threadIdx.x == 0) {
+        s_nfar = 0;
+        s_fmin = SIMTIME_MAX;
+    }
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)blockIdx.x * IPW;
+    uint32_t ent[4], loc[4];
+    uint64_t tim[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = i0 + q * BLOCK + threadIdx.x;
+        ent[q] = FAR;
+        tim[q] = 0;
+        if (i >= n) continue;
+        const uint64_t t = in[i].time;
+        tim[q] = t;
+        const uint64_t b = t >> c.shift;
+        if (b < cur || b >= cur + RB) continue;
+        uint32_t h = (uint32_t)((b * 0x9E3779B97F4A7C15ull) >> 53) & (HT - 1);
+        for (;;) {
+            const unsigned long long old = atomicCAS(&s_key[h], 0ull, (unsigned long long)(b + 1));
+            if (old == 0 || old == b + 1) break;
+            h = (h + 1) & (HT - 1);
+        }
+        ent[q] = h;
+        loc[q] = atomicAdd(&s_cnt[h], 1u);
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < HT; e += BLOCK)
+        if (s_key[e]) s_base[e] = atomicAdd(&c.bh[(uint32_t)(s_key[e] - 1) & (RB - 1)].cnt, s_cnt[e]);
+    __syncthreads();
+    uint32_t fl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = i0 + q * BLOCK + threadIdx.x;
+        fl[q] = 0;
+        if (i >= n) continue;
+        uint32_t slot = ent[q] == FAR ? FAR : s_base[ent[q]] + loc[q];
+        if (slot != FAR && slot >= c.cap) slot = FAR;
+        rslot[i] = slot;
+        if (slot == FAR) {
+            fl[q] = atomicAdd(&s_nfar, 1u) + 1;
+            atomicMin(&s_fmin, (unsigned long long)tim[q]);
+        } else {
+            atomicMin(&s_min[ent[q]], (unsigned long long)tim[q]);  // stored in the bucket
+        }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < HT; e += BLOCK)
+        if (s_key[e] && s_min[e] != SIMTIME_MAX)
+            atomicMin((unsigned long long*)&c.bh[(uint32_t)(s_key[e] - 1) & (RB - 1)].min, s_min[e]);
+    if (threadIdx.x == 0 && s_nfar) {
+        s_fbase = atomicAdd(&c.sc->nfar, (unsigned long long)s_nfar);
+        atomicAdd(&c.sc->farlive, (unsigned long long)s_nfar);
+        atomicMin(&c.sc->farmin, s_fmin);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (!fl[q]) continue;
+        const uint64_t i = i0 + q * BLOCK + threadIdx.x;
+        c.far[s_fbase + fl[q] - 1] = in[i];
+    }
+}
+
+__device__ __forceinline__ uint32_t chunks_for(uint32_t cnt, uint32_t cap) {
+    const uint32_t m = cnt < cap ? cnt : cap;
+    return (m + CH - 1) / CH;
+}
+
+__global__ void k_cneed(Cal c) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t k = 0;
+    if (s < RB) k = chunks_for(c.bh[s].cnt, c.cap) - c.bh[s].chk;
+    k = wave_sum(k);
+    if ((threadIdx.x & 63) == 0 && k) atomicAdd(&c.sc->need, (uint32_t)k);
+}
+
+__global__ void k_calloc(Cal c) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= RB) return;
+    const uint32_t have = c.bh[s].chk, want = chunks_for(c.bh[s].cnt, c.cap);
+    if (want <= have) return;
+    const uint32_t k = want - have;
+    const uint32_t top = atomicSub(&c.sc->ftop, k);  // the host made sure top >= k
+    for (uint32_t j = 0; j < k; ++j) c.btab[(size_t)s * c.nchb + have + j] = c.fst[top - k + j];
+    c.bh[s].chk = want;
+}
+
+// Store the bucket records (their minima were taken in k_cins1).
+__global__ __launch_bounds__(BLOCK) void k_cins2(Cal c, const sgp_rec* in, uint64_t n, const uint32_t* rslot) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * IPW;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = i0 + q * BLOCK + threadIdx.x;
+        const uint32_t slot = i < n ? rslot[i] : FAR;
+        if (slot == FAR) continue;
+        const sgp_rec r = in[i];
+        const uint32_t s = (uint32_t)(r.time >> c.shift) & (RB - 1);
+        const uint32_t ch = c.btab[(size_t)s * c.nchb + slot / CH];
+        c.pool[(size_t)ch * CH + slot % CH] = r;
+    }
+}
+
+// Work items for the due buckets [cur, cur + nbk) (ring order) and, when it
+// holds a due event (or `all`), the far list.  One workgroup: a scan of the
+// buckets' chunk counts, then the items written in parallel (each finds its
+// bucket by binary search over the prefix).
+__global__ __launch_bounds__(1024) void k_xplan(Cal c, uint64_t cur, uint32_t nbk, uint64_t barrier, int all) {
+    __shared__ uint32_t s_sum[1024];
+    __shared__ uint32_t s_pre[RB + 1];
+    constexpr uint32_t PER = RB / 1024;
+    const uint32_t t = threadIdx.x;
+    uint32_t nch[PER], tot = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t k = t * PER + j;
+        nch[j] = k < nbk ? chunks_for(c.bh[(uint32_t)(cur + k) & (RB - 1)].cnt, c.cap) : 0;
+        tot += nch[j];
+    }
+    s_sum[t] = tot;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t u = t >= o ? s_sum[t - o] : 0;
+        __syncthreads();
+        s_sum[t] += u;
+        __syncthreads();
+    }
+    uint32_t at = s_sum[t] - tot;
+    const uint32_t nbucket_items = s_sum[1023];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        s_pre[t * PER + j] = at;
+        at += nch[j];
+    }
+    __syncthreads();
+    const uint32_t nb = nbk ? nbk : 1;
+    for (uint32_t q = t; q < nbucket_items; q += 1024) {
+        uint32_t lo = 0, hi = nb - 1;  // last k with s_pre[k] <= q
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= q) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t s = (uint32_t)(cur + lo) & (RB - 1), x = q - s_pre[lo];
+        const uint32_t m = c.bh[s].cnt < c.cap ? c.bh[s].cnt : c.cap;
+        c.items[q] = make_uint4(c.btab[(size_t)s * c.nchb + x], m - x * CH < CH ? m - x * CH : CH, s, lo + 1 == nbk);
+    }
+    const unsigned long long nfar = c.sc->nfar;
+    const bool farscan = nfar && (all || c.sc->farmin < barrier);
+    const uint32_t nfi = farscan ? (uint32_t)((nfar + CH - 1) / CH) : 0;
+    for (uint32_t q = t; q < nfi; q += 1024)
+        c.items[nbucket_items + q] =
+            make_uint4(FARBIT | q, q + 1 < nfi ? CH : (uint32_t)(nfar - (uint64_t)q * CH), RB, 0);
+    if (t == 0) {
+        c.sc->nitems = nbucket_items + nfi;
+        c.sc->farscan = farscan;
+        c.sc->smin = SIMTIME_MAX;
+        c.sc->fmin = SIMTIME_MAX;
+        c.sc->flive = 0;
+    }
+}
+
+__device__ __forceinline__ const sgp_rec* item_base(const Cal& c, uint4 it) {
+    return it.x & FARBIT ? c.far + (size_t)(it.x & ~FARBIT) * CH : c.pool + (size_t)it.x * CH;
+}
+
+// Exclusive scan across a 1024-thread workgroup (16 waves); *total = the sum.
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* s_w, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t k = 0; k < 16; ++k) {
+        before += k < w ? s_w[k] : 0;
+        all += s_w[k];
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+// Level 1 of the host sort: per unit of UI items (UI * CH records), due events
+// per host block (HB bits: dst >> HB) into a block-major count matrix
+// mat[d * nu + u]; the times that stay give the straddling bucket's and the
+// far list's new minima.
+__global__ __launch_bounds__(1024) void k_hist(Cal c, uint64_t barrier, uint32_t P2, uint32_t* mat) {
+    __shared__ uint32_t s_h[MAXP2];
+    const uint32_t t = threadIdx.x, ni = c.sc->nitems, nu = (ni + UI - 1) / UI;
+    uint64_t smin = SIMTIME_MAX, fmin = SIMTIME_MAX, flive = 0;
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        for (uint32_t d = t; d < P2; d += 1024) s_h[d] = 0;
+        uint64_t tm[UI];
+        uint32_t dst[UI];
+        bool far[UI];
+#pragma unroll
+        for (uint32_t k = 0; k < UI; ++k) {  // every load first, then the bins
+            const uint32_t j = u * UI + k;
+            const uint4 it = j < ni ? c.items[j] : make_uint4(0, 0, 0, 0);
+            far[k] = it.x & FARBIT;
+            tm[k] = TOMB;
+            dst[k] = 0;
+            if (t < it.y) {
+                const sgp_rec* r = item_base(c, it) + t;
+                tm[k] = r->time;
+                dst[k] = r->dst;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < UI; ++k) {
+            if (tm[k] < barrier) {
+                atomicAdd(&s_h[dst[k] >> HB], 1u);
+            } else if (tm[k] != TOMB) {
+                if (far[k]) {
+                    fmin = tm[k] < fmin ? tm[k] : fmin;
+                    ++flive;
+                } else {
+                    smin = tm[k] < smin ? tm[k] : smin;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t d = t; d < P2; d += 1024) mat[d * nu + u] = s_h[d];
+        __syncthreads();
+    }
+    smin = wave_min(smin);
+    fmin = wave_min(fmin);
+    flive = wave_sum(flive);
+    if ((t & 63) == 0) {
+        if (smin != SIMTIME_MAX) atomicMin(&c.sc->smin, (unsigned long long)smin);
+        if (fmin != SIMTIME_MAX) atomicMin(&c.sc->fmin, (unsigned long long)fmin);
+        if (flive) atomicAdd(&c.sc->flive, (unsigned long long)flive);
+    }
+}
+
+// The count matrix scanned in place (it is block-major, so in (block, unit)
+// order): mat[d * nu + u] becomes where unit u's events of host block d start;
+// pbase[d] = host block d's start.  One workgroup; tiles of 16K entries are
+// staged through LDS so global loads and stores stay coalesced.
+__global__ __launch_bounds__(1024) void k_mscan(uint32_t* mat, uint32_t P2, const Cal c, uint32_t* pbase) {
+    constexpr uint32_t V = 16, TILE = 1024 * V;
+    __shared__ uint32_t s_buf[TILE];
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x;
+    const uint32_t nu = (c.sc->nitems + UI - 1) / UI;
+    const uint32_t E = nu * P2;
+    uint32_t carry = 0;
+    for (uint32_t x0 = 0; x0 < E; x0 += TILE) {
+#pragma unroll
+        for (uint32_t k = 0; k < V; ++k) {
+            const uint32_t x = x0 + k * 1024 + t;
+            s_buf[k * 1024 + t] = x < E ? mat[x] : 0;
+        }
+        __syncthreads();
+        uint32_t v[V], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < V; ++k) {
+            v[k] = s_buf[t * V + k];
+            sum += v[k];
+        }
+        uint32_t tot;
+        uint32_t at = carry + block_excl(sum, s_w, &tot);  // (its barriers order the reads above)
+#pragma unroll
+        for (uint32_t k = 0; k < V; ++k) {
+            s_buf[t * V + k] = at;
+            at += v[k];
+        }
+        carry += tot;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < V; ++k) {
+            const uint32_t x = x0 + k * 1024 + t;
+            if (x < E) {
+                mat[x] = s_buf[k * 1024 + t];
+                if (x % nu == 0) pbase[x / nu] = s_buf[k * 1024 + t];
+            }
+        }
+        __syncthreads();
+    }
+    if (nu == 0)
+        for (uint32_t d = t; d < P2; d += 1024) pbase[d] = 0;
+    if (t == 0) {
+        pbase[P2] = carry;
+        c.sc->total = carry;
+    }
+}
+
+// Level 1 scatter: each unit's due events to their host block's range;
+// extracted records that stay in place (last due bucket, far list) tombstoned.
+__global__ __launch_bounds__(1024) void k_part(Cal c, uint64_t barrier, uint32_t P2, const uint32_t* mat,
+                                               sgp_rec* tmp) {
+    __shared__ uint32_t s_c[MAXP2];
+    const uint32_t t = threadIdx.x, ni = c.sc->nitems, nu = (ni + UI - 1) / UI;
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        for (uint32_t d = t; d < P2; d += 1024) s_c[d] = mat[d * nu + u];
+        sgp_rec e[UI];
+        sgp_rec* r[UI];
+        bool keep[UI];
+#pragma unroll
+        for (uint32_t k = 0; k < UI; ++k) {
+            const uint32_t j = u * UI + k;
+            const uint4 it = j < ni ? c.items[j] : make_uint4(0, 0, 0, 0);
+            keep[k] = (it.x & FARBIT) || it.w;  // records that stay must be told apart
+            r[k] = const_cast<sgp_rec*>(item_base(c, it)) + t;
+            e[k].time = TOMB;
+            if (t < it.y) e[k] = *r[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < UI; ++k) {
+            if (e[k].time >= barrier) continue;
+            tmp[atomicAdd(&s_c[e[k].dst >> HB], 1u)] = e[k];
+            if (keep[k]) r[k]->time = TOMB;
+        }
+        __syncthreads();
+    }
+}
+
+// Level 2, one workgroup per host block: an LDS counting sort by host writes
+// the block's run offsets off[] and its events in host order.
+__global__ __launch_bounds__(1024) void k_local(uint32_t n, uint32_t P2, const uint32_t* pbase, const sgp_rec* tmp,
+                                                sgp_rec* tmp2, uint32_t* off) {
+    __shared__ uint32_t s_c[HPB];
+    __shared__ uint32_t s_w[16];
+    const uint32_t t = threadIdx.x, p = blockIdx.x, h0 = p << HB;
+    const uint32_t pb = pbase[p], pe = pbase[p + 1];
+    const uint32_t nh = n - h0 < HPB ? n - h0 : HPB;
+    for (uint32_t j = t; j < HPB; j += 1024) s_c[j] = 0;
+    __syncthreads();
+    for (uint32_t i = pb + t; i < pe; i += 1024) atomicAdd(&s_c[tmp[i].dst - h0], 1u);
+    __syncthreads();
+    constexpr uint32_t PT = HPB / 1024;
+    uint32_t v[PT], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+        v[k] = s_c[t * PT + k];
+        sum += v[k];
+    }
+    uint32_t tot;
+    uint32_t at = pb + block_excl(sum, s_w, &tot);
+#pragma unroll
+    for (uint32_t k = 0; k < PT; ++k) {
+        if (t * PT + k < nh) off[h0 + t * PT + k] = at;
+        s_c[t * PT + k] = at;  // the scatter cursor
+        at += v[k];
+    }
+    if (p + 1 == P2 && t == 0) off[n] = pe;
+    __syncthreads();
+    for (uint32_t i = pb + t; i < pe; i += 1024) {
+        const sgp_rec e = tmp[i];
+        tmp2[atomicAdd(&s_c[e.dst - h0], 1u)] = e;
+    }
+}
+
+// Each extracted event ranked inside its host's run in event_compare order
+// (event.c:110-153; the keys are unique, srcHostEventID being unique per source).
+__global__ __launch_bounds__(BLOCK) void k_xrank(const sgp_rec* tmp2, const uint32_t* off,
+                                                 const unsigned long long* total, sgp_rec* out) {
+    const uint64_t T = *total;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < T; i += (uint64_t)gridDim.x * BLOCK) {
+        const sgp_rec e = tmp2[i];
+        const uint32_t s = off[e.dst], f = off[e.dst + 1];
+        uint32_t rank = 0;
+        for (uint32_t j = s; j < f; ++j)
+            rank += key_less(tmp2[j].time, tmp2[j].src_id, tmp2[j].seq, e.time, e.src_id, e.seq);
+        out[s + rank] = e;
+    }
+}
+
+// Spent buckets back to the free stack (one workgroup per due bucket); the
+// straddling bucket and the far list get their new minima.
+__global__ __launch_bounds__(BLOCK) void k_xfinish(Cal c, uint64_t cur, uint32_t nbk) {
+    __shared__ uint32_t s_at;
+    const uint32_t k = blockIdx.x;
+    if (k == 0 && threadIdx.x == 0 && c.sc->farscan) {
+        c.sc->farmin = c.sc->fmin;
+        c.sc->farlive = c.sc->flive;
+    }
+    if (k >= nbk) return;
+    const uint32_t s = (uint32_t)(cur + k) & (RB - 1);
+    const uint64_t smin = c.sc->smin;
+    if (k + 1 == nbk && smin != SIMTIME_MAX) {  // events remain in the last due bucket
+        if (threadIdx.x == 0) c.bh[s].min = smin;
+        return;
+    }
+    const uint32_t m = c.bh[s].chk;
+    if (threadIdx.x == 0) {
+        s_at = m ? atomicAdd(&c.sc->ftop, m) : 0;
+        c.bh[s].cnt = 0;
+        c.bh[s].chk = 0;
+        c.bh[s].min = SIMTIME_MAX;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < m; j += BLOCK) c.fst[s_at + j] = c.btab[(size_t)s * c.nchb + j];
+}
+
+// MIN over the bucket minima: RB / 1024 workgroups, one partial each (the host
+// takes the minimum of the partials and the far list's).
+__global__ __launch_bounds__(1024) void k_cmin(Cal c) {
+    __shared__ uint64_t s_m[16];
+    const uint64_t x = c.bh[blockIdx.x * 1024 + threadIdx.x].min;
+    const uint64_t m = wave_min(x);
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int i = 0; i < BLOCK / 64; ++i) t += s_w[i];
-        bsum[blockIdx.x] = t;
+        uint64_t r = SIMTIME_MAX;
+        for (int i = 0; i < 16; ++i) r = s_m[i] < r ? s_m[i] : r;
+        c.sc->pmin[blockIdx.x] = r;
     }
 }
 
-// Exclusive scan of nb block sums in place (one workgroup of 1024), total out.
-__global__ __launch_bounds__(1024) void k_pscan(uint32_t* bsum, uint32_t nb, unsigned long long* total) {
-    __shared__ uint32_t s[1024];
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t v = i < nb ? bsum[i] : 0;
-        s[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const uint32_t u = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
-            __syncthreads();
-            s[threadIdx.x] += u;
-            __syncthreads();
-        }
-        if (i < nb) bsum[i] = carry + s[threadIdx.x] - v;
-        carry += s[1023];
-        __syncthreads();
+__global__ __launch_bounds__(BLOCK) void k_call(Cal c, sgp_rec* out, uint64_t cap) {
+    const uint32_t np = c.sc->nitems * PPI;
+    for (uint32_t j = blockIdx.x; j < np; j += gridDim.x) {  // uniform per workgroup
+        const uint4 it = c.items[j / PPI];
+        const sgp_rec* r = item_base(c, it);
+        const uint32_t i = (j % PPI) * PIECE + threadIdx.x;
+        sgp_rec e{};
+        e.time = TOMB;
+        if (i < it.y) e = r[i];
+        const bool live = e.time != TOMB;
+        const uint64_t m = __ballot(live);
+        unsigned long long base = 0;
+        const int lane = threadIdx.x & 63;
+        if (lane == 0 && m) base = atomicAdd(&c.sc->nall, (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        const unsigned long long p = base + __popcll(m & ((1ull << lane) - 1));
+        if (live && p < cap) out[p] = e;
     }
-    if (threadIdx.x == 0) *total = carry;
 }
 
-constexpr uint32_t KREG = 8;  // due events a lane ranks in registers; more take the slow path
-
-__global__ __launch_bounds__(BLOCK) void k_pwrite(Q q, uint64_t barrier, const uint32_t* kcnt,
-                                                  const uint32_t* boff, sgp_rec* out, uint32_t* off) {
-    __shared__ uint32_t s[BLOCK];
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    const size_t N = q.n;
-    const uint32_t k = h < q.n ? kcnt[h] : 0;
-    s[threadIdx.x] = k;
-    __syncthreads();
-    for (int o = 1; o < BLOCK; o <<= 1) {
-        const uint32_t u = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
-        __syncthreads();
-        s[threadIdx.x] += u;
-        __syncthreads();
+// Far list without its tombstones, into `to` (order does not matter: runs are
+// ranked by key).
+__global__ void k_fcompact(const sgp_rec* from, uint64_t n, sgp_rec* to, unsigned long long* count) {
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        const sgp_rec e = from[i];
+        if (e.time != TOMB) to[atomicAdd(count, 1ull)] = e;
     }
-    const uint32_t base = boff[blockIdx.x] + s[threadIdx.x] - k;
-    if (h < q.n) off[h] = base;
-    if (h + 1 == q.n) off[q.n] = base + k;
-    if (k == 0) return;
-    const uint32_t c = q.cnt[h];
-    // the due slots, in registers (the host's times are read once)
-    uint32_t idx[KREG] = {};
-    uint64_t tt[KREG] = {};
-    uint32_t nd = 0;
-    uint64_t rest = SIMTIME_MAX;
-    for (uint32_t j = 0; j < c; ++j) {
-        const uint64_t t = q.time[(size_t)j * N + h];
-        if (t < barrier) {
-#pragma unroll
-            for (uint32_t a = 0; a < KREG; ++a) {  // selects, so the arrays stay in registers
-                const bool w = a == nd;
-                idx[a] = w ? j : idx[a];
-                tt[a] = w ? t : tt[a];
-            }
-            ++nd;
-        } else if (t < rest) {
-            rest = t;
-        }
-    }
-    if (nd <= KREG) {
-        uint32_t ss[KREG];
-        uint64_t sq[KREG];
-#pragma unroll
-        for (uint32_t a = 0; a < KREG; ++a) {
-            if (a >= nd) break;
-            const size_t ka = (size_t)idx[a] * N + h;
-            ss[a] = q.src[ka];
-            sq[a] = q.seq[ka];
-        }
-#pragma unroll
-        for (uint32_t a = 0; a < KREG; ++a) {
-            if (a >= nd) break;
-            uint32_t rank = 0;
-#pragma unroll
-            for (uint32_t b = 0; b < KREG; ++b) {
-                if (b >= nd) break;
-                rank += key_less(tt[b], ss[b], sq[b], tt[a], ss[a], sq[a]);
-            }
-            sgp_rec r;
-            r.time = tt[a];
-            r.seq = sq[a];
-            r.handle = q.handle[(size_t)idx[a] * N + h];
-            r.src_id = ss[a];
-            r.dst = h;
-            out[base + rank] = r;
-        }
-    } else {
-        // many due events at one host: rank each among the due ones from memory
-        for (uint32_t i = 0; i < c; ++i) {
-            const size_t ki = (size_t)i * N + h;
-            const uint64_t ti = q.time[ki];
-            if (ti >= barrier) continue;
-            const uint32_t si = q.src[ki];
-            const uint64_t qi = q.seq[ki];
-            uint32_t rank = 0;
-            for (uint32_t j = 0; j < c; ++j) {
-                const size_t kj = (size_t)j * N + h;
-                const uint64_t tj = q.time[kj];
-                if (tj < barrier && key_less(tj, q.src[kj], q.seq[kj], ti, si, qi)) ++rank;
-            }
-            sgp_rec r;
-            r.time = ti;
-            r.seq = qi;
-            r.handle = q.handle[ki];
-            r.src_id = si;
-            r.dst = h;
-            out[base + rank] = r;
-        }
-    }
-    // compact the events after the barrier to the front
-    uint32_t w = 0;
-    for (uint32_t j = 0; j < c; ++j) {
-        const size_t kj = (size_t)j * N + h;
-        const uint64_t t = q.time[kj];
-        if (t < barrier) continue;
-        if (w != j) {
-            const size_t kw = (size_t)w * N + h;
-            q.time[kw] = t;
-            q.seq[kw] = q.seq[kj];
-            q.handle[kw] = q.handle[kj];
-            q.src[kw] = q.src[kj];
-        }
-        ++w;
-    }
-    q.cnt[h] = w;
-    q.hmin[h] = rest;
 }
 
-__global__ void k_pmin(Q q, unsigned long long* out) {
-    uint64_t m = SIMTIME_MAX;
-    for (uint32_t h = blockIdx.x * BLOCK + threadIdx.x; h < q.n; h += gridDim.x * BLOCK) {
-        const uint64_t x = q.hmin[h];
-        m = x < m ? x : m;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(m, o, 64);
-        m = w < m ? w : m;
-    }
-    if ((threadIdx.x & 63) == 0) atomicMin(out, (unsigned long long)m);
-}
-
-__global__ void k_pall(Q q, sgp_rec* out, uint64_t cap, unsigned long long* n) {
-    const uint32_t h = blockIdx.x * BLOCK + threadIdx.x;
-    if (h >= q.n) return;
-    const uint32_t c = q.cnt[h];
-    for (uint32_t j = 0; j < c; ++j) {
-        const size_t k = (size_t)j * q.n + h;
-        const unsigned long long i = atomicAdd(n, 1ULL);
-        if (i < cap) {
-            sgp_rec r;
-            r.time = q.time[k];
-            r.seq = q.seq[k];
-            r.handle = q.handle[k];
-            r.src_id = q.src[k];
-            r.dst = h;
-            out[i] = r;
-        }
-    }
+uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
 }
 
 }  // namespace
@@ -280,22 +607,29 @@ __global__ void k_pall(Q q, sgp_rec* out, uint64_t cap, unsigned long long* n) {
 struct sgp_dev {
     int device;
     hipStream_t s;
-    Q q;
-    std::vector<void*> qallocs;
-    sgp_rec* d_in;      // staged records
+    Cal c;
+    Scal* h_sc;          // pinned mirror of the device scalars
+    uint64_t cur;        // lowest bucket that may hold a live event
+    uint32_t nchunks;    // pool chunks
+    uint64_t farcap;     // far list capacity (records)
+    sgp_rec* far2;       // compaction target
+    uint64_t items_cap;
+    sgp_rec* d_in;       // staged records
+    uint32_t* d_rslot;
     uint64_t in_cap;
-    uint32_t* d_fail;
-    uint32_t* d_nfail;
-    sgp_rec* d_out;     // extracted runs
+    sgp_rec* d_tmp;      // extracted, by host block
+    sgp_rec* d_tmp2;     // extracted, by host
+    sgp_rec* d_out;      // extracted runs, ranked
     uint64_t out_cap;
     uint32_t* d_off;     // [N + 1] host-ordered run offsets
-    uint32_t* d_cnt;     // [N] due events per host
-    uint32_t* d_bsum;    // [N / BLOCK] block sums, scanned in place
-    unsigned long long* d_scalar;
-    sgp_rec* h_runs;    // pinned
-    uint64_t h_runs_cap;
+    uint32_t P2;         // host blocks
+    uint32_t* d_mat;     // [units][P2] level-1 counts, then bases
+    uint64_t mat_cap;    // units
+    uint32_t* d_pbase;   // [P2 + 1] host block starts
+    sgp_rec* h_runs;     // pinned
     uint32_t* h_off;
-    uint64_t queued;    // events in HBM
+    uint64_t queued;     // events in HBM
+    uint64_t far_compact;  // far records before a tombstone-heavy list is compacted
 };
 
 #define PCHK(x)                                                                         \
@@ -307,28 +641,84 @@ struct sgp_dev {
         }                                                                               \
     } while (0)
 
-static int alloc_q(sgp_dev* d, Q* q, uint32_t n, uint32_t cap, std::vector<void*>& keep) {
-    const size_t S = (size_t)n * cap;
-    q->n = n;
-    q->cap = cap;
-    void* p[6] = {};
-    size_t sz[6] = {S * 8, S * 8, S * 8, S * 4, (size_t)n * 4, (size_t)n * 8};
-    for (int i = 0; i < 6; ++i) {
-        if (hipMalloc(&p[i], sz[i] ? sz[i] : 8) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipFree(p[j]);
-            sg_set_error("sgp: hipMalloc of %zu bytes failed", sz[i]);
-            return 2;
-        }
-        keep.push_back(p[i]);
+static int dmalloc(void** p, size_t bytes) {
+    if (hipMalloc(p, bytes ? bytes : 8) != hipSuccess) {
+        *p = nullptr;
+        sg_set_error("sgp: hipMalloc of %zu bytes failed", bytes);
+        return 2;
     }
-    q->time = (uint64_t*)p[0];
-    q->seq = (uint64_t*)p[1];
-    q->handle = (uint64_t*)p[2];
-    q->src = (uint32_t*)p[3];
-    q->cnt = (uint32_t*)p[4];
-    q->hmin = (uint64_t*)p[5];
-    (void)d;
     return 0;
+}
+
+// items: every chunk of the pool plus every far piece, once
+static int fit_items(sgp_dev* d) {
+    const uint64_t need = (uint64_t)d->nchunks + (d->farcap + CH - 1) / CH + 1;
+    if (need <= d->items_cap) return 0;
+    if (d->c.items) (void)hipFree(d->c.items);
+    int rc = dmalloc((void**)&d->c.items, need * sizeof(uint4));
+    if (rc) return rc;
+    d->items_cap = need;
+    const uint64_t units = (need + UI - 1) / UI;
+    if (d->d_mat) (void)hipFree(d->d_mat);
+    d->d_mat = nullptr;
+    if ((rc = dmalloc((void**)&d->d_mat, units * d->P2 * 4))) return rc;
+    d->mat_cap = units;
+    return 0;
+}
+
+static int grow_far(sgp_dev* d, uint64_t n) {
+    if (n <= d->farcap) return 0;
+    uint64_t c = d->farcap ? d->farcap : 4096;
+    while (c < n) c *= 2;
+    sgp_rec *a = nullptr, *b = nullptr;
+    int rc = dmalloc((void**)&a, c * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&b, c * sizeof(sgp_rec));
+    if (rc) {
+        if (a) (void)hipFree(a);
+        return rc;
+    }
+    if (d->h_sc->nfar) PCHK(hipMemcpyAsync(a, d->c.far, d->h_sc->nfar * sizeof(sgp_rec), hipMemcpyDeviceToDevice, d->s));
+    PCHK(hipStreamSynchronize(d->s));
+    if (d->c.far) (void)hipFree(d->c.far);
+    if (d->far2) (void)hipFree(d->far2);
+    d->c.far = a;
+    d->far2 = b;
+    d->farcap = c;
+    return fit_items(d);
+}
+
+// Pool of at least `want` chunks; live chunks keep their ids.
+static int grow_pool(sgp_dev* d, uint32_t want) {
+    if (want <= d->nchunks) return 0;
+    uint64_t nc = (uint64_t)d->nchunks * 2;
+    if (nc < want) nc = want;
+    if (nc > 0x7FFFFFFFull) {
+        sg_set_error("sgp: chunk pool over 2^31 chunks");
+        return 2;
+    }
+    sgp_rec* pool = nullptr;
+    uint32_t* fst = nullptr;
+    int rc = dmalloc((void**)&pool, nc * CH * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&fst, nc * 4);
+    if (rc) {
+        if (pool) (void)hipFree(pool);
+        return rc;
+    }
+    const uint32_t top = d->h_sc->ftop, add = (uint32_t)nc - d->nchunks;
+    PCHK(hipMemcpyAsync(pool, d->c.pool, (size_t)d->nchunks * CH * sizeof(sgp_rec), hipMemcpyDeviceToDevice, d->s));
+    if (top) PCHK(hipMemcpyAsync(fst, d->c.fst, (size_t)top * 4, hipMemcpyDeviceToDevice, d->s));
+    hipLaunchKernelGGL(k_fpush, dim3((add + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, fst, top, d->nchunks, add);
+    PCHK(hipGetLastError());
+    const uint32_t ntop = top + add;
+    PCHK(hipMemcpyAsync(&d->c.sc->ftop, &ntop, 4, hipMemcpyHostToDevice, d->s));
+    PCHK(hipStreamSynchronize(d->s));
+    (void)hipFree(d->c.pool);
+    (void)hipFree(d->c.fst);
+    d->c.pool = pool;
+    d->c.fst = fst;
+    d->nchunks = (uint32_t)nc;
+    d->h_sc->ftop = ntop;
+    return fit_items(d);
 }
 
 static int grow_in(sgp_dev* d, uint64_t n) {
@@ -336,11 +726,12 @@ static int grow_in(sgp_dev* d, uint64_t n) {
     uint64_t c = d->in_cap ? d->in_cap : 4096;
     while (c < n) c *= 2;
     if (d->d_in) (void)hipFree(d->d_in);
-    if (d->d_fail) (void)hipFree(d->d_fail);
+    if (d->d_rslot) (void)hipFree(d->d_rslot);
     d->d_in = nullptr;
-    d->d_fail = nullptr;
-    PCHK(hipMalloc(&d->d_in, c * sizeof(sgp_rec)));
-    PCHK(hipMalloc(&d->d_fail, c * sizeof(uint32_t)));
+    d->d_rslot = nullptr;
+    int rc = dmalloc((void**)&d->d_in, c * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&d->d_rslot, c * 4);
+    if (rc) return rc;
     d->in_cap = c;
     return 0;
 }
@@ -350,12 +741,25 @@ static int grow_out(sgp_dev* d, uint64_t n) {
     uint64_t c = d->out_cap ? d->out_cap : 4096;
     while (c < n) c *= 2;
     if (d->d_out) (void)hipFree(d->d_out);
+    if (d->d_tmp) (void)hipFree(d->d_tmp);
+    if (d->d_tmp2) (void)hipFree(d->d_tmp2);
     if (d->h_runs) (void)hipHostFree(d->h_runs);
     d->d_out = nullptr;
+    d->d_tmp = nullptr;
+    d->d_tmp2 = nullptr;
     d->h_runs = nullptr;
-    PCHK(hipMalloc(&d->d_out, c * sizeof(sgp_rec)));
+    int rc = dmalloc((void**)&d->d_out, c * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&d->d_tmp, c * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&d->d_tmp2, c * sizeof(sgp_rec));
+    if (rc) return rc;
     PCHK(hipHostMalloc((void**)&d->h_runs, c * sizeof(sgp_rec), hipHostMallocDefault));
     d->out_cap = c;
+    return 0;
+}
+
+static int read_scal(sgp_dev* d) {
+    PCHK(hipMemcpyAsync(d->h_sc, d->c.sc, sizeof(Scal), hipMemcpyDeviceToHost, d->s));
+    PCHK(hipStreamSynchronize(d->s));
     return 0;
 }
 
@@ -375,29 +779,58 @@ int sgp_dev_create(int device, uint32_t n_hosts, uint32_t cap, sgp_dev** out) {
         return 6;
     }
     PCHK(hipSetDevice(device));
+    if (n_hosts == 0) n_hosts = 1;
+    if (n_hosts > MAXP2 * HPB) {
+        sg_set_error("sgp_dev_create: %u hosts, at most %u", n_hosts, MAXP2 * HPB);
+        return 1;
+    }
+    if (cap == 0) cap = 16;
     sgp_dev* d = new sgp_dev();  // value-initialised: pointers and counters zero
     d->device = device;
-    if (n_hosts == 0) n_hosts = 1;
-    if (cap == 0) cap = 64;
-    int rc = alloc_q(d, &d->q, n_hosts, cap, d->qallocs);
+    Cal& c = d->c;
+    c.n = n_hosts;
+    // bucket width 2^shift ns (default 2^18 = 262 us: a 1 ms round reads ~5
+    // buckets, the ring reaches 4.3 s ahead); chunk-table entries per bucket
+    c.shift = env_u32("SG_PBUCKET_SHIFT", 18);
+    c.nchb = env_u32("SG_PBUCKET_CHUNKS", 1024);
+    if (c.shift > 40) c.shift = 40;
+    if (c.nchb == 0) c.nchb = 1;
+    if (c.nchb > (1u << 20)) c.nchb = 1u << 20;
+    c.cap = c.nchb * CH;
+    d->far_compact = env_u32("SG_PFAR_COMPACT", 65536);
+    const uint64_t nch = ((uint64_t)n_hosts * cap + CH - 1) / CH + 1;
+    d->nchunks = nch > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)nch;
+    int rc = 0;
+    if (!rc) rc = dmalloc((void**)&c.pool, (size_t)d->nchunks * CH * sizeof(sgp_rec));
+    if (!rc) rc = dmalloc((void**)&c.fst, (size_t)d->nchunks * 4);
+    if (!rc) rc = dmalloc((void**)&c.btab, (size_t)RB * c.nchb * 4);
+    if (!rc) rc = dmalloc((void**)&c.bh, RB * sizeof(BH));
+    if (!rc) rc = dmalloc((void**)&c.sc, sizeof(Scal));
+    if (!rc) rc = dmalloc((void**)&d->d_off, ((size_t)n_hosts + 1) * 4);
+    d->P2 = (n_hosts + HPB - 1) / HPB;
+    if (!rc) rc = dmalloc((void**)&d->d_pbase, ((size_t)d->P2 + 1) * 4);
+    if (!rc && (hipHostMalloc((void**)&d->h_off, ((size_t)n_hosts + 1) * 4, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void**)&d->h_sc, sizeof(Scal), hipHostMallocDefault) != hipSuccess ||
+                hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking) != hipSuccess)) {
+        sg_set_error("sgp_dev_create: allocation failed");
+        rc = 2;
+    }
+    Scal init{};
+    init.ftop = d->nchunks;
+    init.farmin = SIMTIME_MAX;
+    if (!rc) *d->h_sc = init;
+    if (!rc) rc = grow_far(d, 4096);
+    if (!rc) rc = fit_items(d);
     if (rc) {
         sgp_dev_destroy(d);
         return rc;
     }
-    if (hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->d_off, ((size_t)n_hosts + 1) * 4) != hipSuccess ||
-        hipMalloc(&d->d_cnt, (size_t)n_hosts * 4) != hipSuccess ||
-        hipMalloc(&d->d_bsum, ((size_t)n_hosts + BLOCK - 1) / BLOCK * 4) != hipSuccess ||
-        hipMalloc(&d->d_nfail, 4) != hipSuccess || hipMalloc(&d->d_scalar, 16) != hipSuccess ||
-        hipHostMalloc((void**)&d->h_off, ((size_t)n_hosts + 1) * 4, hipHostMallocDefault) != hipSuccess) {
-        sg_set_error("sgp_dev_create: allocation failed");
+    uint32_t g = (RB > d->nchunks ? RB : d->nchunks);
+    hipLaunchKernelGGL(k_cinit, dim3((g + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, c, d->nchunks);
+    if (hipMemcpyAsync(c.sc, &init, sizeof init, hipMemcpyHostToDevice, d->s) != hipSuccess ||
+        hipStreamSynchronize(d->s) != hipSuccess) {
         sgp_dev_destroy(d);
-        return 2;
-    }
-    hipLaunchKernelGGL(k_pinit, dim3((n_hosts + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, d->q);
-    if (hipStreamSynchronize(d->s) != hipSuccess) {
-        sgp_dev_destroy(d);
-        sg_set_error("sgp_dev_create: init kernel failed");
+        sg_set_error("sgp_dev_create: init failed");
         return 3;
     }
     *out = d;
@@ -407,12 +840,13 @@ int sgp_dev_create(int device, uint32_t n_hosts, uint32_t cap, sgp_dev** out) {
 int sgp_dev_destroy(sgp_dev* d) {
     if (!d) return 0;
     if (d->s) (void)hipStreamSynchronize(d->s);
-    for (void* p : d->qallocs) (void)hipFree(p);
-    void* dp[] = {d->d_in, d->d_fail, d->d_out, d->d_off, d->d_cnt, d->d_bsum, d->d_nfail, d->d_scalar};
+    void* dp[] = {d->c.pool, d->c.fst, d->c.btab, d->c.bh, d->c.sc, d->c.far,
+                  d->far2, d->c.items, d->d_in, d->d_rslot, d->d_tmp, d->d_tmp2, d->d_out, d->d_off, d->d_mat, d->d_pbase};
     for (void* p : dp)
         if (p) (void)hipFree(p);
     if (d->h_runs) (void)hipHostFree(d->h_runs);
     if (d->h_off) (void)hipHostFree(d->h_off);
+    if (d->h_sc) (void)hipHostFree(d->h_sc);
     if (d->s) (void)hipStreamDestroy(d->s);
     delete d;
     return 0;
@@ -438,63 +872,50 @@ int sgp_dev_insert_segs(sgp_dev* d, const sgp_rec* const* segs, const uint64_t* 
     PCHK(hipSetDevice(d->device));
     int rc = grow_in(d, n);
     if (rc) return rc;
+    // h_sc is current: every call that changes the device scalars ends in read_scal
+    Scal* h = d->h_sc;
+    // a far list mostly of tombstones is compacted first
+    if (h->nfar > d->far_compact && h->nfar - h->farlive > h->farlive) {
+        PCHK(hipMemsetAsync(&d->c.sc->nfar, 0, 8, d->s));
+        hipLaunchKernelGGL(k_fcompact, dim3(1024), dim3(BLOCK), 0, d->s, d->c.far, (uint64_t)h->nfar, d->far2,
+                           &d->c.sc->nfar);
+        PCHK(hipGetLastError());
+        sgp_rec* t = d->c.far;
+        d->c.far = d->far2;
+        d->far2 = t;
+        h->nfar = h->farlive;
+    }
+    if ((rc = grow_far(d, h->nfar + n))) return rc;
     uint64_t o = 0;
     for (uint32_t i = 0; i < nseg; ++i) {
         if (lens[i])
             PCHK(hipMemcpyAsync(d->d_in + o, segs[i], lens[i] * sizeof(sgp_rec), hipMemcpyHostToDevice, d->s));
         o += lens[i];
     }
-    const sgp_rec* src = d->d_in;
-    uint64_t m = n;
-    for (int attempt = 0; attempt < 32; ++attempt) {
-        PCHK(hipMemsetAsync(d->d_nfail, 0, 4, d->s));
-        uint32_t grid = (uint32_t)((m + BLOCK - 1) / BLOCK);
-        if (grid > 4096) grid = 4096;
-        // attempt > 0 re-delivers the records that overflowed (gathered into d_out)
-        hipLaunchKernelGGL(k_pins, dim3(grid), dim3(BLOCK), 0, d->s, d->q, src, m, d->d_fail, d->d_nfail);
-        PCHK(hipGetLastError());
-        uint32_t nfail = 0;
-        PCHK(hipMemcpyAsync(&nfail, d->d_nfail, 4, hipMemcpyDeviceToHost, d->s));
-        PCHK(hipStreamSynchronize(d->s));
-        if (nfail == 0) break;
-        // grow every queue x2, keep the delivered events, re-deliver the rest
-        const uint32_t oldcap = d->q.cap;
-        hipLaunchKernelGGL(k_pclamp, dim3((d->q.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, d->q, oldcap);
-        Q nq;
-        std::vector<void*> nk;
-        if ((rc = alloc_q(d, &nq, d->q.n, oldcap * 2, nk))) return rc;
-        hipLaunchKernelGGL(k_pcopy, dim3((d->q.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, nq, d->q);
-        PCHK(hipGetLastError());
-        std::vector<uint32_t> fidx(nfail);
-        std::vector<sgp_rec> all(m);
-        PCHK(hipMemcpyAsync(fidx.data(), d->d_fail, nfail * 4ull, hipMemcpyDeviceToHost, d->s));
-        PCHK(hipMemcpyAsync(all.data(), src, m * sizeof(sgp_rec), hipMemcpyDeviceToHost, d->s));
-        PCHK(hipStreamSynchronize(d->s));
-        for (void* p : d->qallocs) (void)hipFree(p);
-        d->qallocs = nk;
-        d->q = nq;
-        std::vector<sgp_rec> redo(nfail);
-        for (uint32_t i = 0; i < nfail; ++i) redo[i] = all[fidx[i]];
-        if ((rc = grow_out(d, nfail))) return rc;
-        PCHK(hipMemcpy(d->d_out, redo.data(), nfail * sizeof(sgp_rec), hipMemcpyHostToDevice));
-        src = d->d_out;
-        m = nfail;
-    }
+    const uint32_t grid = (uint32_t)((n + IPW - 1) / IPW);
+    PCHK(hipMemsetAsync(&d->c.sc->need, 0, 4, d->s));
+    hipLaunchKernelGGL(k_cins1, dim3(grid), dim3(BLOCK), 0, d->s, d->c, d->cur, d->d_in, n, d->d_rslot);
+    hipLaunchKernelGGL(k_cneed, dim3(RB / BLOCK), dim3(BLOCK), 0, d->s, d->c);
+    PCHK(hipGetLastError());
+    if ((rc = read_scal(d))) return rc;
+    if (h->need > h->ftop && (rc = grow_pool(d, d->nchunks + (h->need - h->ftop)))) return rc;
+    hipLaunchKernelGGL(k_calloc, dim3(RB / BLOCK), dim3(BLOCK), 0, d->s, d->c);
+    hipLaunchKernelGGL(k_cins2, dim3(grid), dim3(BLOCK), 0, d->s, d->c, d->d_in, n, d->d_rslot);
+    PCHK(hipGetLastError());
+    h->ftop -= h->need;
     d->queued += n;
     return 0;
 }
 
 int sgp_dev_min(sgp_dev* d, uint64_t* min_out) {
     PCHK(hipSetDevice(d->device));
-    const unsigned long long init = SIMTIME_MAX;
-    PCHK(hipMemcpyAsync(d->d_scalar, &init, 8, hipMemcpyHostToDevice, d->s));
-    uint32_t grid = (d->q.n + BLOCK - 1) / BLOCK;
-    if (grid > 1024) grid = 1024;
-    hipLaunchKernelGGL(k_pmin, dim3(grid), dim3(BLOCK), 0, d->s, d->q, d->d_scalar);
+    hipLaunchKernelGGL(k_cmin, dim3(RB / 1024), dim3(1024), 0, d->s, d->c);
     PCHK(hipGetLastError());
-    unsigned long long m = 0;
-    PCHK(hipMemcpyAsync(&m, d->d_scalar, 8, hipMemcpyDeviceToHost, d->s));
-    PCHK(hipStreamSynchronize(d->s));
+    int rc = read_scal(d);
+    if (rc) return rc;
+    const Scal* h = d->h_sc;
+    uint64_t m = h->farlive ? (uint64_t)h->farmin : SIMTIME_MAX;
+    for (uint32_t i = 0; i < RB / 1024; ++i) m = h->pmin[i] < m ? h->pmin[i] : m;
     *min_out = m;
     return 0;
 }
@@ -504,17 +925,25 @@ int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const ui
     PCHK(hipSetDevice(d->device));
     int rc = grow_out(d, d->queued ? d->queued : 1);
     if (rc) return rc;
-    const uint32_t n = d->q.n, nb = (n + BLOCK - 1) / BLOCK;
-    hipLaunchKernelGGL(k_pcount, dim3(nb), dim3(BLOCK), 0, d->s, d->q, barrier, d->d_cnt, d->d_bsum);
-    hipLaunchKernelGGL(k_pscan, dim3(1), dim3(1024), 0, d->s, d->d_bsum, nb, d->d_scalar);
-    hipLaunchKernelGGL(k_pwrite, dim3(nb), dim3(BLOCK), 0, d->s, d->q, barrier, d->d_cnt, d->d_bsum,
-                       d->d_out, d->d_off);
+    const uint32_t n = d->c.n, P2 = d->P2;
+    uint32_t nbk = 0;  // due buckets [cur, cur + nbk)
+    if (barrier > 0) {
+        const uint64_t last = (barrier - 1) >> d->c.shift;
+        if (last >= d->cur) nbk = last - d->cur + 1 < RB ? (uint32_t)(last - d->cur + 1) : RB;
+    }
+    hipLaunchKernelGGL(k_xplan, dim3(1), dim3(1024), 0, d->s, d->c, d->cur, nbk, barrier, 0);
+    hipLaunchKernelGGL(k_hist, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat);
+    hipLaunchKernelGGL(k_mscan, dim3(1), dim3(1024), 0, d->s, d->d_mat, P2, d->c, d->d_pbase);
+    hipLaunchKernelGGL(k_part, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat, d->d_tmp);
+    hipLaunchKernelGGL(k_local, dim3(P2), dim3(1024), 0, d->s, n, P2, d->d_pbase, d->d_tmp, d->d_tmp2, d->d_off);
+    hipLaunchKernelGGL(k_xrank, dim3(XG), dim3(BLOCK), 0, d->s, d->d_tmp2, d->d_off, &d->c.sc->total, d->d_out);
+    hipLaunchKernelGGL(k_xfinish, dim3(nbk ? nbk : 1), dim3(BLOCK), 0, d->s, d->c, d->cur, nbk);
     PCHK(hipGetLastError());
-    unsigned long long t = 0;
-    PCHK(hipMemcpyAsync(&t, d->d_scalar, 8, hipMemcpyDeviceToHost, d->s));
     PCHK(hipMemcpyAsync(d->h_off, d->d_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, d->s));
-    PCHK(hipStreamSynchronize(d->s));
+    if ((rc = read_scal(d))) return rc;
+    const uint64_t t = d->h_sc->total;
     if (t) PCHK(hipMemcpy(d->h_runs, d->d_out, t * sizeof(sgp_rec), hipMemcpyDeviceToHost));
+    if (barrier > 0 && (barrier >> d->c.shift) > d->cur) d->cur = barrier >> d->c.shift;
     d->queued -= t;
     *runs = d->h_runs;
     *off = d->h_off;
@@ -526,13 +955,12 @@ int sgp_dev_all(sgp_dev* d, sgp_rec* out, uint64_t capacity, uint64_t* n_out) {
     PCHK(hipSetDevice(d->device));
     int rc = grow_out(d, d->queued ? d->queued : 1);
     if (rc) return rc;
-    PCHK(hipMemsetAsync(d->d_scalar, 0, 8, d->s));
-    hipLaunchKernelGGL(k_pall, dim3((d->q.n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, d->s, d->q, d->d_out,
-                       d->out_cap, d->d_scalar);
+    PCHK(hipMemsetAsync(&d->c.sc->nall, 0, 8, d->s));
+    hipLaunchKernelGGL(k_xplan, dim3(1), dim3(1024), 0, d->s, d->c, d->cur, RB, (uint64_t)0, 1);
+    hipLaunchKernelGGL(k_call, dim3(XG), dim3(BLOCK), 0, d->s, d->c, d->d_out, d->out_cap);
     PCHK(hipGetLastError());
-    unsigned long long t = 0;
-    PCHK(hipMemcpyAsync(&t, d->d_scalar, 8, hipMemcpyDeviceToHost, d->s));
-    PCHK(hipStreamSynchronize(d->s));
+    if ((rc = read_scal(d))) return rc;
+    const uint64_t t = d->h_sc->nall;
     const uint64_t m = t < capacity ? t : capacity;
     if (out && m) PCHK(hipMemcpy(out, d->d_out, m * sizeof(sgp_rec), hipMemcpyDeviceToHost));
     *n_out = t;

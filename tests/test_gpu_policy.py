@@ -44,3 +44,42 @@ def test_gpu_policy_queue_growth():
     ref.run()
     r = policy.run_phold(cfg, 2, policy.gpu_ops(2, cfg["n_hosts"]))
     assert np.array_equal(r["digest"], ref.host_state()["digest"])
+
+
+@pytest.mark.parametrize("shift,chunks,compact", [
+    (4, 1024, 64),     # 16 ns buckets: the ring reaches 262 us ahead, nearly every event is far
+    (30, 1024, 65536),  # 1.07 s buckets: every round extracts from one straddling bucket
+    (22, 1, 64),       # 4 ms buckets of one 1024-record chunk: full buckets overflow to the far list
+])
+def test_gpu_policy_calendar_paths(monkeypatch, shift, chunks, compact):
+    """The device calendar's less common paths stay exact: the far list (beyond
+    the ring, or past a full bucket) with its compaction, and tombstones in a
+    bucket that straddles every barrier."""
+    monkeypatch.setenv("SG_PBUCKET_SHIFT", str(shift))
+    monkeypatch.setenv("SG_PBUCKET_CHUNKS", str(chunks))
+    monkeypatch.setenv("SG_PFAR_COMPACT", str(compact))
+    cfg = phold.c2_config(n_hosts=2000, end_time_s=0.4)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs, st = ref.host_state(), ref.stats()
+    r = policy.run_phold(cfg, 4, policy.gpu_ops(4, cfg["n_hosts"]))
+    assert np.array_equal(r["digest"], rs["digest"])
+    assert np.array_equal(r["pops_per_host"], rs["pops"])
+    for k in ("rounds", "pops", "sends", "bumped"):
+        assert r[k] == st[k], k
+
+
+def test_gpu_policy_many_host_blocks():
+    """50k hosts: the extraction's host sort spans 13 host blocks of 4096 and
+    several level-1 units per round."""
+    cfg = phold.c2_config(n_hosts=50_000, end_time_s=0.15)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs, st = ref.host_state(), ref.stats()
+    r = policy.run_phold(cfg, 8, policy.gpu_ops(8, cfg["n_hosts"]))
+    assert np.array_equal(r["digest"], rs["digest"])
+    assert np.array_equal(r["pops_per_host"], rs["pops"])
+    for k in ("rounds", "pops", "sends", "bumped"):
+        assert r[k] == st[k], k
