@@ -27,8 +27,8 @@
 //                      sort by host, the block's run offsets off[]
 //            k_xrank   each record ranked in its host's run in event_compare
 //                      order (event.c:110-153)
-//            k_xfinish spent buckets reset and their chunks freed; minima of
-//                      the straddling bucket and the far list updated
+//                      (and, on the side, spent buckets reset, their chunks
+//                      freed, the straddling bucket's and far list's minima set)
 //   MIN      k_cmin    over the RB bucket minima and the far minimum
 //                      (host_single.c:273-305)
 #include <hip/hip_runtime.h>
@@ -453,35 +453,65 @@ __global__ __launch_bounds__(1024) void k_part(Cal c, uint64_t barrier, uint32_t
     for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
         for (uint32_t d = t; d < P2; d += 1024) s_c[d] = mat[d * nu + u];
         sgp_rec e[UI];
-        sgp_rec* r[UI];
-        bool keep[UI];
 #pragma unroll
         for (uint32_t k = 0; k < UI; ++k) {
             const uint32_t j = u * UI + k;
             const uint4 it = j < ni ? c.items[j] : make_uint4(0, 0, 0, 0);
-            keep[k] = (it.x & FARBIT) || it.w;  // records that stay must be told apart
-            r[k] = const_cast<sgp_rec*>(item_base(c, it)) + t;
-            e[k].time = TOMB;
-            if (t < it.y) e[k] = *r[k];
+            e[k] = item_base(c, it)[t < it.y ? t : 0];  // unconditional load
+            if (t >= it.y) e[k].time = TOMB;
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t k = 0; k < UI; ++k) {
             if (e[k].time >= barrier) continue;
             tmp[atomicAdd(&s_c[e[k].dst >> HB], 1u)] = e[k];
-            if (keep[k]) r[k]->time = TOMB;
+            const uint4 it = c.items[u * UI + k];  // (uniform: reloaded rather than kept)
+            if ((it.x & FARBIT) || it.w)  // records that stay must be told apart
+                const_cast<sgp_rec*>(item_base(c, it))[t].time = TOMB;
         }
         __syncthreads();
     }
 }
 
+// Spent buckets back to the free stack (workgroup p takes due buckets p,
+// p + P2, ...); the straddling bucket and the far list get their new minima.
+__device__ __forceinline__ void finish_buckets(const Cal& c, uint64_t cur, uint32_t nbk, uint32_t p, uint32_t P2,
+                                               uint32_t* s_at) {
+    if (p == 0 && threadIdx.x == 0 && c.sc->farscan) {
+        c.sc->farmin = c.sc->fmin;
+        c.sc->farlive = c.sc->flive;
+    }
+    const uint64_t smin = c.sc->smin;
+    for (uint32_t k = p; k < nbk; k += P2) {
+        const uint32_t s = (uint32_t)(cur + k) & (RB - 1);
+        if (k + 1 == nbk && smin != SIMTIME_MAX) {  // events remain in the last due bucket
+            if (threadIdx.x == 0) c.bh[s].min = smin;
+            continue;
+        }
+        const uint32_t m = c.bh[s].chk;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            *s_at = m ? atomicAdd(&c.sc->ftop, m) : 0;
+            c.bh[s].cnt = 0;
+            c.bh[s].chk = 0;
+            c.bh[s].min = SIMTIME_MAX;
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < m; j += 1024) c.fst[*s_at + j] = c.btab[(size_t)s * c.nchb + j];
+    }
+}
+
 // Level 2, one workgroup per host block: an LDS counting sort by host writes
-// the block's run offsets off[] and its events in host order.
-__global__ __launch_bounds__(1024) void k_local(uint32_t n, uint32_t P2, const uint32_t* pbase, const sgp_rec* tmp,
-                                                sgp_rec* tmp2, uint32_t* off) {
+// the block's run offsets off[] and its events in host order; the spent
+// buckets are released on the side.
+__global__ __launch_bounds__(1024) void k_local(Cal c, uint64_t cur, uint32_t nbk, uint32_t n, uint32_t P2,
+                                                const uint32_t* pbase, const sgp_rec* tmp, sgp_rec* tmp2,
+                                                uint32_t* off) {
     __shared__ uint32_t s_c[HPB];
     __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_at;
     const uint32_t t = threadIdx.x, p = blockIdx.x, h0 = p << HB;
+    finish_buckets(c, cur, nbk, p, P2, &s_at);
     const uint32_t pb = pbase[p], pe = pbase[p + 1];
     const uint32_t nh = n - h0 < HPB ? n - h0 : HPB;
     for (uint32_t j = t; j < HPB; j += 1024) s_c[j] = 0;
@@ -524,33 +554,6 @@ __global__ __launch_bounds__(BLOCK) void k_xrank(const sgp_rec* tmp2, const uint
             rank += key_less(tmp2[j].time, tmp2[j].src_id, tmp2[j].seq, e.time, e.src_id, e.seq);
         out[s + rank] = e;
     }
-}
-
-// Spent buckets back to the free stack (one workgroup per due bucket); the
-// straddling bucket and the far list get their new minima.
-__global__ __launch_bounds__(BLOCK) void k_xfinish(Cal c, uint64_t cur, uint32_t nbk) {
-    __shared__ uint32_t s_at;
-    const uint32_t k = blockIdx.x;
-    if (k == 0 && threadIdx.x == 0 && c.sc->farscan) {
-        c.sc->farmin = c.sc->fmin;
-        c.sc->farlive = c.sc->flive;
-    }
-    if (k >= nbk) return;
-    const uint32_t s = (uint32_t)(cur + k) & (RB - 1);
-    const uint64_t smin = c.sc->smin;
-    if (k + 1 == nbk && smin != SIMTIME_MAX) {  // events remain in the last due bucket
-        if (threadIdx.x == 0) c.bh[s].min = smin;
-        return;
-    }
-    const uint32_t m = c.bh[s].chk;
-    if (threadIdx.x == 0) {
-        s_at = m ? atomicAdd(&c.sc->ftop, m) : 0;
-        c.bh[s].cnt = 0;
-        c.bh[s].chk = 0;
-        c.bh[s].min = SIMTIME_MAX;
-    }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < m; j += BLOCK) c.fst[s_at + j] = c.btab[(size_t)s * c.nchb + j];
 }
 
 // MIN over the bucket minima: RB / 1024 workgroups, one partial each (the host
@@ -935,9 +938,9 @@ int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const ui
     hipLaunchKernelGGL(k_hist, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat);
     hipLaunchKernelGGL(k_mscan, dim3(1), dim3(1024), 0, d->s, d->d_mat, P2, d->c, d->d_pbase);
     hipLaunchKernelGGL(k_part, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat, d->d_tmp);
-    hipLaunchKernelGGL(k_local, dim3(P2), dim3(1024), 0, d->s, n, P2, d->d_pbase, d->d_tmp, d->d_tmp2, d->d_off);
+    hipLaunchKernelGGL(k_local, dim3(P2), dim3(1024), 0, d->s, d->c, d->cur, nbk, n, P2, d->d_pbase, d->d_tmp,
+                       d->d_tmp2, d->d_off);
     hipLaunchKernelGGL(k_xrank, dim3(XG), dim3(BLOCK), 0, d->s, d->d_tmp2, d->d_off, &d->c.sc->total, d->d_out);
-    hipLaunchKernelGGL(k_xfinish, dim3(nbk ? nbk : 1), dim3(BLOCK), 0, d->s, d->c, d->cur, nbk);
     PCHK(hipGetLastError());
     PCHK(hipMemcpyAsync(d->h_off, d->d_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, d->s));
     if ((rc = read_scal(d))) return rc;
