@@ -555,6 +555,32 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
     __syncthreads();
     return wave_sum(lane < nw ? s16[lane] : (uint64_t)0);
 }
+// A workgroup's {min, sum, sum} for thread 0 alone, at the end of a role: wave
+// reductions, then one barrier that waits for LDS only, so the workgroup's
+// stores drain while the reduction and thread 0's atomics proceed (nothing in
+// the kernel reads those stores back).
+__device__ __forceinline__ void block_tail3(uint64_t& m, uint64_t& a, uint64_t& b) {
+    __shared__ uint64_t s_r[3][16];
+    m = wave_min(m);
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    if (lane == 0) {
+        s_r[0][w] = m;
+        s_r[1][w] = a;
+        s_r[2][w] = b;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (threadIdx.x == 0)
+        for (uint32_t k = 1; k < nw; ++k) {
+            m = s_r[0][k] < m ? s_r[0][k] : m;
+            a += s_r[1][k];
+            b += s_r[2][k];
+        }
+}
+
 // Inclusive scan of a u32 over the wave with DPP row shifts and broadcasts
 // (no LDS round trips).
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
@@ -1046,9 +1072,8 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
     }
-    const uint64_t m = block_min(cmin, s16);
-    const uint64_t nt = block_sum(ntomb, s16);
-    const uint64_t gn = block_sum(ng, s16);
+    uint64_t m = cmin, nt = ntomb, gn = ng;
+    block_tail3(m, nt, gn);
     if (threadIdx.x == 0) {
         if (gn) atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GATHER * d.P + w % d.P], (unsigned long long)gn);
         if (m != UINT64_MAX) atomicMin((unsigned long long*)&d.rs->xcarry2[sv.cur ^ 1], (unsigned long long)m);
@@ -2906,8 +2931,9 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
 __device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uint64_t smin, uint64_t ntomb,
                                               uint64_t* s16) {
     if (!ro.listed || ro.ret == UINT64_MAX) return;  // launch-uniform
-    const uint64_t m = block_min(smin, s16);
-    const uint64_t nt = block_sum(ntomb, s16);
+    (void)s16;
+    uint64_t m = smin, nt = ntomb, unused = 0;
+    block_tail3(m, nt, unused);
     if (threadIdx.x == 0) {
         const uint32_t rb = (uint32_t)(ro.ret % d.R);
         if (nt) atomicAdd(&d.btomb[rb], (uint32_t)nt);
