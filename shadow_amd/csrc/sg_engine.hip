@@ -555,6 +555,15 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* s16) {
     __syncthreads();
     return wave_sum(lane < nw ? s16[lane] : (uint64_t)0);
 }
+// A workgroup barrier for LDS data only: it waits for this wave's LDS
+// operations but not for its global stores and loads in flight, which a
+// __syncthreads() (vmcnt(0) in its release fence) would drain.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // A workgroup's {min, sum, sum} for thread 0 alone, at the end of a role: wave
 // reductions, then one barrier that waits for LDS only, so the workgroup's
 // stores drain while the reduction and thread 0's atomics proceed (nothing in
@@ -570,9 +579,7 @@ __device__ __forceinline__ void block_tail3(uint64_t& m, uint64_t& a, uint64_t& 
         s_r[1][w] = a;
         s_r[2][w] = b;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    lds_barrier();
     if (threadIdx.x == 0)
         for (uint32_t k = 1; k < nw; ++k) {
             m = s_r[0][k] < m ? s_r[0][k] : m;
@@ -594,13 +601,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
 }
 // Exclusive scan across the workgroup of two packed u32 counts (hi << 32 | lo;
 // neither total may overflow 32 bits); *total gets the sums.
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ uint64_t block_excl_scan_2x32(uint64_t v, uint64_t* s16, uint64_t* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
     const uint32_t lo = wave_incl_scan_u32((uint32_t)v), hi = wave_incl_scan_u32((uint32_t)(v >> 32));
     const uint64_t x = ((uint64_t)hi << 32) | lo;
-    __syncthreads();  // s16 may still be read by a previous use
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();  // s16 may still be read by a previous use
     if (lane == 63) s16[wid] = x;
-    __syncthreads();
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();
     // the wave totals one per lane, scanned across the wave: lane w holds the
     // sum of waves 0..w (each half stays within 32 bits by the contract)
     const uint64_t y = lane < nw ? s16[lane] : 0;
@@ -615,8 +623,9 @@ __device__ __forceinline__ uint64_t block_excl_scan_2x32(uint64_t v, uint64_t* s
     return x - v + add;
 }
 // Exclusive scan of u32 counts whose workgroup total fits 32 bits.
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* s16, uint64_t* total) {
-    return block_excl_scan_2x32((uint32_t)v, s16, total);
+    return block_excl_scan_2x32<LDS_ONLY>((uint32_t)v, s16, total);
 }
 
 // Wave-aggregated LDS reservations: one atomic per wave instead of one per
@@ -1452,10 +1461,12 @@ __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint
         mine += nn[q];
     }
     uint64_t total;
-    uint64_t off = block_excl_scan(mine, s16, &total);  // barriers inside
+    // LDS-only barriers: nothing here reads another lane's global stores, so
+    // the caller's stores keep draining
+    uint64_t off = block_excl_scan<true>(mine, s16, &total);
     if (total > sn) {  // uniform: beyond the stash, one ring reservation for the row
         if (tid == 0) *s_h = atomicAdd((unsigned long long*)&d.rs->fl_head, (unsigned long long)(total - sn));
-        __syncthreads();
+        lds_barrier();
     }
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
@@ -2701,7 +2712,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                                           count_local);
         a.emin = m < a.emin ? m : a.emin;  // in this shard's MIN terms from now on
     }
-    __syncthreads();  // staging done: sh.nloc final, bins complete
+    // staging done: sh.nloc final, bins complete (LDS); several shards: the
+    // outbox copy below reads other lanes' staged records from HBM
+    if (d.outn) __syncthreads();
+    else lds_barrier();
     if (d.outn) {
         // multi-shard: the partition's events for other shards into their peers'
         // outbox regions, one reservation per peer
@@ -2741,7 +2755,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         for (int i = 0; i < NPCTR + 2; ++i) s_red[wid][i] = v[i];
     }
     if (a.overflow) flag(d, OV_PROC);
-    __syncthreads();
+    lds_barrier();  // s_red
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     // wave 0: the partials and the MIN accumulators (the last workgroup reads
     // them), issued before the reservations
