@@ -191,7 +191,8 @@ int sg_graph_attach(const sg_graph* g, uint32_t n_hosts, const sg_attach_hint* h
  * 1986-1990, runs no Dijkstra; directed graphs can get the reverse path,
  * topology.c:1312-1318 / 2034-2036): this is its value when every lookup's
  * source runs its own Dijkstra first.  tests/test_topology_cache_order.py
- * models the cache and shows the cases.  Complete graphs are exact. */
+ * models the cache and shows the cases.  Complete graphs are exact; for the
+ * reference's own order use sg_path_cache below. */
 int sg_graph_paths(const sg_graph* g, const uint8_t* attached, double* latency_ms,
                    double* reliability, double* discovered_ms, uint8_t* kind);
 
@@ -202,6 +203,34 @@ int sg_graph_paths(const sg_graph* g, const uint8_t* attached, double* latency_m
 int sg_build_path_tables(uint32_t n_vertices, const double* latency_ms, const double* reliability,
                          const double* discovered_ms, uint64_t* delay_ns, int32_t* keep_max,
                          uint32_t* jump_ms);
+
+/* The reference's lazy path cache in lookup order, for a driver that performs
+ * the lookups in the reference's own order (the CPU-worker driver below: one
+ * worker pops hosts in their list order, each host's events in event_compare
+ * order, host_single.c:210-271).  A miss stores the direct path (complete
+ * graph, or preferred and adjacent: topology.c:2013-2024), the self path
+ * (topology.c:1545-1653), or every attached target's shortest path from the
+ * source (topology.c:1655-1875) under the store rules of topology.c:1306-1336
+ * (no entry in either direction; no non-direct path in a complete graph or
+ * beside a preferred direct edge); a hit may be the reverse entry (undirected:
+ * topology.c:1986-1990; after a miss in either kind of graph: 2033-2036).
+ * latency_ms and kind are sg_graph_paths' V*V tables (the latency a store
+ * would cache), attached its target flags (NULL = all).  The cache copies
+ * them.  Not thread-safe: callers serialise lookups (the reference holds its
+ * path-cache lock). */
+typedef struct sg_path_cache sg_path_cache;
+int sg_path_cache_create(uint32_t n_vertices, const double* latency_ms, const uint8_t* kind,
+                         const uint8_t* attached, int complete, int directed, sg_path_cache** out);
+int sg_path_cache_destroy(sg_path_cache* c);
+/* _topology_getPathEntry(src, dst): *pair_out = the V*V index of the path the
+ * reference returns (src*V+dst, or dst*V+src for a reverse entry: its delay
+ * and reliability are that entry's); *min_ms_out = topology->minimumPathLatency
+ * after the lookup (0 while nothing is stored; topology.c:1374-1385), whose
+ * truncation to ms is the window's next jump (master.c:148-159). */
+int sg_path_cache_lookup(sg_path_cache* c, uint32_t src_vertex, uint32_t dst_vertex, uint64_t* pair_out,
+                         double* min_ms_out);
+/* Source runs (Dijkstra) so far and stored entries. */
+int sg_path_cache_stats(const sg_path_cache* c, uint64_t* runs, uint64_t* stored);
 
 /* ------------------------------------------------------------------------ */
 /* 2. Device engine (synthetic PHOLD-style workload, "Mode S")               */
@@ -548,6 +577,16 @@ int sg_sched_run_phold(const sg_phold_params* params, const sg_phold_tables* tab
                        uint32_t n_workers, uint32_t scheduler_seed, const sg_sched_policy_ops* ops,
                        uint64_t max_rounds, sg_sched_result* result, uint64_t* digest,
                        uint64_t* pops, uint32_t* rng, uint64_t* event_counter);
+/* The same with the reference's ordered path discovery: every send looks its
+ * path up in `paths` (sg_path_cache_lookup, serialised by the driver) and
+ * takes that path's delay and reliability and the cache's minimum latency,
+ * instead of the tables' source-wide jump_ms.  With one worker the lookups come
+ * in the reference's order (`shadow -w 1`); with several, in the order the
+ * workers happen to reach them, as in the reference. */
+int sg_sched_run_phold_paths(const sg_phold_params* params, const sg_phold_tables* tables,
+                             sg_path_cache* paths, uint32_t n_workers, uint32_t scheduler_seed,
+                             const sg_sched_policy_ops* ops, uint64_t max_rounds, sg_sched_result* result,
+                             uint64_t* digest, uint64_t* pops, uint32_t* rng, uint64_t* event_counter);
 
 #ifdef __cplusplus
 }

@@ -89,6 +89,8 @@ def lib():
         L.orc_windows.restype = C.c_size_t
         L.orc_path_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orc_path_counts.restype = C.c_size_t
+        L.orc_set_ordered_discovery.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                                C.c_int]
         L.orc_probe_hash.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.orc_probe_hash.restype = C.c_uint64
         L.orc_digest_mix.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64]
@@ -182,6 +184,16 @@ class Sim:
         if not self.h:
             raise RuntimeError(L.orc_error().decode())
         self._destroy = L.orc_destroy  # held so interpreter shutdown can still free
+        if cfg.get("discovery") == "ordered":  # the reference's path cache in this oracle's pop order
+            pc = cfg["paths"]
+            self._pc = [np.ascontiguousarray(pc["latency_ms"], np.float64),
+                        np.ascontiguousarray(pc["kind"], np.uint8),
+                        np.ascontiguousarray(pc["attached"], np.uint8)]
+            if mode != MODE_HOST or (n_local is not None and n_local != cfg["n_hosts"]):
+                raise ValueError("ordered discovery needs the whole simulation in host order (MODE_HOST)")
+            if L.orc_set_ordered_discovery(self.h, *[a.ctypes.data for a in self._pc], int(pc["complete"]),
+                                           int(pc["directed"])):
+                raise RuntimeError(L.orc_error().decode())
 
     def close(self):
         if getattr(self, "h", None):

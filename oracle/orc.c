@@ -138,6 +138,14 @@ struct orc_sim {
     uint64_t* pcount; /* [V*V] path packet counters (topology.c:2053-2063) */
     uint32_t* seen;   /* gossip: [n_local][mw] message bitsets */
     uint32_t mw;
+    /* ordered discovery (orc_set_ordered_discovery): the reference's path
+     * cache replayed in this oracle's pop order */
+    double* pc_lat;
+    uint8_t *pc_kind, *pc_have;
+    uint32_t* pc_tgt;
+    uint32_t pc_ntgt;
+    int pc_complete, pc_directed;
+    double pc_min; /* topology->minimumPathLatency, 0 = unset */
 };
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
@@ -232,7 +240,66 @@ void orc_destroy(orc_sim* s) {
     free(s->win);
     free(s->pcount);
     free(s->seen);
+    free(s->pc_lat);
+    free(s->pc_kind);
+    free(s->pc_have);
+    free(s->pc_tgt);
     free(s);
+}
+
+/* ---------------- ordered path discovery ---------------------------------- */
+/* Test infrastructure: restates the reference's lazy path cache, looked up in
+ * the order this oracle pops events (hosts in index order, each host's events
+ * in event_compare order: shadow -w 1, host_single.c:210-271). */
+int orc_set_ordered_discovery(orc_sim* s, const double* lat, const uint8_t* kind, const uint8_t* attached,
+                              int complete, int directed) {
+    size_t V = s->p.n_vertices, VV = V * V;
+    s->pc_lat = (double*)malloc(VV * sizeof(double));
+    s->pc_kind = (uint8_t*)malloc(VV);
+    s->pc_have = (uint8_t*)calloc(VV, 1);
+    s->pc_tgt = (uint32_t*)malloc(V * 4);
+    if (!s->pc_lat || !s->pc_kind || !s->pc_have || !s->pc_tgt) {
+        snprintf(orc_err, sizeof orc_err, "orc_set_ordered_discovery: out of memory");
+        return -1;
+    }
+    memcpy(s->pc_lat, lat, VV * sizeof(double));
+    memcpy(s->pc_kind, kind, VV);
+    s->pc_ntgt = 0;
+    for (uint32_t v = 0; v < V; v++) /* _topology_getUniqueVertexTargets */
+        if (!attached || attached[v]) s->pc_tgt[s->pc_ntgt++] = v;
+    s->pc_complete = complete;
+    s->pc_directed = directed;
+    s->pc_min = 0;
+    return 0;
+}
+
+/* _topology_storePathInCache + _topology_shouldStorePath (topology.c:1306-1390) */
+static void pc_put(orc_sim* s, uint32_t a, uint32_t b, int direct) {
+    size_t V = s->p.n_vertices, ab = (size_t)a * V + b, ba = (size_t)b * V + a;
+    int exists = s->pc_have[ab] || s->pc_have[ba];
+    int refused = (s->pc_complete && !direct) || (!direct && s->pc_kind[ab] == 0 /* SG_PATH_DIRECT */);
+    if (exists || refused) return;
+    s->pc_have[ab] = 1;
+    if (s->pc_min == 0 || s->pc_lat[ab] < s->pc_min) s->pc_min = s->pc_lat[ab];
+}
+
+/* _topology_getPathEntry (topology.c:1969-2051): the V*V index of the path
+ * returned, or -1. */
+static int64_t pc_entry(orc_sim* s, uint32_t a, uint32_t b) {
+    size_t V = s->p.n_vertices, ab = (size_t)a * V + b, ba = (size_t)b * V + a;
+    if (s->pc_have[ab]) return (int64_t)ab;
+    if (!s->pc_directed && s->pc_have[ba]) return (int64_t)ba;
+    if (s->pc_kind[ab] == 0) { /* complete, or preferred and adjacent: the edge */
+        pc_put(s, a, b, 1);
+    } else if (a == b) { /* _topology_computeShortestPathToSelf, stored as non-direct */
+        pc_put(s, a, a, 0);
+    } else { /* _topology_computeSourcePaths: every attached target at once */
+        for (uint32_t i = 0; i < s->pc_ntgt; i++)
+            if (s->pc_tgt[i] != a) pc_put(s, a, s->pc_tgt[i], 0);
+    }
+    if (s->pc_have[ab]) return (int64_t)ab;
+    if (s->pc_have[ba]) return (int64_t)ba;
+    return -1;
 }
 
 static inline int is_local(const orc_sim* s, uint32_t h) {
@@ -302,7 +369,17 @@ static int send_one(orc_sim* s, uint32_t h, uint32_t* rng, uint64_t now, uint64_
     s->st.sends++;
     size_t pair = (size_t)s->vertex[h] * s->p.n_vertices + s->vertex[d];
     /* topology_getReliability builds the path (discovery) before the drop test */
-    if (s->jump[pair] < s->jmin) s->jmin = s->jump[pair];
+    if (s->pc_lat) { /* ordered discovery: the cache's entry and running minimum */
+        int64_t k = pc_entry(s, s->vertex[h], s->vertex[d]);
+        if (k < 0) {
+            snprintf(orc_err, sizeof orc_err, "no path %u -> %u", s->vertex[h], s->vertex[d]);
+            return -1;
+        }
+        pair = (size_t)k;
+        if (s->pc_min > 0 && (uint64_t)s->pc_min < s->jmin) s->jmin = (uint64_t)s->pc_min; /* master.c:153 */
+    } else if (s->jump[pair] < s->jmin) {
+        s->jmin = s->jump[pair];
+    }
     int32_t c = orc_rand_r(rng); /* chance = random_nextDouble(host RNG) */
     int bootstrapping = now < s->p.bootstrap_end;
     if (!(bootstrapping || c <= s->keep[pair])) {

@@ -88,6 +88,13 @@ size_t orc_windows(orc_sim* s, uint64_t* out_pairs, size_t cap_pairs);
 uint64_t orc_probe_hash(orc_sim* s, uint64_t* n_msgs);
 /* Kept sends per (source vertex, destination vertex), V*V (topology.c:2053-2063). */
 size_t orc_path_counts(orc_sim* s, uint64_t* out, size_t cap);
+/* Ordered discovery: sends look their path up in a restatement of the
+ * reference's lazy path cache (topology.c:1306-1390, 1655-1875, 1969-2051), in
+ * this oracle's pop order, instead of the jump_ms table.  lat / kind are
+ * sg_graph_paths' V*V tables (kind 0 = direct), attached the target flags
+ * (NULL = all).  Call before orc_boot. */
+int orc_set_ordered_discovery(orc_sim* s, const double* lat, const uint8_t* kind, const uint8_t* attached,
+                              int complete, int directed);
 
 uint64_t orc_digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq);
 

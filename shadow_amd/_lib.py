@@ -105,6 +105,8 @@ EXPORTS = [
     "sg_engine_set_timing", "sg_engine_set_timing_mask", "sg_comm_available", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_barrier_timers", "sg_engine_barrier_times", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
+    "sg_sched_run_phold_paths", "sg_path_cache_create", "sg_path_cache_destroy", "sg_path_cache_lookup",
+    "sg_path_cache_stats",
 ]
 
 

@@ -51,6 +51,9 @@ struct drv {
     sg_simtime min_next;
     pthread_mutex_t glock;
     uint64_t bumped;       /* counted by the driver's own bump detection */
+    sg_path_cache* paths;  /* ordered discovery (NULL: the tables' jump_ms) */
+    pthread_mutex_t plock; /* the reference's path-cache lock */
+    int path_err;
 };
 
 static uint64_t digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
@@ -106,8 +109,21 @@ static void execute(drv* d, wctx* w, sg_hevent* e) {
         if (dst >= d->N) continue;
         w->sends++;
         size_t pair = (size_t)d->T->host_vertex[h] * d->V + d->T->host_vertex[dst];
-        uint64_t jm = d->T->jump_ms[pair];
-        if (jm < w->jmin) w->jmin = jm;
+        if (d->paths) {
+            /* topology_getReliability → _topology_getPathEntry: the path the
+             * reference's cache returns now (possibly the reverse entry), and
+             * the minimum latency stored so far (master.c:148-159 truncates it) */
+            uint64_t k = pair;
+            double m = 0;
+            pthread_mutex_lock(&d->plock);
+            if (sg_path_cache_lookup(d->paths, d->T->host_vertex[h], d->T->host_vertex[dst], &k, &m)) d->path_err = 1;
+            pthread_mutex_unlock(&d->plock);
+            pair = (size_t)k;
+            if (m > 0 && (uint64_t)m < w->jmin) w->jmin = (uint64_t)m;
+        } else {
+            uint64_t jm = d->T->jump_ms[pair];
+            if (jm < w->jmin) w->jmin = jm;
+        }
         int32_t c = sg_rand_r(&d->rng[h]);
         if (!(e->time < d->P.bootstrap_end || c <= d->T->keep_max[pair])) {
             w->dropr++;
@@ -169,6 +185,14 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
                        uint32_t scheduler_seed, const sg_sched_policy_ops* ops, uint64_t max_rounds,
                        sg_sched_result* res, uint64_t* digest, uint64_t* pops, uint32_t* rng,
                        uint64_t* event_counter) {
+    return sg_sched_run_phold_paths(P, T, NULL, n_workers, scheduler_seed, ops, max_rounds, res, digest, pops,
+                                    rng, event_counter);
+}
+
+int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T, sg_path_cache* paths,
+                             uint32_t n_workers, uint32_t scheduler_seed, const sg_sched_policy_ops* ops,
+                             uint64_t max_rounds, sg_sched_result* res, uint64_t* digest, uint64_t* pops,
+                             uint32_t* rng, uint64_t* event_counter) {
     if (!P || !T || !ops || n_workers == 0 || P->n_hosts == 0 ||
         (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh) || P->workload != SG_WORKLOAD_PHOLD) {
         sg_set_error("sg_sched_run_phold: bad arguments (the CPU-worker driver runs the PHOLD body only)");
@@ -183,6 +207,7 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
     d->V = P->n_vertices;
     d->ops = ops;
     d->nw = n_workers;
+    d->paths = paths;
     d->rng = (uint32_t*)malloc((size_t)d->N * 4);
     d->evc = (uint64_t*)calloc(d->N, 8);
     d->pops = (uint64_t*)calloc(d->N, 8);
@@ -199,6 +224,7 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
     pthread_barrier_init(&d->collect_b, NULL, n_workers + 1);
     pthread_barrier_init(&d->prepare_b, NULL, n_workers + 1);
     pthread_mutex_init(&d->glock, NULL);
+    pthread_mutex_init(&d->plock, NULL);
     d->round_end = P->end_time; /* scheduler.c:130 */
     d->min_next = SG_SIMTIME_MAX;
     d->running = 1;
@@ -298,6 +324,8 @@ int sg_sched_run_phold(const sg_phold_params* P, const sg_phold_tables* T, uint3
     free(d->pops);
     free(d->digest);
     free(d->w);
+    pthread_mutex_destroy(&d->plock);
+    if (d->path_err) return SG_ERR_STATE;  /* sg_path_cache_lookup set the message */
     return SG_OK;
 }
 

@@ -821,3 +821,104 @@ int sg_build_path_tables(uint32_t n_vertices, const double* latency_ms, const do
     }
     return SG_OK;
 }
+
+/* ------------------------------------------------------------ path cache -- */
+struct sg_path_cache {
+    uint32_t V;
+    int complete, directed;
+    double* lat;        /* [V*V] the latency a store caches */
+    uint8_t* kind;      /* [V*V] sg_path_kind */
+    uint8_t* cached;    /* [V*V] entry stored for (src, dst) */
+    uint32_t* targets;  /* attached vertices (_topology_getUniqueVertexTargets) */
+    uint32_t nt;
+    double min_ms;      /* topology->minimumPathLatency, 0 = unset */
+    uint64_t runs, stored;
+};
+
+int sg_path_cache_create(uint32_t V, const double* latency_ms, const uint8_t* kind, const uint8_t* attached,
+                         int complete, int directed, sg_path_cache** out) {
+    if (!out || !latency_ms || !kind || V == 0) {
+        sg_set_error("sg_path_cache_create: bad argument");
+        return SG_ERR_INVAL;
+    }
+    *out = NULL;
+    const size_t n = (size_t)V * V;
+    sg_path_cache* c = (sg_path_cache*)calloc(1, sizeof *c);
+    if (c) {
+        c->lat = (double*)malloc(n * sizeof(double));
+        c->kind = (uint8_t*)malloc(n);
+        c->cached = (uint8_t*)calloc(n, 1);
+        c->targets = (uint32_t*)malloc((size_t)V * 4);
+    }
+    if (!c || !c->lat || !c->kind || !c->cached || !c->targets) {
+        sg_path_cache_destroy(c);
+        sg_set_error("sg_path_cache_create: out of memory");
+        return SG_ERR_NOMEM;
+    }
+    c->V = V;
+    c->complete = complete;
+    c->directed = directed;
+    memcpy(c->lat, latency_ms, n * sizeof(double));
+    memcpy(c->kind, kind, n);
+    for (uint32_t v = 0; v < V; ++v)
+        if (!attached || attached[v]) c->targets[c->nt++] = v;
+    *out = c;
+    return SG_OK;
+}
+
+int sg_path_cache_destroy(sg_path_cache* c) {
+    if (!c) return SG_OK;
+    free(c->lat);
+    free(c->kind);
+    free(c->cached);
+    free(c->targets);
+    free(c);
+    return SG_OK;
+}
+
+/* _topology_storePathInCache (topology.c:1337-1390) behind
+ * _topology_shouldStorePath (1306-1336). */
+static void pc_store(sg_path_cache* c, int direct, uint32_t s, uint32_t t) {
+    const size_t k = (size_t)s * c->V + t, kr = (size_t)t * c->V + s;
+    if (c->cached[k] || c->cached[kr]) return;               /* either direction: 1312-1318 */
+    if (c->complete && !direct) return;                      /* 1321-1323 */
+    if (!direct && c->kind[k] == SG_PATH_DIRECT) return;     /* preferred direct edge: 1325-1331 */
+    c->cached[k] = 1;
+    c->stored++;
+    const double l = c->lat[k];
+    if (c->min_ms == 0 || l < c->min_ms) c->min_ms = l;      /* 1374-1385 */
+}
+
+int sg_path_cache_lookup(sg_path_cache* c, uint32_t s, uint32_t d, uint64_t* pair_out, double* min_ms_out) {
+    if (!c || !pair_out || s >= c->V || d >= c->V) {
+        sg_set_error("sg_path_cache_lookup: bad argument");
+        return SG_ERR_INVAL;
+    }
+    const uint32_t V = c->V;
+    const size_t k = (size_t)s * V + d, kr = (size_t)d * V + s;
+    if (!c->cached[k] && (c->directed || !c->cached[kr])) {  /* a miss: topology.c:1986-1990 */
+        if (c->kind[k] == SG_PATH_DIRECT) {
+            pc_store(c, 1, s, d);                            /* 2013-2024 */
+        } else if (s == d) {
+            pc_store(c, 0, s, s);                            /* the self path, stored as non-direct (1650) */
+        } else {                                             /* one Dijkstra run from s: 1655-1875 */
+            c->runs++;
+            for (uint32_t i = 0; i < c->nt; ++i)
+                if (c->targets[i] != s) pc_store(c, 0, s, c->targets[i]);
+        }
+        if (!c->cached[k] && !c->cached[kr]) {               /* 2033-2045 */
+            sg_set_error("sg_path_cache_lookup: no path %u -> %u after the lookup", s, d);
+            return SG_ERR_STATE;
+        }
+    }
+    *pair_out = c->cached[k] ? k : kr;                       /* 2033-2036: either direction after a miss */
+    if (min_ms_out) *min_ms_out = c->min_ms;
+    return SG_OK;
+}
+
+int sg_path_cache_stats(const sg_path_cache* c, uint64_t* runs, uint64_t* stored) {
+    if (!c) return SG_ERR_INVAL;
+    if (runs) *runs = c->runs;
+    if (stored) *stored = c->stored;
+    return SG_OK;
+}

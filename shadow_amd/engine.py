@@ -19,6 +19,9 @@ class Engine:
                  queue_cap: int = 0, trace_capacity: int = 0, exchange_cap: int = 0,
                  stream: int | None = None):
         lib = L.lib()
+        if cfg.get("discovery") == "ordered" and not cfg["paths"]["complete"]:
+            raise ValueError("ordered path discovery (the reference's lookup-order cache) runs in the "
+                             "CPU-worker driver and the oracle; the engine's jump table is source-wide")
         p = L.PholdParams()
         p.n_hosts = cfg["n_hosts"]
         p.n_vertices = cfg["n_vertices"]

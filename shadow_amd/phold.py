@@ -174,17 +174,23 @@ def c5_config(n_hosts=100_000, V=256, fanout=8, msgs=64, start_ms=1.0, interval_
 
 def topology_config(graph, n_hosts, *, load=16, seed=1, end_time_s=10.0, hints=None,
                     dst_rule=L.SG_DST_WEIGHTS, window_rule=L.SG_WINDOW_DISCOVERED, runahead_ms=0,
-                    fixed_jump_ms=0, bootstrap_end=0, weights=None, name=None):
+                    fixed_jump_ms=0, bootstrap_end=0, weights=None, name=None, discovery="source"):
     """PHOLD on a GraphML topology (shadow_amd.topology.Graph): hosts attached
     by topology_attach from their node seeds (host.c:176, topology.c:2094-2369),
     paths resolved as topology.c would (direct, shortest or self), the jump table
-    carrying each lookup's discovered minimum latency (topology.c:1374-1385)."""
+    carrying each lookup's discovered minimum latency (topology.c:1374-1385).
+    discovery="ordered" also carries what the reference's lazy path cache needs
+    (cfg["paths"]): the CPU-worker driver (policy.run_phold) and the oracle then
+    replay the cache in their lookup order, which is the reference's with one
+    worker; the device engine keeps the source-wide jump table and refuses it."""
     from . import topology as T
+    if discovery not in ("source", "ordered"):
+        raise ValueError(f"discovery must be 'source' or 'ordered', not {discovery!r}")
     _, _, node = seed_chain(seed, n_hosts)
     vertex, rng = graph.attach(node, hints)
     attached = np.zeros(graph.n_vertices, bool)
     attached[vertex] = True
-    lat, rel, disc, _ = graph.paths(attached)
+    lat, rel, disc, kind = graph.paths(attached)
     delay, keep, jump = T.path_tables(lat, rel, disc)
     wt = None
     if dst_rule == L.SG_DST_WEIGHTS:
@@ -195,7 +201,10 @@ def topology_config(graph, n_hosts, *, load=16, seed=1, end_time_s=10.0, hints=N
         attach_rule=L.SG_ATTACH_RANDOM, end_time=int(round(end_time_s * 1e9)),
         bootstrap_end=int(bootstrap_end), fixed_jump=int(fixed_jump_ms * L.ONE_MS),
         runahead_min=int(runahead_ms * L.ONE_MS), host_vertex=vertex, host_rng=rng,
-        delay_ns=delay, keep_max=keep, jump_ms=jump, weight_thresh=wt)
+        delay_ns=delay, keep_max=keep, jump_ms=jump, weight_thresh=wt,
+        discovery=discovery,
+        paths=dict(latency_ms=lat, kind=kind, attached=attached.astype(np.uint8), complete=graph.complete,
+                   directed=graph.directed) if discovery == "ordered" else None)
 
 
 def c1_config(end_time_s=3600.0, load=16, seed=1):

@@ -53,8 +53,55 @@ def _bind():
                                            C.c_uint32, C.c_uint32, C.POINTER(PolicyOps), C.c_uint64,
                                            C.POINTER(SchedResult), C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
+        lib.sg_sched_run_phold_paths.argtypes = [C.POINTER(L.PholdParams), C.POINTER(L.PholdTables),
+                                                 C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(PolicyOps),
+                                                 C.c_uint64, C.POINTER(SchedResult), C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_void_p]
+        lib.sg_path_cache_create.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                             C.POINTER(C.c_void_p)]
+        lib.sg_path_cache_destroy.argtypes = [C.c_void_p]
+        lib.sg_path_cache_lookup.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_double)]
+        lib.sg_path_cache_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         lib._policy_bound = True
     return lib
+
+
+class PathCache:
+    """sg_path_cache: the reference's lazy path cache, looked up in the order
+    the driver's workers reach their sends (cfg["discovery"] == "ordered", from
+    phold.topology_config)."""
+
+    def __init__(self, cfg: dict):
+        lib = _bind()
+        pc = cfg["paths"]
+        self._keep = [np.ascontiguousarray(pc["latency_ms"], np.float64),
+                      np.ascontiguousarray(pc["kind"], np.uint8),
+                      np.ascontiguousarray(pc["attached"], np.uint8)]
+        h = C.c_void_p()
+        L.check(lib.sg_path_cache_create(cfg["n_vertices"], *[a.ctypes.data for a in self._keep],
+                                         int(pc["complete"]), int(pc["directed"]), C.byref(h)))
+        self.h = h
+        self._destroy = lib.sg_path_cache_destroy
+
+    def lookup(self, src_vertex: int, dst_vertex: int):
+        """(pair index of the path returned, minimum latency stored so far in ms)."""
+        k, m = C.c_uint64(), C.c_double()
+        L.check(_bind().sg_path_cache_lookup(self.h, src_vertex, dst_vertex, C.byref(k), C.byref(m)))
+        return int(k.value), float(m.value)
+
+    def stats(self):
+        r, n = C.c_uint64(), C.c_uint64()
+        L.check(_bind().sg_path_cache_stats(self.h, C.byref(r), C.byref(n)))
+        return {"runs": int(r.value), "stored": int(n.value)}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def gpu_ops(n_workers: int, n_hosts: int, device: int = 0) -> PolicyOps:
@@ -97,9 +144,10 @@ def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 
     rng = np.zeros(n, np.uint32)
     res = SchedResult()
     res.mark_round = mark_round
-    rc = lib.sg_sched_run_phold(C.byref(p), C.byref(t), n_workers, scheduler_seed, C.byref(ops),
-                                max_rounds, C.byref(res), dig.ctypes.data, pops.ctypes.data,
-                                rng.ctypes.data, ev.ctypes.data)
+    cache = PathCache(cfg) if cfg.get("discovery") == "ordered" else None
+    rc = lib.sg_sched_run_phold_paths(C.byref(p), C.byref(t), cache.h if cache else None, n_workers,
+                                      scheduler_seed, C.byref(ops), max_rounds, C.byref(res), dig.ctypes.data,
+                                      pops.ctypes.data, rng.ctypes.data, ev.ctypes.data)
     err = lib.sg_policy_ops_gpu_error(C.byref(ops)) if getattr(ops, "_owner", "") == "gpu" else 0
     if free_ops:
         ops.free(ops.data)

@@ -83,3 +83,25 @@ def test_gpu_policy_many_host_blocks():
     assert np.array_equal(r["pops_per_host"], rs["pops"])
     for k in ("rounds", "pops", "sends", "bumped"):
         assert r[k] == st[k], k
+
+
+@pytest.mark.parametrize("seed,hosts", [(2, 8), (11, 5), (33, 3)])
+def test_gpu_policy_ordered_discovery(seed, hosts):
+    """Row (f)-2 on the drop-in path: the `gpu` policy under one CPU worker
+    (shadow -w 1) on an incomplete graph, every send looked up in the
+    reference's lazy path cache in pop order (sg_path_cache), equals the
+    oracle's restatement of that cache; source-wide discovery gives another
+    run (tests/test_topology_cache_order.py)."""
+    from tests.test_topology_cache_order import ordered_case
+    runs = {}
+    for disc in ("source", "ordered"):
+        cfg = ordered_case(seed, hosts, disc)
+        ref = O.Sim(cfg)
+        ref.boot()
+        ref.run()
+        st, hs = ref.stats(), ref.host_state()
+        r = policy.run_phold(cfg, 1, policy.gpu_ops(1, hosts))
+        assert (r["rounds"], r["bumped"], r["pops"]) == (st["rounds"], st["bumped"], st["pops"]), disc
+        assert np.array_equal(r["digest"], hs["digest"]) and np.array_equal(r["ev"], hs["ev"]), disc
+        runs[disc] = (st["rounds"], st["bumped"])
+    assert runs["source"] != runs["ordered"]

@@ -31,6 +31,8 @@ Every BASELINE config uses a complete graph, where the two agree exactly.
 """
 import itertools
 
+import pytest
+
 import numpy as np
 
 from shadow_amd import topology as T
@@ -60,19 +62,24 @@ class RefPathCache:
             self.min_lat = lat
 
     def lookup(self, s, d):  # topology.c:1966-2047
+        self.entry = (s, d)  # which cached entry answered (for the product check)
         p = self.cache.get((s, d))
         if p is None and not self.directed:
+            self.entry = (d, s)
             p = self.cache.get((d, s))
         if p is not None:
             return p
         if self.complete or (self.prefer and self.adj[s][d]):
             self._store(s, d, self.dist[s][d], True)
-        elif s != d:
+        elif s == d:  # the path to self (topology.c:1545-1653), stored as non-direct
+            self._store(s, s, self.dist[s][s], False)
+        else:
             self.ran.add(s)
             for t in range(len(self.dist)):  # every attached target (topology.c:1676-1860)
                 if t != s:
                     self._store(s, t, self.dist[s][t], False)
         p = self.cache.get((s, d))
+        self.entry = (s, d) if p is not None else (d, s)
         return p if p is not None else self.cache.get((d, s))
 
 
@@ -176,3 +183,86 @@ def test_directed_graph_reverse_entry_is_returned():
     b = RefPathCache(dist, adj, directed=True)
     assert b.lookup(1, 0) == 6.0 and b.lookup(0, 1) == 6.0  # and the other way round
     assert (dist[0, 1], dist[1, 0]) == (3.0, 6.0)
+
+
+def _cache_cases():
+    rs = np.random.default_rng(11)
+    n = 9
+    und = _random_graph(rs, n, 0.2)
+    yield "undirected", T.Graph(_graphml(n, und)), und, False, False
+    yield "prefer-direct", T.Graph(_graphml(n, und, prefer="true")), und, True, False
+    yield "directed", T.Graph(_graphml(n, _random_graph(rs, n, 0.25), directed=True)), None, False, True
+    full = [(a, b, float(rs.uniform(1, 50)), 0.0) for a in range(5) for b in range(a, 5)]
+    yield "complete", T.Graph(_graphml(5, full)), full, False, False
+
+
+def test_product_path_cache_follows_the_model():
+    """sg_path_cache (the CPU-worker driver's ordered discovery) against the
+    model above on random lookup sequences, self lookups included: the same
+    entry answers every lookup (forward or reverse) and the running minimum is
+    the same after every lookup."""
+    from shadow_amd import policy
+    rs = np.random.default_rng(5)
+    for name, g, edges, prefer, directed in _cache_cases():
+        n = g.n_vertices
+        lat, _, _, kind = g.paths()
+        dist = lat.reshape(n, n)
+        adj = [[False] * n for _ in range(n)]
+        for a, b, _, _ in edges or []:
+            adj[a][b] = True
+            if not directed:
+                adj[b][a] = True
+        cfg = {"n_vertices": n, "paths": dict(latency_ms=lat, kind=kind, attached=np.ones(n, np.uint8),
+                                               complete=g.complete, directed=g.directed)}
+        for trial in range(20):
+            pc = policy.PathCache(cfg)
+            ref = RefPathCache(dist, adj, complete=g.complete, prefer_direct=prefer, directed=directed)
+            for _ in range(30):
+                s, d = (int(x) for x in rs.integers(0, n, 2))
+                k, m = pc.lookup(s, d)
+                want = ref.lookup(s, d)
+                assert want is not None, (name, s, d)
+                assert divmod(k, n) == ref.entry, (name, trial, s, d)
+                assert lat[k] == want and m == ref.min_lat, (name, trial, s, d)
+            pc.close()
+
+
+# small incomplete graphs where the reference's lookup order changes the run
+# (found by searching seeds: source-wide and ordered discovery differ)
+ORDERED_CASES = [(2, 8), (7, 3), (11, 5), (33, 3)]
+
+
+def ordered_case(seed, hosts, discovery):
+    from shadow_amd import phold
+    rs = np.random.default_rng(seed)
+    n = int(rs.integers(4, 9))
+    g = T.Graph(_graphml(n, _random_graph(rs, n, 0.2)))
+    assert not g.complete
+    return phold.topology_config(g, hosts, load=1, end_time_s=0.3, discovery=discovery, seed=seed + 1)
+
+
+@pytest.mark.parametrize("seed,hosts", ORDERED_CASES)
+def test_ordered_discovery_driver_matches_oracle(seed, hosts):
+    """One CPU worker (shadow -w 1) under the host_single restatement: the
+    driver's ordered discovery (sg_path_cache) and the oracle's restatement
+    give the same run, and it is not the source-wide run."""
+    from oracle import oracle as O
+    from shadow_amd import policy
+    runs = {}
+    for disc in ("source", "ordered"):
+        cfg = ordered_case(seed, hosts, disc)
+        ref = O.Sim(cfg)
+        ref.boot()
+        ref.run()
+        st, hs = ref.stats(), ref.host_state()
+        r = policy.run_phold(cfg, 1, O.cpu_policy_ops(False, 1, hosts))
+        assert (r["rounds"], r["bumped"], r["pops"]) == (st["rounds"], st["bumped"], st["pops"]), disc
+        assert np.array_equal(r["digest"], hs["digest"]) and np.array_equal(r["ev"], hs["ev"]), disc
+        runs[disc] = (st["rounds"], st["bumped"])
+    assert runs["source"] != runs["ordered"]
+
+
+def test_engine_refuses_ordered_discovery():
+    from shadow_amd.engine import Engine
+    with pytest.raises(ValueError, match="ordered path discovery"):
+        Engine(ordered_case(7, 3, "ordered"))
