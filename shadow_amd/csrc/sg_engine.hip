@@ -2058,7 +2058,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         const uint32_t wpe = d.pair_fmt == PAIR_NARROW ? 2u : 1u;  // words per record
         nwords = (nrow < d.rows_max ? nrow : d.rows_max) * d.V * wpe;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(d.prow) + (size_t)vlo * d.V * wpe;
-        const uint32_t last = (d.V - vlo) * d.V * wpe - 1;  // the table's end, from the first row
+        // clamped to the partition's own rows (nwords >= V): the loads past
+        // them re-read its last word instead of fetching rows nobody uses
+        const uint32_t last = nwords - 1;
 #pragma unroll
         for (uint32_t q = 0; q < RQ; ++q) {
             const uint32_t i = tid + q * K2_T;
