@@ -1,6 +1,6 @@
 #!/bin/bash
 # Mode P: GPU policy tests, then a kernel trace of the gpu policy at 1M hosts
-# with 16 workers (k_pins, k_pcount, k_pscan, k_pwrite, k_pmin) and the
+# with 16 workers (the calendar insert, extraction and MIN kernels) and the
 # serial-section split.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
