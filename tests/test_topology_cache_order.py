@@ -266,3 +266,18 @@ def test_engine_refuses_ordered_discovery():
     from shadow_amd.engine import Engine
     with pytest.raises(ValueError, match="ordered path discovery"):
         Engine(ordered_case(7, 3, "ordered"))
+
+
+def test_ordered_discovery_several_workers_runs():
+    """With several workers the lookups reach the cache in whatever order the
+    threads take (as in the reference): the run completes, every lookup is
+    served under the driver's lock, and with one worker the run repeats
+    exactly."""
+    from oracle import oracle as O
+    from shadow_amd import policy
+    cfg = ordered_case(2, 8, "ordered")
+    r4 = policy.run_phold(cfg, 4, O.cpu_policy_ops(False, 4, 8))
+    assert r4["pops"] > 0 and r4["rounds"] > 0
+    a = policy.run_phold(cfg, 1, O.cpu_policy_ops(False, 1, 8))
+    b = policy.run_phold(cfg, 1, O.cpu_policy_ops(False, 1, 8))
+    assert a["rounds"] == b["rounds"] and np.array_equal(a["digest"], b["digest"])
