@@ -147,13 +147,23 @@ def drop_in_policy(cfg, warmup, rounds, workers):
     keeps the per-host queues.  PCIe-inclusive by construction (the boundary
     hands over host records), so it is reported beside `value`, never as it."""
     from shadow_amd import policy
+    from shadow_amd.trace import state_fingerprint
     r = policy.run_phold(cfg, workers, policy.gpu_ops(workers, cfg["n_hosts"]),
                          max_rounds=warmup + rounds, mark_round=warmup)
-    return {"value": r["marked_pops"] / r["marked_seconds"], "unit": "events/s",
-            "workers": workers,
-            "sample": f"gpu SchedulerPolicy (Mode P) with {workers} CPU workers under the Shadow "
-                      f"round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} timed "
-                      f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s)"}
+    out = {"value": r["marked_pops"] / r["marked_seconds"], "unit": "events/s",
+           "workers": workers,
+           "sample": f"gpu SchedulerPolicy (Mode P) with {workers} CPU workers under the Shadow "
+                     f"round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} timed "
+                     f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s)"}
+    # the policy's end state against the oracle's per-round fixture (parity
+    # checker only, after the timed rounds)
+    if cfg["n_hosts"] == 1_000_000 and os.path.exists(FIXTURES):
+        rows = {row[0]: row for row in json.load(open(FIXTURES))["c4_1m"]["rounds"]}
+        end = r["rounds"]
+        if end in rows:
+            fp = state_fingerprint(0, r["digest"], r["pops_per_host"], r["rng"], r["ev"])
+            out["parity"] = {"round": end, "match": fp == rows[end][2] and r["pops"] == rows[end][1]}
+    return out
 
 
 def run_single(args):
