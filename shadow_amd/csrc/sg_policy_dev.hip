@@ -35,7 +35,6 @@
 
 #include <cstdlib>
 #include <cstring>
-#include <vector>
 
 #include "sg_policy_dev.h"
 
@@ -627,7 +626,6 @@ struct sgp_dev {
     uint32_t* d_off;     // [N + 1] host-ordered run offsets
     uint32_t P2;         // host blocks
     uint32_t* d_mat;     // [units][P2] level-1 counts, then bases
-    uint64_t mat_cap;    // units
     uint32_t* d_pbase;   // [P2 + 1] host block starts
     sgp_rec* h_runs;     // pinned
     uint32_t* h_off;
@@ -665,7 +663,6 @@ static int fit_items(sgp_dev* d) {
     if (d->d_mat) (void)hipFree(d->d_mat);
     d->d_mat = nullptr;
     if ((rc = dmalloc((void**)&d->d_mat, units * d->P2 * 4))) return rc;
-    d->mat_cap = units;
     return 0;
 }
 
