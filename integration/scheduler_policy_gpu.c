@@ -31,7 +31,9 @@
 #include <pthread.h>
 
 #include "main/core/scheduler/scheduler_policy.h"
+#include "main/core/support/options.h"
 #include "main/core/work/event.h"
+#include "main/core/worker.h"
 #include "main/host/host.h"
 #include "main/utility/utility.h"
 #include "shadowgpu.h"
@@ -65,18 +67,16 @@ typedef struct {
 #define SGCHK(x) do { int _rc = (x); if (_rc != SG_OK) error("gpu policy: %s", sg_last_error()); } while (0)
 
 /* addHost runs single-threaded from scheduler_start (scheduler.c:488-531); the
- * device policy is created at the first call after it, when every host and every
- * worker thread is known (the worker count is the number of distinct threads
- * hosts were assigned to, scheduler.c:437-486). */
+ * device policy is created at the first call after it, when every host is known.
+ * That first call comes from a worker thread (getAssignedHosts at boot,
+ * scheduler.c:572-589), so worker_getOptions() is valid there.  The worker count
+ * is the scheduler's nWorkers (slave.c:196 passes options_getNWorkerThreads to
+ * scheduler_new): every worker, including one that was assigned no host, calls
+ * getNextTime once per round (scheduler.c:393-394), and the device flush counts
+ * exactly those arrivals. */
 static gpointer _gpu_create(gpointer arg) {
     GpuPolicyData* d = arg;
-    GHashTable* threads = g_hash_table_new(g_direct_hash, g_direct_equal);
-    for (guint i = 0; i < d->pending->len; i++) {
-        PendingHost* ph = &g_array_index(d->pending, PendingHost, i);
-        g_hash_table_add(threads, GSIZE_TO_POINTER((gsize)ph->thread));
-    }
-    guint nThreads = g_hash_table_size(threads);
-    g_hash_table_destroy(threads);
+    guint nThreads = options_getNWorkerThreads(worker_getOptions());
     sg_policy_params prm = {.n_threads = nThreads ? nThreads : 1, .max_hosts = d->pending->len,
                             .queue_cap = 0, .device = 0};
     SGCHK(sg_policy_create(&prm, &d->p));

@@ -1,4 +1,5 @@
-"""In-tree build of libshadowgpu.so (gfx950) and the C policy harness.
+"""In-tree build of libshadowgpu.so (gfx950) and of the Shadow-side glue linked
+to it (integration/_bin/, only where the reference headers are present).
 
 hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
 container; the .so files travel to the GPU box with the repository snapshot.
@@ -76,6 +77,41 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", defines
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-lpthread"],
              verbose)
     return LIB
+
+
+REF_SRC = "/root/reference/src"
+GLIB_INC = ["/opt/conda/include/glib-2.0", "/opt/conda/lib/glib-2.0/include"]
+GLIB_LIB = "/opt/conda/lib"
+GLUE_BIN = os.path.join(ROOT, "integration", "_bin")
+GLUE_VARIANTS = {"relabel": [], "exact": ["-DSHADOW_HAS_EVENT_SRCID"]}
+
+
+def glue_available() -> bool:
+    return os.path.isdir(REF_SRC) and all(os.path.isdir(g) for g in GLIB_INC)
+
+
+def build_glue(verbose: bool = False, force: bool = False) -> list:
+    """integration/scheduler_policy_gpu.c + tests/glue_phold.c, compiled against
+    the reference's unmodified headers and linked to the real libshadowgpu.so
+    (rpath $ORIGIN/../../shadow_amd) and conda GLib: integration/_bin/
+    libsgglue_<variant>.so.  Needs /root/reference, so it runs in the build
+    container only; the .so files travel to the GPU box with the tree."""
+    if not glue_available():
+        return []
+    os.makedirs(GLUE_BIN, exist_ok=True)
+    srcs = [os.path.join(ROOT, "integration", "scheduler_policy_gpu.c"),
+            os.path.join(ROOT, "tests", "glue_phold.c"), os.path.join(INC, "shadowgpu.h"), LIB]
+    outs = []
+    for name, defs in GLUE_VARIANTS.items():
+        out = os.path.join(GLUE_BIN, f"libsgglue_{name}.so")
+        if force or _stale(out, srcs):
+            _run(["gcc", "-shared", "-fPIC", "-O2", "-std=gnu99", "-D_GNU_SOURCE", "-Wall",
+                  "-Werror=implicit-function-declaration", "-I" + REF_SRC, "-I" + INC] +
+                 ["-I" + g for g in GLIB_INC] + defs + srcs[:2] +
+                 ["-o", out, "-L" + GLIB_LIB, "-Wl,-rpath," + GLIB_LIB, "-lglib-2.0",
+                  "-L" + PKG, "-lshadowgpu", "-Wl,-rpath,$ORIGIN/../../shadow_amd", "-lpthread"], verbose)
+        outs.append(out)
+    return outs
 
 
 if __name__ == "__main__":

@@ -111,15 +111,9 @@ def gpu_ops(n_workers: int, n_hosts: int, device: int = 0) -> PolicyOps:
     return ops
 
 
-def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 62,
-              scheduler_seed: int | None = None, free_ops: bool = True,
-              mark_round: int = 0) -> dict:
-    """Run PHOLD under `ops` with n_workers CPU workers; returns per-host state
-    (digest, pops, rng, ev) and the driver's counters/timing."""
-    lib = _bind()
-    from .phold import seed_chain
-    if scheduler_seed is None:
-        scheduler_seed = seed_chain(cfg.get("seed", 1), 0)[1]  # slave.c:198
+def phold_args(cfg: dict):
+    """(sg_phold_params, sg_phold_tables, arrays kept alive) for the CPU-worker
+    driver (sg_sched_run_phold)."""
     p = L.PholdParams()
     p.n_hosts = cfg["n_hosts"]
     p.n_vertices = cfg["n_vertices"]
@@ -139,6 +133,23 @@ def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 
     wt = cfg.get("weight_thresh")
     wt = None if wt is None else np.ascontiguousarray(wt, np.int32)
     t = L.PholdTables(*[a.ctypes.data for a in arrs], None if wt is None else wt.ctypes.data)
+    return p, t, (arrs, wt)
+
+
+def default_scheduler_seed(cfg: dict) -> int:
+    from .phold import seed_chain
+    return seed_chain(cfg.get("seed", 1), 0)[1]  # slave.c:198
+
+
+def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 62,
+              scheduler_seed: int | None = None, free_ops: bool = True,
+              mark_round: int = 0) -> dict:
+    """Run PHOLD under `ops` with n_workers CPU workers; returns per-host state
+    (digest, pops, rng, ev) and the driver's counters/timing."""
+    lib = _bind()
+    if scheduler_seed is None:
+        scheduler_seed = default_scheduler_seed(cfg)
+    p, t, _keep = phold_args(cfg)
     n = cfg["n_hosts"]
     dig, pops, ev = (np.zeros(n, np.uint64) for _ in range(3))
     rng = np.zeros(n, np.uint32)
