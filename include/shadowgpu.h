@@ -348,8 +348,9 @@ int sg_engine_host_range(sg_engine* e, uint32_t* first_host, uint32_t* n_local);
 int sg_engine_active_hosts(sg_engine* e, uint64_t* active_host_rounds, uint64_t* emitted);
 /* Cumulative record moves of the insert kernels (the per-kernel roofline's
  * algorithmic bytes): events k_proc staged, events k_scatter's gather moved from
- * the calendar into host partitions, received events k_scatter wrote (several
- * shards). */
+ * the calendar into host partitions, received events k_scatter's receive role
+ * routed into host partitions (several shards; the received events it leaves
+ * for the next k_proc to stage are not counted). */
 int sg_engine_event_moves(sg_engine* e, uint64_t* emitted, uint64_t* gathered, uint64_t* received);
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
 /* Executed windows {start, end} per round (recorded when trace_capacity > 0). */

@@ -106,7 +106,7 @@ enum Ctr {
     C_ACTIVE, C_EMIT,
     NPCTR,                  // counters k_proc accumulates; k_scatter's follow
     C_GATHER = NPCTR,       // events the gather role moved from the calendar into partitions
-    C_RECV,                 // received events the insert role wrote (several shards)
+    C_RECV,                 // received events the receive role wrote into partitions (several shards)
     NCTR
 };
 
@@ -3202,14 +3202,14 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // per (workgroup, partition)); the next k_proc stages the rest
     // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
+    __shared__ uint32_t s_routed;
+    if (tid == 0) s_routed = 0;
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         s_pc[p] = 0;
         s_pk[p] = 0;
     }
     const uint64_t total = recv_offsets(d, recv, d.xrows, d.xcap, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
-    if (tid == 0 && hi > lo)  // C_RECV: the received events this workgroup looks at
-        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_RECV * d.P + w % d.P], (unsigned long long)(hi - lo));
     if (!ro.listed) return;  // uniform: no new window, nothing is due
     for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
         uint64_t t, k;
@@ -3223,9 +3223,12 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             const uint32_t base = atomicAdd(&d.pcnt[p], c);
             if (base + c > d.CAPP) flag(d, OV_PART);
             s_pc[p] = base;
+            atomicAdd(&s_routed, c);
         }
     }
     __syncthreads();
+    if (tid == 0 && s_routed)  // C_RECV: received events this workgroup writes into partitions
+        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_RECV * d.P + w % d.P], (unsigned long long)s_routed);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
         uint64_t t, k;
         uint32_t dl;

@@ -16,6 +16,7 @@
 #define _GNU_SOURCE
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -54,6 +55,7 @@ struct drv {
     sg_path_cache* paths;  /* ordered discovery (NULL: the tables' jump_ms) */
     pthread_mutex_t plock; /* the reference's path-cache lock */
     int path_err;
+    char path_msg[256];    /* the failing lookup's message (sg_last_error is per thread) */
 };
 
 static uint64_t digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
@@ -116,8 +118,15 @@ static void execute(drv* d, wctx* w, sg_hevent* e) {
             uint64_t k = pair;
             double m = 0;
             pthread_mutex_lock(&d->plock);
-            if (sg_path_cache_lookup(d->paths, d->T->host_vertex[h], d->T->host_vertex[dst], &k, &m)) d->path_err = 1;
+            int bad = sg_path_cache_lookup(d->paths, d->T->host_vertex[h], d->T->host_vertex[dst], &k, &m);
+            if (bad && !d->path_err) snprintf(d->path_msg, sizeof d->path_msg, "%s", sg_last_error());
             pthread_mutex_unlock(&d->plock);
+            if (bad) {  /* no path the cache returned: send nothing, and the main
+                         * loop ends the run after this round (a worker cannot
+                         * leave mid-round: the others wait at its barriers) */
+                __atomic_store_n(&d->path_err, 1, __ATOMIC_RELAXED);
+                continue;
+            }
             pair = (size_t)k;
             if (m > 0 && (uint64_t)m < w->jmin) w->jmin = (uint64_t)m;
         } else {
@@ -284,7 +293,7 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
         if (P->window_rule == SG_WINDOW_DISCOVERED && jmin != UINT64_MAX)
             ws.next_min_jump = jmin * SG_ONE_MS; /* topology.c:1374-1385 → master.c:153 */
         keep = sg_window_next(&ws, d->min_next, &start, &end);
-        if (rounds >= max_rounds) keep = 0;
+        if (rounds >= max_rounds || __atomic_load_n(&d->path_err, __ATOMIC_RELAXED)) keep = 0;
     }
     /* scheduler_finish */
     d->running = 0;
@@ -325,7 +334,10 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
     free(d->digest);
     free(d->w);
     pthread_mutex_destroy(&d->plock);
-    if (d->path_err) return SG_ERR_STATE;  /* sg_path_cache_lookup set the message */
+    if (d->path_err) {  /* the worker's message, on the caller's thread */
+        sg_set_error("%s", d->path_msg);
+        return SG_ERR_STATE;
+    }
     return SG_OK;
 }
 

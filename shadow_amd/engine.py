@@ -101,7 +101,8 @@ class Engine:
 
     def event_moves(self) -> dict:
         """Cumulative events staged by k_proc, gathered by k_scatter from the
-        calendar into partitions, and received events k_scatter wrote."""
+        calendar into partitions, and received events k_scatter routed into
+        partitions (several shards)."""
         v = [C.c_uint64() for _ in range(3)]
         L.check(L.lib().sg_engine_event_moves(self.h, *[C.byref(x) for x in v]))
         return dict(zip(("emitted", "gathered", "received"), (x.value for x in v)))

@@ -281,3 +281,29 @@ def test_ordered_discovery_several_workers_runs():
     a = policy.run_phold(cfg, 1, O.cpu_policy_ops(False, 1, 8))
     b = policy.run_phold(cfg, 1, O.cpu_policy_ops(False, 1, 8))
     assert a["rounds"] == b["rounds"] and np.array_equal(a["digest"], b["digest"])
+
+
+def test_ordered_discovery_stops_at_missing_path():
+    """a send whose path the cache cannot return fails the run at
+    the end of that round, instead of sending on a path the cache never
+    returned and running on to endTime.  (sg_graph_paths refuses disconnected
+    graphs, so the case is made by attaching no shortest-path target: every
+    lookup that needs a Dijkstra run then stores nothing.)"""
+    import ctypes as C
+    from oracle import oracle as O
+    from shadow_amd import _lib as L
+    from shadow_amd import policy
+    cfg = ordered_case(2, 8, "ordered")
+    cfg["end_time"] = 100 * L.ONE_MS * 1000  # 100 s: a run that went on would take many rounds
+    cfg["paths"] = dict(cfg["paths"], attached=np.zeros_like(np.asarray(cfg["paths"]["attached"])))
+    lib = policy._bind()
+    p, t, _keep = policy.phold_args(cfg)
+    cache = policy.PathCache(cfg)
+    ops = O.cpu_policy_ops(False, 2, cfg["n_hosts"])
+    res = policy.SchedResult()
+    rc = lib.sg_sched_run_phold_paths(C.byref(p), C.byref(t), cache.h, 2, policy.default_scheduler_seed(cfg),
+                                      C.byref(ops), 1 << 40, C.byref(res), None, None, None, None)
+    ops.free(ops.data)
+    assert rc == L.SG_ERR_STATE
+    assert "no path" in lib.sg_last_error().decode()
+    assert res.rounds <= 2  # the boot round sends; the run ends after it
