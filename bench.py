@@ -32,7 +32,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+from shadow_amd.roofline import HBM_PEAK_GBS, kernel_line, proc_bytes, scatter_bytes  # noqa: E402
 # PMC HBM bytes per launch of the dominant kernel for this default workload:
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
@@ -53,24 +53,15 @@ def pmc_traffic(n_hosts, kernel=DOMINANT):
     return k["traffic_bytes"], k.get("traffic_bytes_lower"), os.path.relpath(PMC_JSON, ROOT)
 
 
-ALG_BYTES_PER_EVENT = 64
-ALG_BYTES_PER_ACTIVE_HOST = 24
-# k_scatter: every record it moves is read once and written once,
-# 16 B each way: staged events into the calendar (insert role, due ones routed
-# straight to their partition) and the new window's calendar events into the
-# host partitions (gather role); the rmin and refill roles' few KB are not counted
-ALG_BYTES_PER_MOVE = 32
-
-
 def kernel_roofline(name, alg_bytes, avg_s, n_hosts):
     """One kernel's line of roofline.per_kernel: algorithmic bytes per launch
     over its average launch time against HBM peak, beside the committed PMC
     traffic per launch."""
     traffic, lower, src = pmc_traffic(n_hosts, name)
-    ach = alg_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    return {"avg_us": avg_s * 1e6, "alg_bytes_per_launch": alg_bytes, "achieved": ach,
-            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": lower,
-            "traffic_gbs": traffic / avg_s / 1e9 if traffic and avg_s else None, "traffic_source": src}
+    out = kernel_line(alg_bytes, avg_s)
+    out.update(traffic=traffic, traffic_lower=lower,
+               traffic_gbs=traffic / avg_s / 1e9 if traffic and avg_s else None, traffic_source=src)
+    return out
 
 
 def parse():
@@ -210,17 +201,17 @@ def run_single(args):
     a2, _ = eng.active_hosts()
     mv2 = eng.event_moves()
     kpops = s2["pops"] - s1["pops"]
-    alg_bytes = ALG_BYTES_PER_EVENT * kpops + ALG_BYTES_PER_ACTIVE_HOST * (a2 - a1)
+    alg_bytes = proc_bytes(kpops, a2 - a1)
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic, traffic_lower, traffic_src = pmc_traffic(args.hosts)
     kus = {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]}
     ins_ms, ins_n = kt["insert"]
-    moves = (mv2["emitted"] - mv1["emitted"]) + (mv2["gathered"] - mv1["gathered"])
+    moves = {k: mv2[k] - mv1[k] for k in mv2}
     per_kernel = {
         DOMINANT: kernel_roofline(DOMINANT, per_launch_bytes, avg_launch_s, args.hosts),
-        "k_scatter": kernel_roofline("k_scatter", ALG_BYTES_PER_MOVE * moves / max(ins_n, 1),
+        "k_scatter": kernel_roofline("k_scatter", scatter_bytes(moves) / max(ins_n, 1),
                                      ins_ms / 1e3 / max(ins_n, 1), args.hosts),
     }
     res = {

@@ -355,14 +355,24 @@ def bench(args, make_shard=None):
     end_round = end["rounds"]
     # per-rank kernel times over the next steps (HIP events on the engine stream;
     # the exchange class is this rank's RCCL all-to-all: its wait for the slowest
-    # rank plus the transfer, the barrier idle time of scheduler.c:380-389)
+    # rank plus the transfer, the barrier idle time of scheduler.c:380-389), with
+    # the algorithmic bytes the same steps moved: each rank's roofline per kernel
     kr = max(1, min(args.steps, args.kernel_rounds))
-    if native:
-        shard.eng.set_timing(True)
+    eng = getattr(shard, "eng", None)
+    if eng is not None:
+        from .roofline import proc_bytes, scatter_bytes
+        sa, a1, mv1 = shard.stats(), eng.active_hosts()[0], eng.event_moves()
+        eng.set_timing(True)
         run(shard, world, kr, check_every=1 << 30)
-        kt = shard.eng.kernel_times()
-        shard.eng.set_timing(False)
-        rows = _gather_rows([kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES], cdev)
+        kt = eng.kernel_times()
+        eng.set_timing(False)
+        sb, a2, mv2 = shard.stats(), eng.active_hosts()[0], eng.event_moves()
+        moves = {k: mv2[k] - mv1[k] for k in mv2}
+        vals = [kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES]  # us per step per class
+        vals += [kt["process"][1], proc_bytes(sb["pops"] - sa["pops"], a2 - a1),
+                 kt["insert"][1], scatter_bytes(moves), kt["exchange"][1],
+                 float(world * shard.rows * 3 * 8)]  # exchange bytes this rank sends per step
+        rows = _gather_rows(vals, cdev)
     else:
         rows = None
     shard.close_native()
@@ -404,9 +414,41 @@ def bench(args, make_shard=None):
         "_end_round": end_round, "_fingerprint": fp,
     }
     if rows is not None:
+        nk = len(KERNEL_CLASSES)
         res["per_rank_us_per_step"] = {
-            "classes": list(KERNEL_CLASSES), "steps": kr, "rows": rows,
+            "classes": list(KERNEL_CLASSES), "steps": kr, "rows": [r[:nk] for r in rows],
             "note": "HIP events around every launch on each rank's engine stream (they inflate "
                     "each kernel by a few us); 'exchange' is the RCCL all-to-all: wait for the "
-                    "slowest rank + transfer (barrier idle, scheduler.c:380-389)"}
+                    "slowest rank + transfer (barrier idle, scheduler.c:380-389); the Python "
+                    "step loop (--py-steps, gloo) leaves it untimed"}
+        res["roofline"] = dist_roofline(rows, nk, kr, KERNEL_CLASSES)
     return res
+
+
+def dist_roofline(rows, nk, steps, classes):
+    """The N > 1 line's roofline: per rank, k_proc and k_scatter's algorithmic
+    bytes per launch over their average launch time (HIP events) against 8 TB/s,
+    and the exchange's µs and bytes per step; the top-level fields are the
+    slowest rank's k_proc (the dominant kernel)."""
+    from .roofline import HBM_PEAK_GBS, kernel_line
+    per_rank = []
+    for r in rows:
+        us = dict(zip(classes, r[:nk]))
+        pn, pb, sn, sb, xn, xb = r[nk:nk + 6]
+        kp = kernel_line(pb / max(pn, 1), us["process"] * 1e-6 * steps / max(pn, 1))
+        ks = kernel_line(sb / max(sn, 1), us["insert"] * 1e-6 * steps / max(sn, 1))
+        per_rank.append({"k_proc": kp, "k_scatter": ks,
+                         "exchange": {"avg_us": us["exchange"] * steps / xn if xn else None,
+                                      "bytes_per_step": xb, "timed": bool(xn)}})
+    slow = max(range(len(per_rank)), key=lambda i: per_rank[i]["k_proc"]["avg_us"])
+    kp = per_rank[slow]["k_proc"]
+    return {"bound": "hbm", "kernel": "k_proc", "rank": slow, "achieved": kp["achieved"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kp["frac"], "traffic": None,
+            "avg_launch_us": kp["avg_us"], "alg_bytes_per_launch": kp["alg_bytes_per_launch"],
+            "timing_rounds": steps, "per_rank": per_rank,
+            "per_kernel": {k: {"frac_min": min(p[k]["frac"] for p in per_rank),
+                               "frac_max": max(p[k]["frac"] for p in per_rank),
+                               "avg_us_max": max(p[k]["avg_us"] for p in per_rank)}
+                           for k in ("k_proc", "k_scatter")},
+            "timing_method": "HIP events as each launch's dispatch-packet timestamps, steps after "
+                             "the timed region; traffic (PMC) is profiled at N = 1 only"}

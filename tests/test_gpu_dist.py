@@ -130,3 +130,13 @@ def test_bench_two_ranks_self_launched():
     assert res["n_gpus"] == 2 and res["value"] > 0
     assert res["parity"]["match"] is True, res["parity"]
     assert res["metric"].endswith("; bit-exact")
+    # the N > 1 line's roofline: every rank's k_proc / k_scatter fraction and
+    # the exchange's bytes per step (north_star: a fraction per kernel at N > 1)
+    rf = res["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_proc"
+    assert len(rf["per_rank"]) == 2
+    for pr in rf["per_rank"]:
+        for k in ("k_proc", "k_scatter"):
+            assert pr[k]["avg_us"] > 0 and pr[k]["alg_bytes_per_launch"] > 0 and 0 < pr[k]["frac"] < 1, (k, pr)
+        assert pr["exchange"]["bytes_per_step"] > 0
+    assert set(rf["per_kernel"]) == {"k_proc", "k_scatter"}

@@ -16,7 +16,8 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _run_shards(cfg, world, xcap, trace=0):
+def _run_shards(cfg, world, xcap, trace=0, between=None):
+    """between(step, shards): called after each step's post (on the stream)."""
     from shadow_amd.dist import EngineShard
     stream = torch.cuda.Stream()
     shards = [EngineShard(cfg, r, world, 0, exchange_cap=xcap, stream=stream, trace_capacity=trace)
@@ -33,6 +34,8 @@ def _run_shards(cfg, world, xcap, trace=0):
             for s in shards:
                 s.post()
             steps += 1
+            if between is not None:
+                between(steps, shards)
             if steps % 8 == 0 and shards[0].done():
                 break
             assert steps < 200_000
@@ -130,3 +133,60 @@ def test_graph_rounds_match_oracle(graph):
     for k in ("digest", "pops", "rng", "ev"):
         assert np.array_equal(g[k], o[k]), k
     assert eng.stats()["rounds"] == ref.stats()["rounds"]
+
+
+POISON = -0x0123456789ABCDF  # not a valid event row or header
+
+
+def test_exchange_cap_change_keeps_received_blocks():
+    """sg_engine_set_exchange_cap between steps while the last received blocks
+    are still unconsumed (the next k_proc stages the ones k_scatter did not
+    route): the caller reallocates its buffers, and the new receive buffer is
+    poisoned, so a k_proc that read it instead of the engine's copy would
+    diverge (the round-3 mismatch, gpurun_out/ab/sharded.log).  Changes land on
+    process steps and on drain steps, shrinking and growing the blocks."""
+    cfg = phold.tiny_config(n_hosts=600, V=6, load=6, end_time_s=0.4, loss=0.1)
+    plan = {3: 4096, 5: 9, 9: 40, 14: 4096, 20: 13}
+    seen = {"drain": 0, "process": 0}
+
+    def between(step, shards):
+        cap = plan.get(step)
+        if cap is None and step > 20 and step % 7 == 0:
+            cap = 13 if shards[0].eng.exchange_rows() > 100 else 4096
+        if cap is None:
+            return
+        st = shards[0].stats()
+        seen["drain" if st["phase"] else "process"] += 1
+        for sh in shards:
+            sh.set_exchange_cap(cap)
+            sh.recv.fill_(POISON)
+            sh.send.fill_(POISON)
+
+    shards, _ = _run_shards(cfg, 3, 4096, between=between)
+    st, want = _check(cfg, shards)
+    assert st[0]["exchange_steps"] > want["rounds"]  # small caps drained over extra steps
+    assert seen["drain"] >= 1 and seen["process"] >= 1, seen
+
+
+def test_native_exchange_cap_change_world1():
+    """The native step loop (world-1 RCCL communicator) with exchange_cap changed
+    between batches of steps: buffers reallocated and poisoned, graphs rebuilt."""
+    from shadow_amd.dist import EngineShard
+    from shadow_amd.engine import Comm
+    cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
+    sh = EngineShard(cfg, 0, 1, 0, exchange_cap=4096)
+    sh.comm = Comm(Comm.unique_id(), 0, 1, 0)
+    sh.eng.set_graph(4)
+    sh.boot()
+    n, caps = 0, [256, 4096, 512, 1024]
+    while not sh.done():
+        sh.run_native(8)
+        n += 8
+        sh.set_exchange_cap(caps[(n // 8) % len(caps)])
+        with sh.stream_ctx():  # ordered before the next steps on the engine stream
+            sh.recv.fill_(POISON)
+            sh.send.fill_(POISON)
+        assert n < 100_000
+    sh.sync()
+    _check(cfg, [sh])
+    sh.close_native()
