@@ -139,13 +139,19 @@ def drop_in_policy(cfg, warmup, rounds, workers):
     hands over host records), so it is reported beside `value`, never as it."""
     from shadow_amd import policy
     from shadow_amd.trace import state_fingerprint
-    r = policy.run_phold(cfg, workers, policy.gpu_ops(workers, cfg["n_hosts"]),
-                         max_rounds=warmup + rounds, mark_round=warmup)
+
+    def one(w):
+        return policy.run_phold(cfg, w, policy.gpu_ops(w, cfg["n_hosts"]),
+                                max_rounds=warmup + rounds, mark_round=warmup)
+
+    r = one(workers)
+    r1 = one(1) if workers > 1 else r
     out = {"value": r["marked_pops"] / r["marked_seconds"], "unit": "events/s",
-           "workers": workers,
+           "workers": workers, "single_thread_value": r1["marked_pops"] / r1["marked_seconds"],
            "sample": f"gpu SchedulerPolicy (Mode P) with {workers} CPU workers under the Shadow "
                      f"round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} timed "
-                     f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s)"}
+                     f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s); single_thread_value "
+                     f"is -w 1 on the same rounds"}
     # the policy's end state against the oracle's per-round fixture (parity
     # checker only, after the timed rounds)
     if cfg["n_hosts"] == 1_000_000 and os.path.exists(FIXTURES):

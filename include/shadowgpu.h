@@ -562,6 +562,16 @@ typedef struct sg_sched_result {
     uint64_t mark_round;
     double marked_seconds;
     uint64_t marked_pops, marked_rounds;
+    /* CPU time by stage, summed over the workers (input: profile != 0; the
+     * rounds after mark_round when it is set, else the whole run): the policy's
+     * push / pop / getNextTime calls (pop includes the extraction the first pop
+     * of a round runs; getNextTime includes its flush and the wait for the
+     * other workers' arrivals), the event bodies without their pushes, and the
+     * scheduler barriers (scheduler.c:380-408).  Costs two clock reads per
+     * call. */
+    uint64_t profile;
+    double prof_push_s, prof_pop_s, prof_next_s, prof_exec_s, prof_barrier_s;
+    uint64_t prof_pushes, prof_pops;
 } sg_sched_result;
 
 /* The gpu policy as a vtable (data = a new sg_policy on `device`); release it

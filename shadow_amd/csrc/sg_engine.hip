@@ -2051,6 +2051,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // them, and stored into LDS after the scatter
     constexpr uint32_t RQ = (32u << 10) / 4 / K2_T;
     uint32_t vlo = 0, rw[RQ], nwords = 0;
+    auto load_rows = [&]() __attribute__((always_inline)) {
     if constexpr (ROWS) {
         const uint32_t s0 = p * HP, s1 = (p + 1) * HP < d.L ? (p + 1) * HP : d.L;
         vlo = d.sinfo[s0].v;
@@ -2068,6 +2069,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         if (nrow > d.rows_max && tid == 0) flag(d, OV_BUG);  // the host sized rows_max
     }
+    };
+#ifndef SG_X_ROWLATE
+    load_rows();
+#endif
     auto pair_of = [&](uint32_t sv, uint32_t dv, bool wj) __attribute__((always_inline)) {
         if constexpr (ROWS) return lds_pair(d, s_rows, vlo, sv, dv, wj);
         else return load_pair(d, sv, dv, wj);
@@ -2109,6 +2114,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     __syncthreads();
+#ifdef SG_X_ROWLATE
+    load_rows();  // experiment: the rows after the partition records and the histogram
+#endif
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;

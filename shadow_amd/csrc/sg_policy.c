@@ -77,32 +77,48 @@ static void sheap_pop(sheap* h) {
 }
 
 /* ---------------------------------------------------------------- state -- */
+/* Per host: what other threads may touch.  The owner's pop position lives in
+ * its thread_rt (pos / gen, by the host's place in the thread's list), so the
+ * pops of different workers never write a shared cache line (hosts of
+ * different workers sit side by side in this array: the assignment is a
+ * shuffle, scheduler.c:437-531). */
 typedef struct host_rt {
-    uint32_t run_pos;         /* next event of this round's extracted run ... */
-    uint32_t run_gen;         /* ... valid while equal to sg_policy.run_gen */
-    sheap selfq;
+    sheap selfq;              /* same-round self events (owner pushes and pops) */
     uint32_t id;              /* GQuark */
     uint32_t thread;          /* owning thread slot */
+    uint32_t lpos;            /* place in the owner's host list */
     int in_self_list;
-    pthread_mutex_t lock;
+    pthread_mutex_t lock;     /* selfq, for a push from another thread */
 } host_rt;
 
-typedef struct thread_rt {
+/* Per worker, one 128-B aligned slot each: a worker's pushes (arena) and pops
+ * (cursor, positions) write only its own lines. */
+typedef struct __attribute__((aligned(128))) thread_rt {
     uint64_t token;
     uint32_t* hosts;
+    uint32_t* pos;            /* [n] next event of the host's extracted run ... */
+    uint32_t* gen;            /* [n] ... valid while equal to sg_policy.run_gen */
     uint32_t n, cap, cursor;
     sg_simtime cur_barrier;
     sgp_rec* arena;
     uint64_t na, ca;
 } thread_rt;
 
+/* The calling thread's slot of the last policy it used (pop / push are called
+ * per event; a linear search over the workers would read every slot). */
+static _Atomic uint64_t g_policy_uid;
+static __thread uint64_t tl_uid;
+static __thread uint64_t tl_token;
+static __thread void* tl_slot;
+
 struct sg_policy {
+    sg_simtime prepared;      /* barrier the current runs were extracted for (read per pop) */
+    uint64_t uid;             /* this policy's id for the per-thread slot cache */
     sg_policy_params prm;
     sgp_dev* dev;
     host_rt* hosts;
     uint32_t n_hosts;
-    uint32_t* map_key;        /* open addressing: host id -> index + 1 */
-    uint32_t* map_val;
+    uint64_t* map;            /* open addressing: id << 32 | (index + 1), one load per probe */
     uint32_t map_cap;
     thread_rt* threads;
     uint32_t n_threads;
@@ -112,7 +128,6 @@ struct sg_policy {
     /* round state */
     pthread_mutex_t m;
     pthread_cond_t cv;
-    sg_simtime prepared;      /* barrier the current runs were extracted for */
     int preparing;
     uint32_t arrivals;
     uint64_t gen;
@@ -128,6 +143,11 @@ struct sg_policy {
     int prof;
     int pinned;               /* worker arenas in pinned memory (SG_POLICY_PINNED=1; measured
                                * no faster than pageable ones, so off by default) */
+    /* flush scratch, kept across rounds (no allocation per round) */
+    sgp_rec* ex;
+    uint64_t ex_cap;
+    const sgp_rec** segs;
+    uint64_t* lens;
     double t_gather, t_insert, t_min, t_extract, t_runs;
 };
 
@@ -149,17 +169,28 @@ static uint32_t hash32(uint32_t x) {
 static int64_t host_index(const sg_policy* p, uint32_t id) {
     uint32_t mask = p->map_cap - 1, i = hash32(id) & mask;
     for (;;) {
-        uint32_t v = p->map_val[i];
-        if (v == 0) return -1;
-        if (p->map_key[i] == id) return (int64_t)v - 1;
+        const uint64_t e = p->map[i];
+        if (e == 0) return -1;
+        if ((uint32_t)(e >> 32) == id) return (int64_t)(uint32_t)e - 1;
         i = (i + 1) & mask;
     }
 }
 
-static thread_rt* thread_of(sg_policy* p, uint64_t token) {
+static thread_rt* thread_lookup(sg_policy* p, uint64_t token) {
     for (uint32_t i = 0; i < p->n_threads; i++)
         if (p->threads[i].token == token) return &p->threads[i];
     return NULL;
+}
+
+/* Workers are registered by add_host before any push / pop, so a slot found
+ * (or not) stays valid for the policy's life. */
+static thread_rt* thread_of(sg_policy* p, uint64_t token) {
+    if (tl_uid == p->uid && tl_token == token) return (thread_rt*)tl_slot;
+    thread_rt* t = thread_lookup(p, token);
+    tl_uid = p->uid;
+    tl_token = token;
+    tl_slot = t;
+    return t;
 }
 
 int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
@@ -171,14 +202,18 @@ int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
     sg_policy* p = (sg_policy*)calloc(1, sizeof *p);
     if (!p) return SG_ERR_NOMEM;
     p->prm = *prm;
+    p->uid = __atomic_add_fetch(&g_policy_uid, 1, __ATOMIC_RELAXED);
     p->hosts = (host_rt*)calloc(prm->max_hosts, sizeof(host_rt));
     p->map_cap = 16;
     while (p->map_cap < 2 * prm->max_hosts) p->map_cap <<= 1;
-    p->map_key = (uint32_t*)calloc(p->map_cap, 4);
-    p->map_val = (uint32_t*)calloc(p->map_cap, 4);
-    p->threads = (thread_rt*)calloc(prm->n_threads + 1, sizeof(thread_rt));
+    p->map = (uint64_t*)calloc(p->map_cap, 8);
+    const size_t tbytes = (prm->n_threads + 1) * sizeof(thread_rt);
+    p->threads = (thread_rt*)aligned_alloc(128, tbytes);
+    if (p->threads) memset(p->threads, 0, tbytes);
     p->self_list = (uint32_t*)malloc((size_t)prm->max_hosts * 4);
-    if (!p->hosts || !p->map_key || !p->map_val || !p->threads || !p->self_list) {
+    p->segs = (const sgp_rec**)malloc((prm->n_threads + 1) * sizeof *p->segs);
+    p->lens = (uint64_t*)malloc((prm->n_threads + 1) * sizeof *p->lens);
+    if (!p->hosts || !p->map || !p->threads || !p->self_list || !p->segs || !p->lens) {
         sg_policy_destroy(p);
         return SG_ERR_NOMEM;
     }
@@ -215,15 +250,19 @@ int sg_policy_destroy(sg_policy* p) {
     if (p->threads)
         for (uint32_t i = 0; i < p->n_threads; i++) {
             free(p->threads[i].hosts);
+            free(p->threads[i].pos);
+            free(p->threads[i].gen);
             if (p->pinned) sgp_host_free(p->threads[i].arena);
             else free(p->threads[i].arena);
         }
     free(p->hosts);
-    free(p->map_key);
-    free(p->map_val);
+    free(p->map);
     free(p->threads);
     free(p->foreign);
     free(p->self_list);
+    free(p->ex);
+    free(p->segs);
+    free(p->lens);
     free(p);
     return SG_OK;
 }
@@ -233,7 +272,7 @@ int sg_policy_add_host(sg_policy* p, uint32_t host_id, uint64_t token) {
         sg_set_error("sg_policy_add_host: capacity exceeded or duplicate host %u", host_id);
         return SG_ERR_INVAL;
     }
-    thread_rt* t = thread_of(p, token);
+    thread_rt* t = thread_lookup(p, token);
     if (!t) {
         if (p->n_threads >= p->prm.n_threads) {
             sg_set_error("sg_policy_add_host: more than %u worker threads", p->prm.n_threads);
@@ -245,8 +284,12 @@ int sg_policy_add_host(sg_policy* p, uint32_t host_id, uint64_t token) {
     if (t->n == t->cap) {
         uint32_t nc = t->cap ? 2 * t->cap : 64;
         uint32_t* nh = (uint32_t*)realloc(t->hosts, (size_t)nc * 4);
-        if (!nh) return SG_ERR_NOMEM;
-        t->hosts = nh;
+        if (nh) t->hosts = nh;
+        uint32_t* np = (uint32_t*)realloc(t->pos, (size_t)nc * 4);
+        if (np) t->pos = np;
+        uint32_t* ng = (uint32_t*)realloc(t->gen, (size_t)nc * 4);
+        if (ng) t->gen = ng;
+        if (!nh || !np || !ng) return SG_ERR_NOMEM;
         t->cap = nc;
     }
     uint32_t idx = p->n_hosts++;
@@ -254,17 +297,19 @@ int sg_policy_add_host(sg_policy* p, uint32_t host_id, uint64_t token) {
     memset(h, 0, sizeof *h);
     h->id = host_id;
     h->thread = (uint32_t)(t - p->threads);
+    h->lpos = t->n;
     pthread_mutex_init(&h->lock, NULL);
+    t->pos[t->n] = 0;
+    t->gen[t->n] = 0;
     t->hosts[t->n++] = idx;
     uint32_t mask = p->map_cap - 1, i = hash32(host_id) & mask;
-    while (p->map_val[i]) i = (i + 1) & mask;
-    p->map_key[i] = host_id;
-    p->map_val[i] = idx + 1;
+    while (p->map[i]) i = (i + 1) & mask;
+    p->map[i] = ((uint64_t)host_id << 32) | (idx + 1);
     return SG_OK;
 }
 
 int sg_policy_thread_hosts(sg_policy* p, uint64_t token, uint32_t* ids, uint32_t cap, uint32_t* n) {
-    thread_rt* t = thread_of(p, token);
+    thread_rt* t = thread_lookup(p, token);
     uint32_t c = t ? t->n : 0;
     for (uint32_t i = 0; i < c && i < cap; i++) ids[i] = p->hosts[t->hosts[i]].id;
     if (n) *n = c;
@@ -335,15 +380,17 @@ int sg_policy_push(sg_policy* p, uint64_t token, uint64_t handle, sg_simtime tim
     return rc ? SG_ERR_NOMEM : SG_OK;
 }
 
-/* This round's run of host idx: its length, and run_pos reset on first use. */
+/* This round's run of host idx: its length, and its position (the owner's
+ * pos[] entry) reset on first use. */
 static uint32_t run_len(const sg_policy* p, uint32_t idx) {
     return p->run_off ? p->run_off[idx + 1] - p->run_off[idx] : 0;
 }
-static void run_touch(sg_policy* p, host_rt* h) {
-    if (h->run_gen != p->run_gen) {
-        h->run_gen = p->run_gen;
-        h->run_pos = 0;
+static uint32_t* run_pos(sg_policy* p, thread_rt* t, uint32_t lpos) {
+    if (t->gen[lpos] != p->run_gen) {
+        t->gen[lpos] = p->run_gen;
+        t->pos[lpos] = 0;
     }
+    return &t->pos[lpos];
 }
 
 /* Extract the runs for `barrier` once; other threads wait for the leader. */
@@ -392,21 +439,29 @@ int sg_policy_pop(sg_policy* p, uint64_t token, sg_simtime barrier, uint64_t* ha
         t->cursor = 0;
     }
     while (t->cursor < t->n) {
-        const uint32_t idx = t->hosts[t->cursor];
+        const uint32_t c = t->cursor;
+        const uint32_t idx = t->hosts[c];
         host_rt* h = &p->hosts[idx];
         const uint32_t len = run_len(p, idx);
-        run_touch(p, h);  /* only this thread pops, or pushes self events for, its hosts */
-        if (h->run_pos >= len && h->selfq.n == 0) {
+        uint32_t* rp = run_pos(p, t, c);  /* only this thread pops its hosts */
+        /* self events are pushed by the thread executing the host, its owner
+         * (worker.c:218-234), so the heap needs the lock only when it is not
+         * empty (a push from elsewhere takes it too) */
+        if (__atomic_load_n(&h->selfq.n, __ATOMIC_ACQUIRE) == 0) {
+            if (*rp < len) {
+                *handle_out = p->runs[p->run_off[idx] + (*rp)++].handle;
+                return SG_OK;
+            }
             t->cursor++; /* nothing left this round */
             continue;
         }
         pthread_mutex_lock(&h->lock);
-        const sgp_rec* a = h->run_pos < len ? &p->runs[p->run_off[idx] + h->run_pos] : NULL;
+        const sgp_rec* a = *rp < len ? &p->runs[p->run_off[idx] + *rp] : NULL;
         const sgp_rec* b = (h->selfq.n && h->selfq.a[0].time < barrier) ? &h->selfq.a[0] : NULL;
         uint64_t handle = 0;
         if (a && (!b || rec_less(a, b))) {
             handle = a->handle;
-            h->run_pos++;
+            (*rp)++;
         } else if (b) {
             handle = b->handle;
             sheap_pop(&h->selfq);
@@ -429,21 +484,23 @@ static int flush(sg_policy* p) {
      * and left-over CPU heap entries (few) are gathered into one more segment */
     uint64_t extra = p->nf;
     for (uint32_t k = 0; k < p->n_self; k++) extra += p->hosts[p->self_list[k]].selfq.n;
-    sgp_rec* ex = (sgp_rec*)malloc((extra ? extra : 1) * sizeof(sgp_rec));
-    const sgp_rec** segs = (const sgp_rec**)malloc((p->n_threads + 1) * sizeof *segs);
-    uint64_t* lens = (uint64_t*)malloc((p->n_threads + 1) * sizeof *lens);
-    if (!ex || !segs || !lens) {
-        free(ex);
-        free(segs);
-        free(lens);
-        return SG_ERR_NOMEM;
+    if (extra > p->ex_cap) {  /* grows rarely: foreign pushes and left-over self events are few */
+        uint64_t nc = p->ex_cap ? 2 * p->ex_cap : 1024;
+        while (nc < extra) nc *= 2;
+        sgp_rec* nx = (sgp_rec*)realloc(p->ex, nc * sizeof(sgp_rec));
+        if (!nx) return SG_ERR_NOMEM;
+        p->ex = nx;
+        p->ex_cap = nc;
     }
+    sgp_rec* ex = p->ex;
+    const sgp_rec** segs = p->segs;
+    uint64_t* lens = p->lens;
     for (uint32_t i = 0; i < p->n_threads; i++) {
         segs[i] = p->threads[i].arena;
         lens[i] = p->threads[i].na;
     }
     uint64_t n = 0;
-    memcpy(ex, p->foreign, p->nf * sizeof(sgp_rec));
+    if (p->nf) memcpy(ex, p->foreign, p->nf * sizeof(sgp_rec));
     n += p->nf;
     p->nf = 0;
     for (uint32_t k = 0; k < p->n_self; k++) {
@@ -459,9 +516,6 @@ static int flush(sg_policy* p) {
     double t1 = p->prof ? now_s() : 0;
     int rc = sgp_dev_insert_segs(p->dev, segs, lens, p->n_threads + 1);  /* synchronises */
     for (uint32_t i = 0; i < p->n_threads; i++) p->threads[i].na = 0;   /* arenas reusable */
-    free(ex);
-    free(segs);
-    free(lens);
     if (rc) return rc;
     double t2 = p->prof ? now_s() : 0;
     rc = sgp_dev_min(p->dev, &p->next_min);
@@ -505,8 +559,8 @@ int sg_policy_remaining(sg_policy* p, uint64_t* handles, uint64_t cap, uint64_t*
         host_rt* h = &p->hosts[i];
         for (uint32_t k = 0; k < h->selfq.n; k++, n++)
             if (n < cap) handles[n] = h->selfq.a[k].handle;
-        run_touch(p, h);
-        for (uint32_t k = h->run_pos; k < run_len(p, i); k++, n++)
+        const uint32_t rp = *run_pos(p, &p->threads[h->thread], h->lpos);
+        for (uint32_t k = rp; k < run_len(p, i); k++, n++)
             if (n < cap) handles[n] = p->runs[p->run_off[i] + k].handle;
     }
     uint64_t nd = 0;

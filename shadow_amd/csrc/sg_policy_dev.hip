@@ -26,7 +26,8 @@
 //            k_local   level 2, one workgroup per host block: LDS counting
 //                      sort by host, the block's run offsets off[]
 //            k_xrank   each record ranked in its host's run in event_compare
-//                      order (event.c:110-153)
+//                      order (event.c:110-153); runs longer than XR_SHORT
+//                      are listed for k_xlong (LDS bitonic sort per run)
 //                      (and, on the side, spent buckets reset, their chunks
 //                      freed, the straddling bucket's and far list's minima set)
 //   MIN      k_cmin    over the RB bucket minima and the far minimum
@@ -74,6 +75,8 @@ struct Scal {
     unsigned long long flive;      // remaining far records (scan)
     unsigned long long pmin[RB / 1024];  // k_cmin's partial minima
     unsigned long long nall;       // k_call's count
+    uint32_t nlong;                // runs longer than XR_SHORT (k_xrank lists them for k_xlong)
+    uint32_t pad_;
 };
 
 // One cache line per bucket: the insert's atomics on neighbouring buckets do
@@ -542,16 +545,100 @@ __global__ __launch_bounds__(1024) void k_local(Cal c, uint64_t cur, uint32_t nb
 
 // Each extracted event ranked inside its host's run in event_compare order
 // (event.c:110-153; the keys are unique, srcHostEventID being unique per source).
+// A short run (most hosts: one or a few events) is ranked by one lane per event
+// scanning the run; a longer one (an incast) is listed for k_xlong, which sorts
+// it in LDS, so no lane scans more than XR_SHORT records.
+constexpr uint32_t XR_SHORT = 32;    // longest run ranked by scanning
+constexpr uint32_t XL_SORT = 2048;   // longest run k_xlong sorts in LDS (bitonic)
+constexpr uint32_t XL_T = 1024;      // k_xlong workgroup
+constexpr uint32_t XL_G = 256;       // k_xlong grid (workgroups loop over the list)
 __global__ __launch_bounds__(BLOCK) void k_xrank(const sgp_rec* tmp2, const uint32_t* off,
-                                                 const unsigned long long* total, sgp_rec* out) {
+                                                 const unsigned long long* total, sgp_rec* out, Scal* sc,
+                                                 uint32_t* longl) {
     const uint64_t T = *total;
     for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < T; i += (uint64_t)gridDim.x * BLOCK) {
         const sgp_rec e = tmp2[i];
         const uint32_t s = off[e.dst], f = off[e.dst + 1];
+        if (f - s > XR_SHORT) {
+            if (i == s) longl[atomicAdd(&sc->nlong, 1u)] = e.dst;  // the run's first record lists it
+            continue;
+        }
         uint32_t rank = 0;
         for (uint32_t j = s; j < f; ++j)
             rank += key_less(tmp2[j].time, tmp2[j].src_id, tmp2[j].seq, e.time, e.src_id, e.seq);
         out[s + rank] = e;
+    }
+}
+
+// The long runs k_xrank listed, one workgroup per run: up to XL_SORT records
+// bitonic-sorted in LDS by event_compare key (a padding key above every real
+// one); beyond that (a host receiving thousands of events in one round) each
+// record's rank counted against the run in LDS tiles of XL_SORT.
+__global__ __launch_bounds__(XL_T) void k_xlong(const sgp_rec* tmp2, const uint32_t* off, const Scal* sc,
+                                                const uint32_t* longl, sgp_rec* out) {
+    __shared__ uint64_t s_t[XL_SORT], s_q[XL_SORT];
+    __shared__ uint32_t s_s[XL_SORT];
+    __shared__ uint16_t s_i[XL_SORT];
+    const uint32_t tid = threadIdx.x, nl = sc->nlong;
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {  // uniform per workgroup
+        const uint32_t h = longl[j], s = off[h], k = off[h + 1] - s;
+        __syncthreads();  // the previous run's LDS reads are done
+        if (k <= XL_SORT) {
+            uint32_t P = 64;
+            while (P < k) P <<= 1;
+            for (uint32_t i = tid; i < P; i += XL_T) {
+                const bool v = i < k;
+                const sgp_rec e = tmp2[s + (v ? i : 0)];
+                s_t[i] = v ? e.time : UINT64_MAX;
+                s_s[i] = v ? e.src_id : UINT32_MAX;
+                s_q[i] = v ? e.seq : UINT64_MAX;
+                s_i[i] = (uint16_t)i;
+            }
+            __syncthreads();
+            for (uint32_t size = 2; size <= P; size <<= 1) {
+                for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                    for (uint32_t i = tid; i < P / 2; i += XL_T) {
+                        const uint32_t lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+                        const bool up = (lo & size) == 0;
+                        const bool lt = key_less(s_t[hi], s_s[hi], s_q[hi], s_t[lo], s_s[lo], s_q[lo]);
+                        if (lt == up) {
+                            const uint64_t t = s_t[lo], q = s_q[lo];
+                            const uint32_t a = s_s[lo];
+                            const uint16_t x = s_i[lo];
+                            s_t[lo] = s_t[hi];
+                            s_q[lo] = s_q[hi];
+                            s_s[lo] = s_s[hi];
+                            s_i[lo] = s_i[hi];
+                            s_t[hi] = t;
+                            s_q[hi] = q;
+                            s_s[hi] = a;
+                            s_i[hi] = x;
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            for (uint32_t i = tid; i < k; i += XL_T) out[s + i] = tmp2[s + s_i[i]];
+            continue;
+        }
+        for (uint32_t b = 0; b < k; b += XL_T) {  // every record's rank, tile by tile
+            const bool v = b + tid < k;
+            const sgp_rec e = tmp2[s + (v ? b + tid : 0)];
+            uint32_t rank = 0;
+            for (uint32_t t0 = 0; t0 < k; t0 += XL_SORT) {
+                const uint32_t m = k - t0 < XL_SORT ? k - t0 : XL_SORT;
+                __syncthreads();
+                for (uint32_t i = tid; i < m; i += XL_T) {
+                    const sgp_rec r = tmp2[s + t0 + i];
+                    s_t[i] = r.time;
+                    s_s[i] = r.src_id;
+                    s_q[i] = r.seq;
+                }
+                __syncthreads();
+                for (uint32_t i = 0; i < m; ++i) rank += key_less(s_t[i], s_s[i], s_q[i], e.time, e.src_id, e.seq);
+            }
+            if (v) out[s + rank] = e;
+        }
     }
 }
 
@@ -624,6 +711,7 @@ struct sgp_dev {
     sgp_rec* d_out;      // extracted runs, ranked
     uint64_t out_cap;
     uint32_t* d_off;     // [N + 1] host-ordered run offsets
+    uint32_t* d_long;    // [N] hosts whose run k_xlong ranks
     uint32_t P2;         // host blocks
     uint32_t* d_mat;     // [units][P2] level-1 counts, then bases
     uint32_t* d_pbase;   // [P2 + 1] host block starts
@@ -807,6 +895,7 @@ int sgp_dev_create(int device, uint32_t n_hosts, uint32_t cap, sgp_dev** out) {
     if (!rc) rc = dmalloc((void**)&c.bh, RB * sizeof(BH));
     if (!rc) rc = dmalloc((void**)&c.sc, sizeof(Scal));
     if (!rc) rc = dmalloc((void**)&d->d_off, ((size_t)n_hosts + 1) * 4);
+    if (!rc) rc = dmalloc((void**)&d->d_long, (size_t)n_hosts * 4);
     d->P2 = (n_hosts + HPB - 1) / HPB;
     if (!rc) rc = dmalloc((void**)&d->d_pbase, ((size_t)d->P2 + 1) * 4);
     if (!rc && (hipHostMalloc((void**)&d->h_off, ((size_t)n_hosts + 1) * 4, hipHostMallocDefault) != hipSuccess ||
@@ -841,7 +930,8 @@ int sgp_dev_destroy(sgp_dev* d) {
     if (!d) return 0;
     if (d->s) (void)hipStreamSynchronize(d->s);
     void* dp[] = {d->c.pool, d->c.fst, d->c.btab, d->c.bh, d->c.sc, d->c.far,
-                  d->far2, d->c.items, d->d_in, d->d_rslot, d->d_tmp, d->d_tmp2, d->d_out, d->d_off, d->d_mat, d->d_pbase};
+                  d->far2, d->c.items, d->d_in, d->d_rslot, d->d_tmp, d->d_tmp2, d->d_out, d->d_off, d->d_mat, d->d_pbase,
+                  d->d_long};
     for (void* p : dp)
         if (p) (void)hipFree(p);
     if (d->h_runs) (void)hipHostFree(d->h_runs);
@@ -937,7 +1027,10 @@ int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const ui
     hipLaunchKernelGGL(k_part, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat, d->d_tmp);
     hipLaunchKernelGGL(k_local, dim3(P2), dim3(1024), 0, d->s, d->c, d->cur, nbk, n, P2, d->d_pbase, d->d_tmp,
                        d->d_tmp2, d->d_off);
-    hipLaunchKernelGGL(k_xrank, dim3(XG), dim3(BLOCK), 0, d->s, d->d_tmp2, d->d_off, &d->c.sc->total, d->d_out);
+    PCHK(hipMemsetAsync(&d->c.sc->nlong, 0, 4, d->s));
+    hipLaunchKernelGGL(k_xrank, dim3(XG), dim3(BLOCK), 0, d->s, d->d_tmp2, d->d_off, &d->c.sc->total, d->d_out,
+                       d->c.sc, d->d_long);
+    hipLaunchKernelGGL(k_xlong, dim3(XL_G), dim3(XL_T), 0, d->s, d->d_tmp2, d->d_off, d->c.sc, d->d_long, d->d_out);
     PCHK(hipGetLastError());
     PCHK(hipMemcpyAsync(d->h_off, d->d_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, d->s));
     if ((rc = read_scal(d))) return rc;

@@ -35,6 +35,9 @@ typedef struct wctx {
     uint64_t pops, sends, dropr, drope;
     uint64_t jmin;
     sg_simtime now;
+    /* stage profile (drv.prof): seconds and calls */
+    double t_push, t_pop, t_next, t_exec, t_bar;
+    uint64_t n_push, n_pop;
 } wctx;
 
 struct drv {
@@ -52,11 +55,18 @@ struct drv {
     sg_simtime min_next;
     pthread_mutex_t glock;
     uint64_t bumped;       /* counted by the driver's own bump detection */
+    int prof;              /* stage profile on (sg_sched_result.profile) */
     sg_path_cache* paths;  /* ordered discovery (NULL: the tables' jump_ms) */
     pthread_mutex_t plock; /* the reference's path-cache lock */
     int path_err;
     char path_msg[256];    /* the failing lookup's message (sg_last_error is per thread) */
 };
+
+static double mono_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static uint64_t digest_mix(uint64_t pos, uint64_t time, uint32_t src, uint64_t seq) {
 #define FMIX(z) (z ^= z >> 33, z *= 0xff51afd7ed558ccdULL, z ^= z >> 33, z *= 0xc4ceb9fe1a85ec53ULL, z ^= z >> 33)
@@ -93,7 +103,14 @@ static void sched_push(drv* d, wctx* w, sg_hevent* e, uint32_t src, uint32_t dst
         return;
     }
     sg_simtime before = e->time;
-    d->ops->push(d->ops->data, e, src, dst, d->round_end);
+    if (d->prof) {
+        const double t0 = mono_s();
+        d->ops->push(d->ops->data, e, src, dst, d->round_end);
+        w->t_push += mono_s() - t0;
+        w->n_push++;
+    } else {
+        d->ops->push(d->ops->data, e, src, dst, d->round_end);
+    }
     if (src != dst && before < d->round_end) __atomic_add_fetch(&d->bumped, 1, __ATOMIC_RELAXED);
 }
 
@@ -148,17 +165,30 @@ static void execute(drv* d, wctx* w, sg_hevent* e) {
 }
 
 /* scheduler_pop (scheduler.c:359-414) */
-static sg_hevent* sched_pop(drv* d) {
+static sg_hevent* sched_pop(drv* d, wctx* w) {
     while (d->running) {
+        double t0 = d->prof ? mono_s() : 0;
         sg_hevent* e = d->ops->pop(d->ops->data, d->round_end);
+        if (d->prof) {
+            const double t1 = mono_s();
+            w->t_pop += t1 - t0;
+            w->n_pop++;
+            t0 = t1;
+        }
         if (e) return e;
         pthread_barrier_wait(&d->exec_b);
+        double t1 = d->prof ? mono_s() : 0;
         sg_simtime t = d->ops->get_next_time(d->ops->data);
         pthread_mutex_lock(&d->glock);
         if (t < d->min_next) d->min_next = t;
         pthread_mutex_unlock(&d->glock);
+        double t2 = d->prof ? mono_s() : 0;
         pthread_barrier_wait(&d->collect_b);
         pthread_barrier_wait(&d->prepare_b);
+        if (d->prof) {
+            w->t_next += t2 - t1;
+            w->t_bar += (t1 - t0) + (mono_s() - t2);
+        }
     }
     return NULL;
 }
@@ -183,9 +213,16 @@ static void* worker_run(void* arg) {
     free(mine);
     pthread_barrier_wait(&d->prepare_b);
     sg_hevent* e;
-    while ((e = sched_pop(d)) != NULL) {
-        execute(d, w, e);
-        free(e);
+    while ((e = sched_pop(d, w)) != NULL) {
+        if (d->prof) {  /* the body without its pushes (timed in sched_push) */
+            const double t0 = mono_s(), p0 = w->t_push;
+            execute(d, w, e);
+            free(e);
+            w->t_exec += mono_s() - t0 - (w->t_push - p0);
+        } else {
+            execute(d, w, e);
+            free(e);
+        }
     }
     return NULL;
 }
@@ -217,6 +254,7 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
     d->ops = ops;
     d->nw = n_workers;
     d->paths = paths;
+    d->prof = res && res->profile;
     d->rng = (uint32_t*)malloc((size_t)d->N * 4);
     d->evc = (uint64_t*)calloc(d->N, 8);
     d->pops = (uint64_t*)calloc(d->N, 8);
@@ -264,6 +302,7 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
     struct timespec t0, t1, tm;
     const uint64_t mark_round = res ? res->mark_round : 0;
     uint64_t mark_pops = 0;
+    wctx* snap = d->prof ? (wctx*)calloc(n_workers, sizeof(wctx)) : NULL;  /* profile at the mark */
     pthread_barrier_wait(&d->start_b); /* scheduler_start */
     clock_gettime(CLOCK_MONOTONIC, &t0);
     sg_window_state ws;
@@ -286,6 +325,7 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
         if (mark_round && rounds == mark_round) { /* workers idle between barriers */
             clock_gettime(CLOCK_MONOTONIC, &tm);
             for (uint32_t i = 0; i < n_workers; i++) mark_pops += d->w[i].pops;
+            if (snap) memcpy(snap, d->w, n_workers * sizeof(wctx));
         }
         uint64_t jmin = UINT64_MAX;
         for (uint32_t i = 0; i < n_workers; i++)
@@ -319,7 +359,24 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
             res->marked_pops = res->pops - mark_pops;
             res->marked_rounds = rounds - mark_round;
         }
+        res->profile = d->prof;
+        if (d->prof) {
+            const int since = mark_round && rounds > mark_round;
+            for (uint32_t i = 0; i < n_workers; i++) {
+                const wctx* a = &d->w[i];
+                const wctx z = {0};
+                const wctx* b = since && snap ? &snap[i] : &z;
+                res->prof_push_s += a->t_push - b->t_push;
+                res->prof_pop_s += a->t_pop - b->t_pop;
+                res->prof_next_s += a->t_next - b->t_next;
+                res->prof_exec_s += a->t_exec - b->t_exec;
+                res->prof_barrier_s += a->t_bar - b->t_bar;
+                res->prof_pushes += a->n_push - b->n_push;
+                res->prof_pops += a->n_pop - b->n_pop;
+            }
+        }
     }
+    free(snap);
     if (digest) memcpy(digest, d->digest, (size_t)d->N * 8);
     if (pops) memcpy(pops, d->pops, (size_t)d->N * 8);
     if (rng) memcpy(rng, d->rng, (size_t)d->N * 4);

@@ -38,7 +38,10 @@ class SchedResult(C.Structure):
                [("seconds", C.c_double), ("last_window_start", C.c_uint64),
                 ("last_window_end", C.c_uint64), ("mark_round", C.c_uint64),
                 ("marked_seconds", C.c_double), ("marked_pops", C.c_uint64),
-                ("marked_rounds", C.c_uint64)]
+                ("marked_rounds", C.c_uint64), ("profile", C.c_uint64)] + \
+               [(n, C.c_double) for n in ("prof_push_s", "prof_pop_s", "prof_next_s", "prof_exec_s",
+                                          "prof_barrier_s")] + \
+               [("prof_pushes", C.c_uint64), ("prof_pops", C.c_uint64)]
 
     def as_dict(self):
         return {n: (float if t is C.c_double else int)(getattr(self, n)) for n, t in self._fields_}
@@ -143,7 +146,7 @@ def default_scheduler_seed(cfg: dict) -> int:
 
 def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 62,
               scheduler_seed: int | None = None, free_ops: bool = True,
-              mark_round: int = 0) -> dict:
+              mark_round: int = 0, profile: bool = False) -> dict:
     """Run PHOLD under `ops` with n_workers CPU workers; returns per-host state
     (digest, pops, rng, ev) and the driver's counters/timing."""
     lib = _bind()
@@ -155,6 +158,7 @@ def run_phold(cfg: dict, n_workers: int, ops: PolicyOps, max_rounds: int = 1 << 
     rng = np.zeros(n, np.uint32)
     res = SchedResult()
     res.mark_round = mark_round
+    res.profile = int(profile)
     cache = PathCache(cfg) if cfg.get("discovery") == "ordered" else None
     rc = lib.sg_sched_run_phold_paths(C.byref(p), C.byref(t), cache.h if cache else None, n_workers,
                                       scheduler_seed, C.byref(ops), max_rounds, C.byref(res), dig.ctypes.data,

@@ -128,7 +128,7 @@ def test_glue_phold_matches_oracle(variant, kind, workers):
     assert rep["exact_ids"] == (variant == "exact")
     assert rep["errors"] == 0
     assert rep["live_after_free"] == 0
-    assert rep["unref_at_free"] == st["pending"] == 0  # ran to endTime: nothing left
+    assert rep["unref_at_free"] == st["pending"]  # whatever the run left queued, free unrefs
 
 
 @pytest.mark.gpu

@@ -105,3 +105,24 @@ def test_gpu_policy_ordered_discovery(seed, hosts):
         assert np.array_equal(r["digest"], hs["digest"]) and np.array_equal(r["ev"], hs["ev"]), disc
         runs[disc] = (st["rounds"], st["bumped"])
     assert runs["source"] != runs["ordered"]
+
+
+@pytest.mark.parametrize("n,w0", [(600, 200.0), (3000, 3000.0)])
+def test_gpu_policy_incast(n, w0):
+    """one destination receives a large share of every round's events
+    (weights rule, host 0 weighted w0).  Runs longer than k_xrank's scan bound
+    go to k_xlong: up to 2048 records sorted in LDS (600 hosts: runs up to ~600
+    per round), beyond that ranked in LDS tiles (3000 hosts: runs up to ~5400)."""
+    w = np.ones(n)
+    w[0] = w0
+    cfg = phold.tiny_config(n_hosts=n, V=4, load=8, end_time_s=0.3, loss=0.0, weights=w)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs, st = ref.host_state(), ref.stats()
+    r = policy.run_phold(cfg, 4, policy.gpu_ops(4, cfg["n_hosts"]))
+    assert np.array_equal(r["digest"], rs["digest"])
+    assert np.array_equal(r["pops_per_host"], rs["pops"])
+    assert np.array_equal(r["ev"], rs["ev"])
+    for k in ("rounds", "pops", "sends", "bumped"):
+        assert r[k] == st[k], k
