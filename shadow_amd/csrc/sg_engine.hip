@@ -2051,7 +2051,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // them, and stored into LDS after the scatter
     constexpr uint32_t RQ = (32u << 10) / 4 / K2_T;
     uint32_t vlo = 0, rw[RQ], nwords = 0;
-    auto load_rows = [&]() __attribute__((always_inline)) {
     if constexpr (ROWS) {
         const uint32_t s0 = p * HP, s1 = (p + 1) * HP < d.L ? (p + 1) * HP : d.L;
         vlo = d.sinfo[s0].v;
@@ -2069,10 +2068,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         if (nrow > d.rows_max && tid == 0) flag(d, OV_BUG);  // the host sized rows_max
     }
-    };
-#ifndef SG_X_ROWLATE
-    load_rows();
-#endif
     auto pair_of = [&](uint32_t sv, uint32_t dv, bool wj) __attribute__((always_inline)) {
         if constexpr (ROWS) return lds_pair(d, s_rows, vlo, sv, dv, wj);
         else return load_pair(d, sv, dv, wj);
@@ -2114,9 +2109,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     __syncthreads();
-#ifdef SG_X_ROWLATE
-    load_rows();  // experiment: the rows after the partition records and the histogram
-#endif
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
@@ -2416,9 +2408,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             uint64_t pops_end;  // the host's pops after the round (its last event writes it)
             uint64_t sq;        // this send's srcHostEventID
             uint64_t term;      // digest term; one-event host: the new digest
-#ifdef SG_X_PIPE
-            uint64_t pos, dold, key;  // the digest term's inputs (computed under the loads)
-#endif
         };
         // stage 1: place in the host's order, replay, draws (LDS and ALU only)
         auto flat_draw = [&](const Rec& ev, bool valid, ulonglong2 w01, ulonglong2 w23)
@@ -2454,14 +2443,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.bt = S + et;
             const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
             const uint64_t bseq = ev.k & SEQ_MASK;
-#ifdef SG_X_PIPE
-            f.pos = pops0 + sc.rank;
-            f.dold = sc.rank + 1 == cnt ? w23.x : 0;
-            f.key = ev.k;
-#else
             f.term = (SG_ABL & 32) ? f.bt ^ bseq : digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
             if (sc.rank + 1 == cnt) f.term += w23.x;  // the last event: the old digest + its term
-#endif
             if (d.trace) {
                 const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
                 if (ts < d.trace_cap) {
@@ -2536,22 +2519,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         };
         const bool stf = stamp && tid == 0;
         if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
-#ifdef SG_X_PIPE
-        FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
-        FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
-#else
         const FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
         const FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
-#endif
-#ifdef SG_X_PIPE
-        // experiment: the digest terms computed after the destination loads are issued
-        auto flat_term = [&](FlatEv& f) __attribute__((always_inline)) {
-            if (!(f.flags & F_OK)) return;
-            const uint32_t bsrc = (uint32_t)(f.key >> SRC_SHIFT);
-            const uint64_t bseq = f.key & SEQ_MASK;
-            f.term = digest_mix(f.pos, f.bt, bsrc, bseq) + f.dold;
-        };
-#endif
         if (stf) stamp[17] = wait_stamp();
         // stage 2: both events' destination records in flight together
         // (unconditional loads; an unused one reads record 0's line), resolved
@@ -2567,18 +2536,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             } else {
                 const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
                 const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
-#ifdef SG_X_PIPE
-                flat_term(f0);
-                flat_term(f1);
-#endif
                 near_resolve(d, f0.x, a0, b0, vd0, dst0);
                 near_resolve(d, f1.x, a1, b1, vd1, dst1);
             }
         } else {
-#ifdef SG_X_PIPE
-            flat_term(f0);
-            flat_term(f1);
-#endif
             const Probe pb0 = dst_probe(d, f0.g), pb1 = dst_probe(d, f1.g);
             dst0 = (f0.flags & F_OK) && (f0.flags & F_SND) ? dst_resolve(d, f0.x, f0.g, pb0, vd0) : 0u;
             dst1 = (f1.flags & F_OK) && (f1.flags & F_SND) ? dst_resolve(d, f1.x, f1.g, pb1, vd1) : 0u;
