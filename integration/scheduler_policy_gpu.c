@@ -25,7 +25,10 @@
  *
  * tests/test_integration_glue.py compiles this file against the unmodified
  * reference headers (and conda GLib) whenever /root/reference is present, and
- * runs it under AddressSanitizer through tests/glue_harness.c.
+ * runs it under AddressSanitizer through tests/glue_harness.c (test doubles).
+ * tests/glue_phold.c links it to the real libshadowgpu.so, and
+ * tests/test_gpu_glue.py runs PHOLD through its vtable on the GPU against the
+ * oracle.
  */
 #include <glib.h>
 #include <pthread.h>

@@ -290,7 +290,7 @@ struct Dev {
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
-    uint32_t check;           // SG_CHECK=1: k_scatter's planner re-derives the sent headers' MIN terms (debug)
+    uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
     const PairRec* pairs;     // [V*V] full records (PAIR_WIDE), else null
     const uint2* pairs8;      // [V*V] {delay, keep} (PAIR_NARROW)
     const uint32_t* pdelay;   // [V*V] delay only (PAIR_DELAY: every pair keeps every packet)
@@ -2960,40 +2960,30 @@ __device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uin
     }
 }
 
-// The planner (one thread) waits until the n other workgroups have read the
-// round state, then publishes.  Every workgroup of the grid runs to its
-// arrival without waiting for anything, so the wait ends; it is bounded all
-// the same (a missed arrival is reported as OV_BUG, never a hang).
-__device__ void plan_when_read(const Dev& d, int mode, const StepView& sv, const int64_t* recv, uint32_t n) {
-    uint64_t* ctr = &d.rs->splan;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
-        if (++spins > (1u << 22)) {
-            flag(d, OV_BUG);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    publish_step(d, mode, sv, recv);
-}
-
 // mode: 0 one shard (after k_proc), 1 several shards (after the all-to-all; recv the
 // exchange blocks), 2 boot.  Every workgroup plans the step (step_view) from
-// the state as the previous kernels left it and reports that it has read it
-// (a fire-and-forget arrival); the last workgroup (the rmin role) publishes
-// the plan (publish_step) once every other one has arrived.
+// the state as the previous kernels left it, then arrives on a counter once its
+// reads of that state have returned; the last to arrive publishes the plan
+// (publish_step).  Nothing waits for anything: no workgroup depends on another
+// being resident, whatever the order the hardware dispatches them in.
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, int mode) {
     RoundState* rs = d.rs;
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     __shared__ StepView sv;
+#ifdef SG_X_GFIRST
+    // experiment: the gather workgroups take the lowest block indices (dispatched first)
+    const uint32_t g0x = d.P + (recv ? d.G3 : 0), bx = blockIdx.x;
+    const uint32_t R = d.R, tid = threadIdx.x,
+                   blk = bx < d.G1 ? g0x + bx : (bx < d.G1 + g0x ? bx - d.G1 : bx);
+#else
     const uint32_t R = d.R, blk = blockIdx.x, tid = threadIdx.x;
-    const bool planner = blk == gridDim.x - 1;
+#endif
     if (tid == 0) {
         step_view(d, mode, recv, sv);
-        if (!sv.quit && !planner) {
+        if (!sv.quit) {
             // every read of the round state has returned before the arrival
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            atomicAdd((unsigned long long*)&rs->splan, 1ull);
+            if (atomicAdd((unsigned long long*)&rs->splan, 1ull) == gridDim.x - 1) publish_step(d, mode, sv, recv);
         }
     }
     // Insert role: what does not depend on the window is loaded while thread 0
@@ -3004,8 +2994,10 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     if (blk < d.P) {  // uniform
         const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
         pre_n = d.rcnt[blk];
+#ifndef SG_X_NOPRE
 #pragma unroll
         for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[threadIdx.x + q * K3_T]);
+#endif
         uint32_t* s_cur = (uint32_t*)lds;
         uint32_t* s_pc = s_cur + RMAX;
         const uint32_t* wb = d.wbase + (size_t)blk * R;
@@ -3051,10 +3043,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         // launch changes only the straddling bucket's minimum, so the minima
         // read are final.  No new window: the current value carries over.
         if (!sv.listed) {
-            if (tid == 0) {
-                rs->rmin2[sv.cur ^ 1] = sv.rmin0;
-                plan_when_read(d, mode, sv, recv, gridDim.x - 1);
-            }
+            if (tid == 0) rs->rmin2[sv.cur ^ 1] = sv.rmin0;
             return;
         }
         const uint64_t bS = sv.bS, bL = sv.bL, pbS = sv.pbS, pbL = sv.pbL;
@@ -3070,7 +3059,6 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         mn = block_min(mn, s16);  // barriers inside
         if (tid == 0) {
             rs->rmin2[sv.cur ^ 1] = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
-            plan_when_read(d, mode, sv, recv, gridDim.x - 1);
             if (st) st[3] = __builtin_amdgcn_s_memrealtime();
         }
         return;
@@ -3170,10 +3158,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             st[5] = n;
         }
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+#ifndef SG_X_NOPRE
             if (i0 == 0) {  // uniform
 #pragma unroll
                 for (int q = 0; q < SU; ++q) r[q] = pre[q];
-            } else {
+            } else
+#endif
+            {
 #pragma unroll
                 for (int q = 0; q < SU; ++q) {
                     const uint32_t i = i0 + threadIdx.x + q * K3_T;
@@ -3545,7 +3536,9 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.R = (uint32_t)(span / W + 3);
     d.ring32 = (uint64_t)d.R * W < (1ull << 32);
     d.wdiv = make_div32(W);
-    d.G3 = env_u32("SG_INS_GRID", 128);
+    // the receive role's workgroups: none on one shard (a world-1 step receives
+    // only its own header block)
+    d.G3 = env_u32("SG_INS_GRID", p.shard_count > 1 ? 128 : 0);
     // default event slots per host: PHOLD keeps `load` events per host in flight;
     // gossip floods keep about ten fan-outs' worth (configs[4]: 82 per host at peak)
     const uint64_t qc = p.queue_cap ? p.queue_cap
