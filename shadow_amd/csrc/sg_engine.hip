@@ -260,6 +260,24 @@ struct RoundState {
     uint64_t recv_ok;    // a several-shard k_scatter read the receive buffer: the next k_proc stages it
 };
 
+// The gather's due list, guessed one kernel ahead.  In steady state a window
+// is one whole bucket, the one after the window being executed (the barrier
+// bump puts events at exactly its end, which becomes the next start), and the
+// chunk ids of that bucket's slots written before the step are final when
+// k_proc starts.  So one k_proc workgroup copies them here, and k_scatter's
+// gather workgroups load their chunk ids beside the round state instead of
+// after it (bucket words, a scan, the chunk table: two dependent round trips
+// fewer), then check the guess against the window they planned.
+constexpr uint32_t NSPEC = 1024;  // chunk ids kept (a million events)
+struct GSpec {
+    uint64_t fold;  // the step it is for (rs->fold while that k_proc ran); UINT64_MAX: none
+    uint64_t b;     // the bucket (absolute)
+    uint32_t lo;    // its slots written before the step (bw[fold & 1])
+    uint32_t nid;   // chunk ids below: ceil(lo / CH)
+    uint32_t ids[NSPEC];
+};
+static_assert(offsetof(GSpec, ids) == 24, "ids follow three words");
+
 struct Dev {
     uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
     // gossip workload (SG_WORKLOAD_GOSSIP): keys carry the message id in their
@@ -317,6 +335,7 @@ struct Dev {
     uint32_t* stash;          // [P + G3][ST] chunk ids each reserving row keeps at hand
     uint32_t* stn;            // [P + G3] ids in the row's stash
     uint32_t* wbase;          // [P + G3][R] reserved base per (row, bucket) in the row's sub-list
+    GSpec* gspec;             // the next gather's guessed due list (k_proc -> k_scatter)
     // partitions
     uint32_t* pcnt;           // [P] due events of the partition this round
     Rec* part;                // [P][CAPP]
@@ -943,14 +962,35 @@ __device__ __forceinline__ DueEnt due_entry(const Dev& d, const DueList& dl, con
 // only the slots written before this launch ("old" slots); the same launch's
 // insert workgroups route the new due events themselves, so the two never
 // touch the same slot.
-constexpr size_t GATHER_LDS = (2 * PMAX) * 4 + GDMAX * sizeof(DueEnt) + 16 * 8 + 2 * SEGMAX * 4;
+constexpr size_t GDE_OFF = (2 * PMAX) * 4;  // s_de's offset in the gather role's LDS
+constexpr size_t GATHER_LDS = GDE_OFF + GDMAX * sizeof(DueEnt) + 16 * 8 + 2 * SEGMAX * 4;
+constexpr uint32_t GSPEC_N = 4;  // chunks per gather workgroup on the GSpec path (the one-pass capacity)
+// Gather workgroup w of nw, its wave 1 at launch (beside the round state): the
+// GSpec header words into s_gsw and the workgroup's entries w + k * nw (k <
+// GSPEC_N) of the guessed due list into s_de, one load per lane.
+__device__ __forceinline__ void gspec_load(const Dev& d, uint32_t w, uint32_t nw, uint64_t* s_gsw, DueEnt* s_de) {
+    const uint32_t k = threadIdx.x & 63;
+    const uint32_t i = w + (k >= 3 ? k - 3 : 0) * nw, ic = i < NSPEC ? i : 0u;
+    const uint32_t wi = k < 3 ? k : (k < 3 + GSPEC_N ? 3 + (ic >> 1) : 0u);
+    const uint64_t v = reinterpret_cast<const uint64_t*>(d.gspec)[wi];
+    const uint64_t b = __shfl(v, 1, 64), ln = __shfl(v, 2, 64);
+    if (k < 3) {
+        s_gsw[k] = v;
+    } else if (k < 3 + GSPEC_N) {
+        const uint32_t lo = (uint32_t)ln, nid = (uint32_t)(ln >> 32);
+        const bool ok = i < nid && i < NSPEC;
+        const uint32_t left = ok ? lo - i * CH : 0u;
+        s_de[k - 3] = DueEnt{ok ? (uint32_t)(v >> ((ic & 1) * 32)) : EMPTY, left < CH ? left : CH, b * d.W};
+    }
+}
 template <int GT>
 __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32_t nw, unsigned char* lds,
-                            uint64_t* st) {
+                            const uint64_t* s_gsw, uint64_t* st) {
     constexpr int GR = 4 * (int)CH / GT;
+    static_assert(GR * GT == (int)(GSPEC_N * CH), "the one-pass path holds GSPEC_N chunks");
     uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
     uint32_t* s_cur = s_cnt + PMAX;                        // [PMAX]
-    DueEnt* s_de = (DueEnt*)(s_cur + PMAX);                // [GDMAX]
+    DueEnt* s_de = (DueEnt*)(lds + GDE_OFF);               // [GDMAX]
     uint64_t* s16 = (uint64_t*)(s_de + GDMAX);             // [16]
     uint32_t* s_start = (uint32_t*)(s16 + 16);             // [SEGMAX] the due list's segments
     uint32_t* s_lo = s_start + SEGMAX;                     // [SEGMAX]
@@ -964,6 +1004,101 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
         s_cnt[p] = 0;
         s_cur[p] = 0;
     }
+    uint64_t cmin = UINT64_MAX, ntomb = 0, ng = 0;  // ng: events moved (C_GATHER)
+    auto reserve = [&]() {  // one reservation per partition this workgroup feeds
+        for (uint32_t p = threadIdx.x; p < P; p += GT) {
+            const uint32_t c = s_cnt[p];
+            if (c) {
+                const uint32_t base = atomicAdd(&d.pcnt[p], c);
+                if (base + c > d.CAPP) flag(d, OV_PART);
+                s_cnt[p] = base;
+            }
+        }
+    };
+    // The workgroup's chunks s_de[0, nb) (nb <= GSPEC_N, visible to every
+    // thread) in registers: load once, count, reserve, scatter.  mid() runs
+    // between the count and the reservations.
+    auto one_pass = [&](uint32_t nb, auto&& mid) __attribute__((always_inline)) {
+        const uint32_t tot = nb * CH;
+        Rec r[GR];
+        uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {  // every load unconditional (clamped address)
+            const uint32_t e = threadIdx.x + q * GT;
+            const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
+            const bool v = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
+            r[q] = ld_stream(&d.pool[v ? ((size_t)de.id << CH_SHIFT) + (e & (CH - 1)) : 0]);
+            if (!v) r[q].a = TOMB;
+        }
+        lds_barrier();  // s_cnt / s_cur zeroed
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {
+            pp[q] = UINT32_MAX;
+            if (r[q].a == TOMB) continue;
+            const uint32_t e = threadIdx.x + q * GT;
+            const uint64_t t = s_de[e >> CH_SHIFT].base + (r[q].a & M40);
+            const uint32_t dl = (uint32_t)(r[q].a >> 40);
+            if (dl >= d.L) {
+                flag(d, OV_BUG);
+                continue;
+            }
+            if (t >= E) {
+                cmin = t < cmin ? t : cmin;
+                continue;
+            }
+            pp[q] = part_of(d, dl);
+            r[q].a = ((uint64_t)(dl - pp[q] * d.HP) << 52) | (t - S);  // the partition record
+            atomicAdd(&s_cnt[pp[q]], 1u);
+        }
+        lds_barrier();
+        if (st) st[2] = __builtin_amdgcn_s_memrealtime();
+        mid();
+        reserve();
+        lds_barrier();
+        if (st) st[6] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {
+            if (pp[q] == UINT32_MAX) continue;
+            const uint32_t p = pp[q];
+            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
+            ++ng;
+            if (slot < d.CAPP) st_stream(&d.part[(size_t)p * d.CAPP + slot], r[q]);
+            const uint32_t e = threadIdx.x + q * GT;
+            const DueEnt de = s_de[e >> CH_SHIFT];
+            if (de.nflags & RETAINED) {
+                d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
+                ++ntomb;
+            }
+        }
+    };
+    // The GSpec path: the window is the one whole bucket the k_proc before
+    // guessed, and s_de holds this workgroup's entries w + k * nw of its
+    // written chunks already.  Every chunk of the bucket (the slots reserved
+    // since included: their due events were routed by the insert role) goes
+    // back to the ring, entry i at tail + i, as the list path would put it.
+    const uint64_t gb = s_gsw[1];
+    const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
+    const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
+    if (XS == 1 && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb && sv.ret == UINT64_MAX && !spent &&
+        gnid <= GSPEC_N * nw) {  // uniform
+        const uint32_t row = (uint32_t)(gb % d.R);
+        const uint32_t hi = d.bk[row];  // in flight under the pool loads
+        if (st) st[1] = __builtin_amdgcn_s_memrealtime();
+        one_pass(GSPEC_N, [&]() __attribute__((always_inline)) {
+            const uint32_t nd = (hi + CH - 1) >> CH_SHIFT;
+            if (w == 0 && threadIdx.x == 0) d.rs->nfree2[sv.cur ^ 1] = nd;
+            if (st) {
+                st[5] = nd;
+                st[7] = 1;
+            }
+            for (uint32_t i = w + threadIdx.x * nw; i < nd; i += GT * nw) {
+                const uint32_t id = threadIdx.x < GSPEC_N && i < gnid ? s_de[threadIdx.x].id
+                                                                     : d.btab[(size_t)row * d.NCH + i];
+                const uint32_t pos = tail_r + i;  // i < NCH: one wrap at most
+                d.fring[pos >= d.NCH ? pos - d.NCH : pos] = id;
+            }
+        });
+    } else {
     DueList dl;
     uint64_t nfree;
     const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree);  // barriers inside
@@ -985,79 +1120,17 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
         const uint64_t pos = tail_r + i;  // i < NCH: one wrap at most
         d.fring[pos >= d.NCH ? pos - d.NCH : pos] = de.id;
     };
-    for (uint32_t p = threadIdx.x; p < P; p += GT) {
-        s_cnt[p] = 0;
-        s_cur[p] = 0;
-    }
-    uint64_t cmin = UINT64_MAX, ntomb = 0, ng = 0;  // ng: events moved (C_GATHER)
-    auto reserve = [&]() {  // one reservation per partition this workgroup feeds
-        for (uint32_t p = threadIdx.x; p < P; p += GT) {
-            const uint32_t c = s_cnt[p];
-            if (c) {
-                const uint32_t base = atomicAdd(&d.pcnt[p], c);
-                if (base + c > d.CAPP) flag(d, OV_PART);
-                s_cnt[p] = base;
-            }
-        }
-    };
     if ((c1 - c0) * CH <= (uint64_t)GR * GT) {
         // the workgroup's chunks fit in registers: load once, count, reserve, scatter
-        const uint32_t nb = (uint32_t)(c1 - c0), tot = nb * CH;
+        const uint32_t nb = (uint32_t)(c1 - c0);
         if (threadIdx.x < nb) {
             const DueEnt de = due_entry(d, dl, s_start, s_lo, (uint32_t)(c0 + threadIdx.x));
             s_de[threadIdx.x] = de;
             free_chunk(de, c0 + threadIdx.x);
         }
-        __syncthreads();
+        lds_barrier();
         if (st) st[1] = __builtin_amdgcn_s_memrealtime();
-        Rec r[GR];
-        uint32_t pp[GR];  // partition of the event, UINT32_MAX: not gathered
-#pragma unroll
-        for (int q = 0; q < GR; ++q) {  // every load unconditional (clamped address)
-            const uint32_t e = threadIdx.x + q * GT;
-            const DueEnt de = s_de[(e < tot ? e : 0) >> CH_SHIFT];
-            const bool v = e < tot && de.id < d.NCH && (e & (CH - 1)) < (de.nflags & 0xFFFFu);
-            r[q] = ld_stream(&d.pool[v ? ((size_t)de.id << CH_SHIFT) + (e & (CH - 1)) : 0]);
-            if (!v) r[q].a = TOMB;
-        }
-#pragma unroll
-        for (int q = 0; q < GR; ++q) {
-            pp[q] = UINT32_MAX;
-            if (r[q].a == TOMB) continue;
-            const uint32_t e = threadIdx.x + q * GT;
-            const uint64_t t = s_de[e >> CH_SHIFT].base + (r[q].a & M40);
-            const uint32_t dl = (uint32_t)(r[q].a >> 40);
-            if (dl >= d.L) {
-                flag(d, OV_BUG);
-                continue;
-            }
-            if (t >= E) {
-                cmin = t < cmin ? t : cmin;
-                continue;
-            }
-            pp[q] = part_of(d, dl);
-            r[q].a = ((uint64_t)(dl - pp[q] * d.HP) << 52) | (t - S);  // the partition record
-            atomicAdd(&s_cnt[pp[q]], 1u);
-        }
-        __syncthreads();
-        if (st) st[2] = __builtin_amdgcn_s_memrealtime();
-        reserve();
-        __syncthreads();
-        if (st) st[6] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-        for (int q = 0; q < GR; ++q) {
-            if (pp[q] == UINT32_MAX) continue;
-            const uint32_t p = pp[q];
-            const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
-            ++ng;
-            if (slot < d.CAPP) st_stream(&d.part[(size_t)p * d.CAPP + slot], r[q]);
-            const uint32_t e = threadIdx.x + q * GT;
-            const DueEnt de = s_de[e >> CH_SHIFT];
-            if (de.nflags & RETAINED) {
-                d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
-                ++ntomb;
-            }
-        }
+        one_pass(nb, []() {});
     } else {
         // more chunks than registers hold (the boot round): two passes over them
         for (uint64_t cb = c0; cb < c1; cb += GDMAX) {
@@ -1081,6 +1154,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
     }
+    }  // the list path
     uint64_t m = cmin, nt = ntomb, gn = ng;
     block_tail3(m, nt, gn);
     if (threadIdx.x == 0) {
@@ -1528,11 +1602,21 @@ __device__ __forceinline__ uint64_t rmw_read(uint64_t* p) {
     return atomicAdd((unsigned long long*)p, 0ull);
 }
 
-// mode 0: one shard, after k_proc; 1: several shards, after the all-to-all (recv:
-// the exchange blocks); 2: boot (the first window is listed already).  One
-// thread.
-__device__ void step_view(const Dev& d, int mode, const int64_t* recv, StepView& sv) {
-    const RoundState* rs = d.rs;
+// A 64-bit value of lane i (wave-uniform i), and a round state field's word.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)i) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)i);
+}
+#define RSF(f) ((uint32_t)(offsetof(RoundState, f) / 8))
+
+// mode 0: one shard, after k_proc; 1: several shards, after the all-to-all
+// (hdr: the G blocks' HDR_W header words, LDS); 2: boot (the first window is
+// listed already).  One thread, from the LDS copy of the round state
+// (load_round_state), so no load of it waits for another.
+constexpr uint32_t HDR_W = HDR * 3;  // header words per exchange block
+constexpr uint32_t RSW = sizeof(RoundState) / 8;
+static_assert(sizeof(RoundState) % 8 == 0 && RSW <= 64, "one word per lane of a wave");
+__device__ void step_view(const Dev& d, int mode, const RoundState* rs, const int64_t* hdr, StepView& sv) {
     const uint64_t W = d.W;
     sv.quit = rs->done != 0;
     sv.fold = rs->fold;
@@ -1573,7 +1657,7 @@ __device__ void step_view(const Dev& d, int mode, const int64_t* recv, StepView&
     } else if (mode == 1) {
         uint64_t more = 0;
         for (uint32_t p = 0; p < d.G; ++p) {
-            const int64_t* blk = recv + (size_t)p * d.xrows * 3;
+            const int64_t* blk = hdr + (size_t)p * HDR_W;
             more |= (uint64_t)blk[H_MORE];
             const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
             m = bm < m ? bm : m;
@@ -1606,6 +1690,30 @@ __device__ void step_view(const Dev& d, int mode, const int64_t* recv, StepView&
         sv.bL = (w.E - 1) / W;
         sv.ret = w.E < (sv.bL + 1) * W ? sv.bL : UINT64_MAX;
     }
+}
+
+// The round state as the previous kernels left it and, with several shards,
+// the G blocks' header words, copied into LDS with one load per lane (a chain
+// of dependent scalar loads of the round state cost about a microsecond per
+// link).  Every lane of wave 0.
+__device__ __forceinline__ void load_round_state(const Dev& d, int mode, const int64_t* recv, uint64_t* s_rsw,
+                                                 int64_t* s_hdr) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t v = reinterpret_cast<const uint64_t*>(d.rs)[lane < RSW ? lane : 0u];
+    constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
+    int64_t h[HPL];
+    if (mode == 1) {  // uniform
+        const uint32_t nh = d.G * HDR_W;
+#pragma unroll
+        for (uint32_t q = 0; q < HPL; ++q) {
+            const uint32_t i = lane + q * 64, j = i < nh ? i : 0u;
+            h[q] = recv[(size_t)(j / HDR_W) * d.xrows * 3 + j % HDR_W];
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < HPL; ++q)
+            if (lane + q * 64 < nh) s_hdr[lane + q * 64] = h[q];
+    }
+    if (lane < RSW) s_rsw[lane] = v;
 }
 
 // The last workgroup to read the round state writes the plan (one thread).
@@ -1917,13 +2025,72 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
 #ifndef SG_ABL
 #define SG_ABL 0
 #endif
+// The next gather's guessed due list (GSpec): when this window ends on a
+// bucket boundary, the next one most likely is that bucket, whole.  Its slots
+// written before the step are bw[fold & 1] (the last k_scatter's copy) and
+// their chunks were allocated before that k_scatter, so their ids are final
+// now (this launch's reservations append beyond them).  One workgroup, every
+// thread; the loads go out together.
+__device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_t E) {
+    const uint64_t b = E / d.W;
+    const bool guess = XS == 1 && b * d.W == E;
+    const uint32_t row = (uint32_t)(b % d.R), i = threadIdx.x;
+    const uint32_t lo = d.bw[(size_t)(fold & 1) * XS * d.R + row];
+    const uint32_t id = d.btab[(size_t)row * d.NCH + (i < d.NCH ? i : 0u)];
+    const uint32_t nid = (lo + CH - 1) >> CH_SHIFT;
+    GSpec* g = d.gspec;
+    if (guess && i < nid && i < NSPEC) g->ids[i] = id;
+    if (i == 0) {
+        g->fold = guess && nid <= NSPEC ? fold : UINT64_MAX;
+        g->b = b;
+        g->lo = lo;
+        g->nid = nid;
+    }
+}
+
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
 template <bool EXACT, bool ROWS, bool FLAT>
 __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     RoundState* rs = d.rs;
-    if (rs->done) return;
+    const uint32_t p = blockIdx.x;
+    const uint32_t tid = threadIdx.x;
+    // One batch of loads before anything waits: the round state, one word per
+    // lane of every wave (its fields then come by readlane), and what the
+    // partition needs from nothing else (its first records, count, chunk
+    // stash, slot range).  Read field by field, the round state was a chain of
+    // dependent scalar loads in front of the partition's loads.
+    const uint64_t rsv = reinterpret_cast<const uint64_t*>(rs)[(tid & 63) < RSW ? (tid & 63) : 0u];
+    const Rec* part = d.part + (size_t)p * d.CAPP;
+    // the first SPEC records per lane are loaded before the count arrives
+    // (CAPP >= SPEC * K2_T; records past the count are ignored)
+    constexpr uint32_t SPEC = 2;
+    constexpr uint32_t EPTF = FLAT ? SPEC : EPT;
+    Rec rr[EPTF];
+#pragma unroll
+    for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
+    const uint32_t n_raw = d.pcnt[p];
+    // the partition's chunk stash (reserve_buckets), loaded now, used at the end
+    const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
+    uint32_t v_first = 0, v_last = 0;  // ROWS: the partition's first and last slots' vertices
+    if constexpr (ROWS) {
+        const uint32_t s0 = p * d.HP, s1 = (p + 1) * d.HP < d.L ? (p + 1) * d.HP : d.L;
+        v_first = d.sinfo[s0].v;
+        v_last = d.sinfo[s1 - 1].v;
+    }
+    auto rsf = [&](uint32_t w) __attribute__((always_inline)) { return readlane64(rsv, w); };
+    // a use of those loads on the paths that do not need them keeps the
+    // compiler from sinking them below the branches (and so behind the wait)
+    auto pin = [&]() __attribute__((always_inline)) {
+        asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_raw), "v"(stash_id), "v"(stash_n), "v"(v_first),
+                     "v"(v_last));
+    };
+    if (rsf(RSF(done))) {
+        pin();
+        return;
+    }
+    const uint64_t rs_fold = rsf(RSF(fold)), rs_bS = rsf(RSF(bS));
     extern __shared__ __align__(16) unsigned char dyn[];
     const uint32_t HP = d.HP, R = d.R;
     uint32_t* s_n = (uint32_t*)dyn;             // [HP] events per host
@@ -1944,15 +2111,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ uint32_t s_roff[MAXG];  // received blocks' offsets (stage_received)
     __shared__ uint32_t s_ids[ST];
     __shared__ uint64_t s_h;
-    const uint64_t S = rs->S, E = rs->E;
+    const uint64_t S = rsf(RSF(S)), E = rsf(RSF(E));
     // several shards: stage the previous step's received events this step
     // (k_scatter routed those due in this window when it planned it: listed)
-    const bool stage_recv = d.xrecv && rs->recv_ok;
-    const bool recv_routed = rs->listed != 0;
-    const bool want_jump = rs->jmin > d.gjmin;  // discovery can still lower the window's jump
-    const uint32_t p = blockIdx.x;
-    const uint32_t tid = threadIdx.x;
-    if (rs->phase) {
+    const bool stage_recv = d.xrecv && rsf(RSF(recv_ok));
+    const bool recv_routed = rsf(RSF(listed)) != 0;
+    const bool want_jump = rsf(RSF(jmin)) > d.gjmin;  // discovery can still lower the window's jump
+    const uint64_t ring_end = rsf(RSF(fl_tail)) + rsf(RSF(nfree2) + (uint32_t)(rs_fold & 1));  // the last gather freed nfree more
+    if (rsf(RSF(phase))) {
+        pin();
         // drain step: outbox leftovers into the exchange blocks; the previous
         // step's received events staged and reserved (no window was planned,
         // so none was routed).  The headers repeat the process step's MIN
@@ -1964,9 +2131,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         if (!stage_recv) return;  // uniform
         const uint32_t R = d.R;
-        const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
-        const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];
-        const uint64_t bS = rs->bS, bSW = bS * d.W;
+        const uint64_t bS = rs_bS, bSW = bS * d.W;
         const uint32_t bSr = (uint32_t)(bS % R);
         uint32_t* s_bc = (uint32_t*)(dyn + d.bin_off);
         uint32_t* s_bm = s_bc + R;
@@ -1993,19 +2158,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
-    const Rec* part = d.part + (size_t)p * d.CAPP;
-    // the first SPEC records per lane are loaded before the count arrives
-    // (CAPP >= SPEC * K2_T; records past the count are ignored)
-    constexpr uint32_t SPEC = 2;
-    constexpr uint32_t EPTF = FLAT ? SPEC : EPT;
-    Rec rr[EPTF];
-#pragma unroll
-    for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
-    uint32_t n = d.pcnt[p];
-    n = n < d.CAPP ? n : d.CAPP;
-    // the partition's chunk stash (reserve_buckets), loaded now, used at the end
-    const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
-    const uint64_t ring_end = rs->fl_tail + rs->nfree2[rs->fold & 1];  // the last gather freed nfree more
+    const uint32_t n = n_raw < d.CAPP ? n_raw : d.CAPP;
     // flat pass: a host's digest terms of its events but the last, summed in
     // LDS over s_vh / s_sb (phase A's arrays, free until phase A runs)
     unsigned long long* s_dig = reinterpret_cast<unsigned long long*>(s_vh);
@@ -2052,9 +2205,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     constexpr uint32_t RQ = (32u << 10) / 4 / K2_T;
     uint32_t vlo = 0, rw[RQ], nwords = 0;
     if constexpr (ROWS) {
-        const uint32_t s0 = p * HP, s1 = (p + 1) * HP < d.L ? (p + 1) * HP : d.L;
-        vlo = d.sinfo[s0].v;
-        const uint32_t nrow = d.sinfo[s1 - 1].v - vlo + 1;
+        vlo = v_first;
+        const uint32_t nrow = v_last - vlo + 1;
         const uint32_t wpe = d.pair_fmt == PAIR_NARROW ? 2u : 1u;  // words per record
         nwords = (nrow < d.rows_max ? nrow : d.rows_max) * d.V * wpe;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(d.prow) + (size_t)vlo * d.V * wpe;
@@ -2072,6 +2224,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if constexpr (ROWS) return lds_pair(d, s_rows, vlo, sv, dv, wj);
         else return load_pair(d, sv, dv, wj);
     };
+    static_assert(K2_T >= NSPEC, "one GSpec id per thread");
+    if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
     if (stamp && tid == 0) stamp[20] = wait_stamp();
     __syncthreads();
     if (in_lds) {
@@ -2201,7 +2355,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const int32_t last = s_last;
 
     // ---- phase A (segments in LDS or in part2: two instantiations)
-    const uint64_t W = d.W, bS = rs->bS;
+    const uint64_t W = d.W, bS = rs_bS;
     const uint32_t bSr = (uint32_t)(bS % R);
     const bool self_possible = E - S > d.vself_min;
     // few due events (a small shard): every host records its sends and the
@@ -2919,8 +3073,10 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r;
     }
     if (!ro.listed) return;  // launch-uniform
-    // due events: one reservation per (workgroup, partition), then the copies
-    __syncthreads();
+    // due events: one reservation per (workgroup, partition), then the copies.
+    // The barriers order LDS only: the calendar and partition stores drain
+    // while the workgroup goes on (nothing in the launch reads them back).
+    lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) {
         const uint32_t c = s_pc[p];
         s_pk[p] = 0;
@@ -2930,7 +3086,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
             s_pc[p] = base;
         }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < SU; ++q) {
         if (!due[q]) continue;
@@ -2939,9 +3095,9 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (slot < d.CAPP)
             d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]};
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
-    __syncthreads();
+    lds_barrier();
 }
 
 __device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uint64_t smin, uint64_t ntomb,
@@ -2970,22 +3126,29 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     RoundState* rs = d.rs;
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     __shared__ StepView sv;
-#ifdef SG_X_GFIRST
-    // experiment: the gather workgroups take the lowest block indices (dispatched first)
-    const uint32_t g0x = d.P + (recv ? d.G3 : 0), bx = blockIdx.x;
-    const uint32_t R = d.R, tid = threadIdx.x,
-                   blk = bx < d.G1 ? g0x + bx : (bx < d.G1 + g0x ? bx - d.G1 : bx);
-#else
+    __shared__ uint64_t s_rsw[RSW];              // the round state as the previous kernels left it
+    __shared__ int64_t s_hdr[MAXG * HDR_W];      // several shards: the received blocks' headers
+    __shared__ uint64_t s_gsw[3];                // gather: the GSpec header
+    __shared__ uint32_t s_routed;
     const uint32_t R = d.R, blk = blockIdx.x, tid = threadIdx.x;
-#endif
+    const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = gridDim.x - 2;  // gather workgroups [g0, gx)
+    // wave 0: the round state (and headers) in one batch of loads, then thread
+    // 0 plans the step from LDS and arrives.  The arrival's return is not
+    // waited for until the workgroup's end: the last to arrive publishes then.
+    uint64_t ticket = 0;
+    if (tid < 64) load_round_state(d, mode, recv, s_rsw, s_hdr);
+    asm volatile("" ::: "memory");  // the copy's stores before thread 0's reads of it
     if (tid == 0) {
-        step_view(d, mode, recv, sv);
-        if (!sv.quit) {
-            // every read of the round state has returned before the arrival
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            if (atomicAdd((unsigned long long*)&rs->splan, 1ull) == gridDim.x - 1) publish_step(d, mode, sv, recv);
-        }
+        step_view(d, mode, reinterpret_cast<const RoundState*>(s_rsw), s_hdr, sv);
+        // every read of the round state has returned (they are in LDS).  The
+        // address is made opaque (divergent to the compiler): for a uniform one
+        // the atomic optimizer reads the result back at once, which would wait
+        // for the arrival's round trip here.
+        const uint32_t z = opaque(tid) - tid;  // 0
+        if (!sv.quit) ticket = atomicAdd((unsigned long long*)&rs->splan + z, 1ull);
     }
+    // gather workgroups, wave 1: the guessed due list (GSpec) beside the round state
+    if (blk >= g0 && blk < gx && (tid >> 6) == 1) gspec_load(d, blk - g0, gx - g0, s_gsw, (DueEnt*)(lds + GDE_OFF));
     // Insert role: what does not depend on the window is loaded while thread 0
     // plans (waves 1.. at once; wave 0 after its plan): the partition's count,
     // its first SU staged events per thread and its reservation bases.
@@ -2994,19 +3157,26 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     if (blk < d.P) {  // uniform
         const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
         pre_n = d.rcnt[blk];
-#ifndef SG_X_NOPRE
 #pragma unroll
         for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[threadIdx.x + q * K3_T]);
-#endif
         uint32_t* s_cur = (uint32_t*)lds;
         uint32_t* s_pc = s_cur + RMAX;
         const uint32_t* wb = d.wbase + (size_t)blk * R;
-        for (uint32_t rb = tid; rb < R; rb += K3_T) s_cur[rb] = wb[rb];
+        constexpr uint32_t WPT = RMAX / K3_T;
+        uint32_t wv[WPT];  // every base load in flight at once (R <= RMAX)
+#pragma unroll
+        for (uint32_t q = 0; q < WPT; ++q) {
+            const uint32_t rb = tid + q * K3_T;
+            wv[q] = wb[rb < R ? rb : 0u];
+        }
         for (uint32_t p = tid; p < d.P; p += K3_T) s_pc[p] = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < WPT; ++q)
+            if (tid + q * K3_T < R) s_cur[tid + q * K3_T] = wv[q];
     }
-    __syncthreads();
+    lds_barrier();  // the plan, the headers, the guess and the bases are in LDS
     if (sv.quit) return;  // uniform: the run ended (no workgroup took a ticket)
-    const uint32_t g0 = d.P + (recv ? d.G3 : 0);
+    do {  // the roles (break: this workgroup's role is done)
     Route ro;
     ro.listed = sv.listed != 0;
     ro.cur = sv.cur;
@@ -3044,31 +3214,48 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         // read are final.  No new window: the current value carries over.
         if (!sv.listed) {
             if (tid == 0) rs->rmin2[sv.cur ^ 1] = sv.rmin0;
-            return;
+            break;
         }
         const uint64_t bS = sv.bS, bL = sv.bL, pbS = sv.pbS, pbL = sv.pbL;
         const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
+        constexpr uint32_t OPT = RMAX / K3_T;
+        uint64_t bv[OPT];  // every minimum in flight at once (clamped slots)
+#pragma unroll
+        for (uint32_t q = 0; q < OPT; ++q) {
+            const uint32_t o = tid + 1 + q * K3_T;
+            const uint32_t rb = o + span < R ? (bLr + o >= R ? bLr + o - R : bLr + o) : 0u;
+            bv[q] = d.bmin[rb];
+        }
         uint64_t mn = UINT64_MAX;
-        for (uint32_t o = tid + 1; o + span < R; o += K3_T) {
+#pragma unroll
+        for (uint32_t q = 0; q < OPT; ++q) {
+            const uint32_t o = tid + 1 + q * K3_T;
             const uint64_t b = bL + o - R;  // the ring slot's consumed bucket, if any
-            if (pbS != UINT64_MAX && b >= pbS && b <= pbL) continue;
-            const uint32_t rb = bLr + o >= R ? bLr + o - R : bLr + o;
-            const uint64_t v = d.bmin[rb];
-            mn = v < mn ? v : mn;
+            const bool live = o + span < R && !(pbS != UINT64_MAX && b >= pbS && b <= pbL);
+            mn = live && bv[q] < mn ? bv[q] : mn;
         }
         mn = block_min(mn, s16);  // barriers inside
         if (tid == 0) {
             rs->rmin2[sv.cur ^ 1] = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
             if (st) st[3] = __builtin_amdgcn_s_memrealtime();
         }
-        return;
+        break;
     }
     if (blk == gridDim.x - 2) {
         // fold: every slot reserved so far is written by this launch, so the
         // next step's gather may read them all
         {
             const uint32_t nx = sv.cur ^ 1;
-            for (uint32_t i = tid; i < XS * R; i += K3_T) d.bw[(size_t)nx * XS * R + i] = d.bk[i];
+            constexpr uint32_t CPT = XS * RMAX / K3_T;
+            uint32_t cv[CPT];  // every load in flight at once
+#pragma unroll
+            for (uint32_t q = 0; q < CPT; ++q) {
+                const uint32_t i = tid + q * K3_T;
+                cv[q] = d.bk[i < XS * R ? i : 0u];
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < CPT; ++q)
+                if (tid + q * K3_T < XS * R) d.bw[(size_t)nx * XS * R + tid + q * K3_T] = cv[q];
         }
         // stash refill: every reserving row back to ST chunk ids, one ring
         // reservation for all of them; the ring is usable up to the tail the
@@ -3093,7 +3280,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         }
         uint64_t total;
         uint32_t off = (uint32_t)block_excl_scan(mine, s16, &total);  // barriers inside
-        if (total == 0) return;  // uniform
+        if (total == 0) break;  // uniform
 #pragma unroll
         for (uint32_t q = 0; q < RPT; ++q) {
             const uint32_t r = tid + q * K3_T;
@@ -3132,13 +3319,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             const uint64_t got = e0 >= avail ? 0 : std::min<uint64_t>(avail - e0, ST - have[q]);
             d.stn[r] = have[q] + (uint32_t)got;
         }
-        return;
+        if (st) st[3] = __builtin_amdgcn_s_memrealtime();
+        break;
     }
-    const uint32_t gx = gridDim.x - 2;  // gather workgroups [g0, gx)
     if (blk >= g0) {
-        if (ro.listed) gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, st);
+        if (ro.listed) gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, s_gsw, st);
         if (st) st[3] = wait_stamp();
-        return;
+        break;
     }
     uint32_t* s_cur = (uint32_t*)lds;    // [RMAX] slot cursor per bucket
     uint32_t* s_pc = s_cur + RMAX;       // [PMAX] routed events per partition, then their base
@@ -3149,9 +3336,9 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     if (blk < d.P) {  // partition blk's staged local events (bases and first batch loaded above)
         const Rec* src = d.loc + (size_t)blk * d.ECAP;
         Rec r[SU];
-        if (!sv.ins_local) return;
+        if (!sv.ins_local) break;
         const uint32_t n = pre_n;
-        if (n == 0) return;  // uniform: nothing routed, nothing to finish
+        if (n == 0) break;  // uniform: nothing routed, nothing to finish
         const uint64_t S = sv.ins_S;
         if (st) {
             st[1] = __builtin_amdgcn_s_memrealtime();
@@ -3186,14 +3373,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (st) st[2] = wait_stamp();
         insert_finish(d, ro, smin, ntomb, s16);
         if (st) st[3] = wait_stamp();
-        return;
+        break;
     }
     // the received blocks' events due in the new window, split evenly over G3
     // workgroups, routed straight to their host partitions (one reservation
     // per (workgroup, partition)); the next k_proc stages the rest
     // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
-    __shared__ uint32_t s_routed;
     if (tid == 0) s_routed = 0;
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         s_pc[p] = 0;
@@ -3201,7 +3387,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     }
     const uint64_t total = recv_offsets(d, recv, d.xrows, d.xcap, s_off, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
-    if (!ro.listed) return;  // uniform: no new window, nothing is due
+    if (!ro.listed) break;  // uniform: no new window, nothing is due
     for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
         uint64_t t, k;
         uint32_t dl;
@@ -3228,6 +3414,9 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
         if (slot < d.CAPP) d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k};
     }
+    } while (0);
+    // the last workgroup to arrive publishes the plan for the next kernels
+    if (tid == 0 && ticket == gridDim.x - 1) publish_step(d, mode, sv, recv);
 }
 
 // ----------------------------------------------------------------- plan ----
@@ -3766,6 +3955,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.stash, (size_t)(D.P + D.G3) * ST);
     ALLOC(D.stn, D.P + D.G3);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
+    ALLOC(D.gspec, 1);
     ALLOC(D.pcnt, P);
     ALLOC(D.part, P * D.CAPP);
     ALLOC(D.part2, P * D.CAPP);
@@ -3937,6 +4127,7 @@ int sg_engine_boot(sg_engine* e) {
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
+    HIPCHK(hipMemsetAsync(d.gspec, 0xFF, sizeof(GSpec), e->stream));  // no guess (fold UINT64_MAX)
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P + d.G3));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
     HIPCHK(hipGetLastError());
