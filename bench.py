@@ -37,7 +37,7 @@ from shadow_amd.roofline import HBM_PEAK_GBS, kernel_line, proc_bytes, scatter_b
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = os.path.join(ROOT, "profiles", "r03", "bench", "pmc.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r04", "bench", "pmc.json")
 DOMINANT = "k_proc"
 
 

@@ -271,7 +271,7 @@ struct RoundState {
 constexpr uint32_t NSPEC = 1024;  // chunk ids kept (a million events)
 struct GSpec {
     uint64_t fold;  // the step it is for (rs->fold while that k_proc ran); UINT64_MAX: none
-    uint64_t b;     // the bucket (absolute)
+    uint64_t b;     // the bucket (absolute, low 48 bits) | its ring row << 48
     uint32_t lo;    // its slots written before the step (bw[fold & 1])
     uint32_t nid;   // chunk ids below: ceil(lo / CH)
     uint32_t ids[NSPEC];
@@ -870,6 +870,7 @@ struct StepView {
     uint64_t fold, rounds0, S0, E0;
     Window w;
     uint32_t cur, listed, ins_local, round_done, more, done, quit;
+    uint32_t tail_r, bSr;    // tail % NCH, bS % R (64-bit divisions done once, by the planner)
 };
 constexpr uint32_t SEGMAX = (NBMAX + 2) * XS;  // segments, at most
 // Segment j is bucket sub-list x = j % XS of the list's k-th bucket, k = j / XS:
@@ -980,7 +981,8 @@ __device__ __forceinline__ void gspec_load(const Dev& d, uint32_t w, uint32_t nw
         const uint32_t lo = (uint32_t)ln, nid = (uint32_t)(ln >> 32);
         const bool ok = i < nid && i < NSPEC;
         const uint32_t left = ok ? lo - i * CH : 0u;
-        s_de[k - 3] = DueEnt{ok ? (uint32_t)(v >> ((ic & 1) * 32)) : EMPTY, left < CH ? left : CH, b * d.W};
+        s_de[k - 3] = DueEnt{ok ? (uint32_t)(v >> ((ic & 1) * 32)) : EMPTY, left < CH ? left : CH,
+                             (b & ((1ull << 48) - 1)) * d.W};
     }
 }
 template <int GT>
@@ -999,7 +1001,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     // The window's chunks outside the retained bucket go back to the free ring
     // behind the tail as the entries are staged below (the next step's plan
     // advances the tail; nothing allocates before it).
-    const uint32_t tail_r = (uint32_t)(sv.tail % d.NCH);
+    const uint32_t tail_r = sv.tail_r;
     for (uint32_t p = threadIdx.x; p < P; p += GT) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
@@ -1076,12 +1078,12 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     // written chunks already.  Every chunk of the bucket (the slots reserved
     // since included: their due events were routed by the insert role) goes
     // back to the ring, entry i at tail + i, as the list path would put it.
-    const uint64_t gb = s_gsw[1];
+    const uint64_t gb = s_gsw[1] & ((1ull << 48) - 1);
     const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
     const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
     if (XS == 1 && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb && sv.ret == UINT64_MAX && !spent &&
         gnid <= GSPEC_N * nw) {  // uniform
-        const uint32_t row = (uint32_t)(gb % d.R);
+        const uint32_t row = (uint32_t)(s_gsw[1] >> 48);
         const uint32_t hi = d.bk[row];  // in flight under the pool loads
         if (st) st[1] = __builtin_amdgcn_s_memrealtime();
         one_pass(GSPEC_N, [&]() __attribute__((always_inline)) {
@@ -1670,6 +1672,8 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.m = m;
     sv.j = j;
     sv.ovf = ovf;
+    sv.tail_r = (uint32_t)(sv.tail % d.NCH);
+    sv.bSr = (uint32_t)(sv.bS % d.R);
     if (mode == 2 || sv.more) return;
     sv.round_done = 1;
     const Window w = next_window(d, m, j, mj0, nmj0);
@@ -1690,6 +1694,8 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
         sv.bL = (w.E - 1) / W;
         sv.ret = w.E < (sv.bL + 1) * W ? sv.bL : UINT64_MAX;
     }
+    sv.tail_r = (uint32_t)(sv.tail % d.NCH);
+    sv.bSr = (uint32_t)(sv.bS % d.R);
 }
 
 // The round state as the previous kernels left it and, with several shards,
@@ -2042,12 +2048,23 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
     if (guess && i < nid && i < NSPEC) g->ids[i] = id;
     if (i == 0) {
         g->fold = guess && nid <= NSPEC ? fold : UINT64_MAX;
-        g->b = b;
+        g->b = b | ((uint64_t)row << 48);
         g->lo = lo;
         g->nid = nid;
     }
 }
 
+// SG_SORT_LDS: 1, the sort's barriers after the histogram order LDS only (the
+// flat pass's state loads stay in flight under the scan); 2, also the first
+// barrier, with the state loads issued as soon as the records arrive.
+#ifndef SG_SORT_LDS
+#define SG_SORT_LDS 0
+#endif
+// SG_FLAT_LDSB: the barrier after the flat pass orders LDS only (default;
+// profiles/r04/flatb: 52.2 against 52.5-53.3 us/round, interleaved).
+#ifndef SG_FLAT_LDSB
+#define SG_FLAT_LDSB 1
+#endif
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
@@ -2226,16 +2243,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     };
     static_assert(K2_T >= NSPEC, "one GSpec id per thread");
     if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
-    if (stamp && tid == 0) stamp[20] = wait_stamp();
-    __syncthreads();
-    if (in_lds) {
-#pragma unroll
-        for (uint32_t q = 0; q < EPTF; ++q) {
-            if (tid + q * K2_T >= n) continue;
-            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
-            if (hl < HP) atomicAdd(&s_n[hl], 1u);
-            else flag(d, OV_BUG);
-        }
+    auto state_prefetch = [&]() __attribute__((always_inline)) {
         if (flat) {  // uniform
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
             uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
@@ -2248,6 +2256,38 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
             }
         }
+    };
+#if SG_SORT_LDS >= 2
+    state_prefetch();  // as soon as the records arrive, under the row loads and the sort
+#endif
+    if (stamp && tid == 0) stamp[20] = wait_stamp();
+#if SG_SORT_LDS >= 2
+    lds_barrier();  // the LDS zeroing; the row and state loads stay in flight
+#else
+    __syncthreads();
+#endif
+    if (in_lds) {
+#pragma unroll
+        for (uint32_t q = 0; q < EPTF; ++q) {
+            if (tid + q * K2_T >= n) continue;
+            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
+            if (hl < HP) atomicAdd(&s_n[hl], 1u);
+            else flag(d, OV_BUG);
+        }
+#if SG_SORT_LDS < 2
+        if (flat) {  // uniform
+            const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
+            uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
+            l0 = l0 < d.L ? l0 : d.L - 1;  // a record past the count: any valid slot
+            l1 = l1 < d.L ? l1 : d.L - 1;
+            pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
+            pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
+            if (tid + K2_T < n) {  // most lanes have one event
+                pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
+                pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
+            }
+        }
+#endif
         // the records are in registers now: re-defining them through asm keeps
         // the scatter below from waiting on the state prefetch (vmcnt(0))
 #pragma unroll
@@ -2262,7 +2302,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             else flag(d, OV_BUG);
         }
     }
+#if SG_SORT_LDS >= 1
+    lds_barrier();  // the counts; the state (and row) loads stay in flight under the scan
+#else
     __syncthreads();
+#endif
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
@@ -2276,7 +2320,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     uint64_t tot;
-    uint64_t run = block_excl_scan_2x32(mine, s16, &tot);
+    uint64_t run = block_excl_scan_2x32<(SG_SORT_LDS >= 1)>(mine, s16, &tot);
     for (uint32_t j = 0; j < per; ++j) {
         const uint32_t h = h0 + j;
         if (h < HP) {
@@ -2287,7 +2331,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     const uint32_t nact = (uint32_t)tot;
+#if SG_SORT_LDS >= 1
+    lds_barrier();
+#else
     __syncthreads();
+#endif
     if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
     const uint32_t sbase = p * HP;  // the partition's first local slot
     // phase A's first host of every lane: state loads issued now, under the
@@ -2713,7 +2761,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         flat_send(f0, vd0, dst0, pr0);
         flat_send(f1, vd1, dst1, pr1);
         if (stf) stamp[19] = wait_stamp();
+#if SG_FLAT_LDSB
+        // LDS only (s_dig, s_nser): no lane reads another's global stores from
+        // here on (phase A takes hosts the flat pass did not write), so the
+        // staging and state stores drain under the rest of the kernel
+        lds_barrier();
+#else
         __syncthreads();
+#endif
         // a multi-event host's digest: the last event's lane adds the others'
         // terms (LDS; global atomics on the state's line next to the state
         // stores cost about 10 us per round, profiles/r03/flat)
@@ -3185,7 +3240,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     ro.ret = sv.ret;
     ro.bS = sv.bS;
     ro.bSW = ro.bS * d.W;
-    ro.bSr = (uint32_t)(ro.bS % R);
+    ro.bSr = sv.bSr;
     // SG_STAMPS: {start, after setup, after the events, end, role, events}
     uint64_t* st = d.stamps && tid == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
     if (st) {
