@@ -81,6 +81,7 @@ constexpr uint32_t RMAX = 4096;          // ring buckets (LDS bucket bins)
 #define SG_XS 1
 #endif
 constexpr uint32_t XS = SG_XS;
+
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t G3MAX = 512;          // k_scatter receive-role workgroups (received-block split)
@@ -163,6 +164,29 @@ __device__ __forceinline__ void st_stream2(ulonglong2* p, uint64_t a, uint64_t b
 #else
     *p = make_ulonglong2(a, b);
 #endif
+}
+// Write-through 16-B stores of the streamed records (SG_WT): a buffer store
+// with the sc1 policy sends the line to memory now and drops it from the XCD's
+// L2, instead of leaving it dirty for the write-back at the kernel boundary
+// (MI355X_MICROARCH.md, boundary row: + B / 6 TB/s for B bytes left dirty).
+// base: a wave-uniform array start; the byte offset fits 32 bits when d.wt
+// (host-checked), else a plain store.
+#ifndef SG_WT
+#define SG_WT 0
+#endif
+__device__ __forceinline__ void st_wt(bool wt, const void* base, uint64_t off, uint64_t a, uint64_t b) {
+#if SG_WT
+    if (wt) {
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
+        const u32x4_t v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(uint32_t)off, 0, 16 /* sc1 */);
+        return;
+    }
+#else
+    (void)wt;
+#endif
+    *reinterpret_cast<ulonglong2*>(static_cast<char*>(const_cast<void*>(base)) + off) = make_ulonglong2(a, b);
 }
 struct DueEnt {
     uint32_t id;      // chunk
@@ -258,6 +282,7 @@ struct RoundState {
     uint64_t ticket;     // k_proc workgroups finished this launch (the last one writes the headers)
     uint64_t xacc[2];    // emitted min, discovery min of k_proc's workgroups (atomics)
     uint64_t recv_ok;    // a several-shard k_scatter read the receive buffer: the next k_proc stages it
+    uint64_t tail_r, bS_r;  // fl_tail % NCH, bS % R, kept with them (the planner's 64-bit divisions)
 };
 
 // The gather's due list, guessed one kernel ahead.  In steady state a window
@@ -306,6 +331,7 @@ struct Dev {
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
+    bool wt;                      // SG_WT builds: the streamed arrays fit 32-bit byte offsets (write-through stores)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
@@ -773,6 +799,8 @@ __global__ void k_boot(Dev d) {
         }
         rs->fl_head = nb0;
         rs->fl_tail = d.NCH;
+        rs->tail_r = 0;  // fl_tail % NCH
+        rs->bS_r = 0;    // bS % R
         rs->ins_local = 0;
         rs->ins_S = 0;
         rs->phase = 0;
@@ -835,7 +863,7 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
             if (slot < d.CAPP)
-                st_stream(&d.part[(size_t)p * d.CAPP + slot], Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k});
+                st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
                 ++ntomb;
@@ -1064,7 +1092,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPP) st_stream(&d.part[(size_t)p * d.CAPP + slot], r[q]);
+            if (slot < d.CAPP) st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, r[q].a, r[q].k);
             const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             if (de.nflags & RETAINED) {
@@ -1221,7 +1249,7 @@ __device__ __forceinline__ bool stage_event(const Dev& d, uint64_t S, uint32_t p
     ++a.ctr[C_EMIT];
     if (dl < d.L) {
         const uint32_t slot = wave_slot(&sh.nloc);
-        if (slot < d.ECAP) st_stream(&d.loc[(size_t)part * d.ECAP + slot], Rec{((uint64_t)dl << 40) | (tn - S), key});
+        if (slot < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (tn - S), key);
         else a.overflow = true;
         return true;
     }
@@ -1371,13 +1399,13 @@ __device__ __forceinline__ void commit_two(const Dev& d, uint64_t S, uint64_t E,
     const uint32_t base = wave_slots(&sh.nloc, (uint32_t)l0 + (uint32_t)l1);
     Rec* loc = d.loc + (size_t)part * d.ECAP;
     if (l0) {
-        if (base < d.ECAP) st_stream(&loc[base], Rec{((uint64_t)dl0 << 40) | (tn0 - S), k0});
+        if (base < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + base) * 16, ((uint64_t)dl0 << 40) | (tn0 - S), k0);
         else a.overflow = true;
         count(tn0);
     }
     if (l1) {
         const uint32_t sl = base + (l0 ? 1u : 0u);
-        if (sl < d.ECAP) st_stream(&loc[sl], Rec{((uint64_t)dl1 << 40) | (tn1 - S), k1});
+        if (sl < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + sl) * 16, ((uint64_t)dl1 << 40) | (tn1 - S), k1);
         else a.overflow = true;
         count(tn1);
     }
@@ -1672,8 +1700,8 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.m = m;
     sv.j = j;
     sv.ovf = ovf;
-    sv.tail_r = (uint32_t)(sv.tail % d.NCH);
-    sv.bSr = (uint32_t)(sv.bS % d.R);
+    sv.tail_r = (uint32_t)rs->tail_r;
+    sv.bSr = (uint32_t)rs->bS_r;
     if (mode == 2 || sv.more) return;
     sv.round_done = 1;
     const Window w = next_window(d, m, j, mj0, nmj0);
@@ -1682,6 +1710,8 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.S = w.S;
     sv.E = w.E;
     sv.tail = tail0 + sv.nfree0;  // the last gather's chunks are in the ring now
+    sv.tail_r += (uint32_t)sv.nfree0;  // nfree0 <= NCH: one wrap at most
+    sv.tail_r -= sv.tail_r >= d.NCH ? d.NCH : 0u;
     // the executed window: its consumed buckets are skipped by rmin until the
     // next k_proc resets them; its straddling bucket is spent unless the new
     // window starts in it
@@ -1690,12 +1720,21 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.pret = sv.ret;
     if (!sv.done) {
         sv.listed = 1;
-        sv.bS = w.S / W;
-        sv.bL = (w.E - 1) / W;
+        // the buckets from the old first bucket (S >= its start): one 32-bit
+        // multiply-high division while the offsets fit, as in steady state
+        const uint64_t bS0 = sv.bS, x = w.S - bS0 * W;
+        const uint64_t o = d.ring32 && x < (1ull << 32) ? wdiv(d, (uint32_t)x) : w.S / W - bS0;
+        sv.bS = bS0 + o;
+        const uint64_t y = w.E - 1 - sv.bS * W;
+        sv.bL = sv.bS + (d.ring32 && y < (1ull << 32) ? wdiv(d, (uint32_t)y) : y / W);
         sv.ret = w.E < (sv.bL + 1) * W ? sv.bL : UINT64_MAX;
+        if (o < d.R) {
+            sv.bSr += (uint32_t)o;
+            sv.bSr -= sv.bSr >= d.R ? d.R : 0u;
+        } else {
+            sv.bSr = (uint32_t)(sv.bS % d.R);
+        }
     }
-    sv.tail_r = (uint32_t)(sv.tail % d.NCH);
-    sv.bSr = (uint32_t)(sv.bS % d.R);
 }
 
 // The round state as the previous kernels left it and, with several shards,
@@ -1793,6 +1832,8 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     rs->E = sv.E;
     rs->done = sv.done;
     rs->fl_tail = sv.tail;
+    rs->tail_r = sv.tail_r;
+    rs->bS_r = sv.bSr;
     rs->pbS = sv.pbS;
     rs->pbL = sv.pbL;
     rs->pret = sv.pret;
@@ -2016,7 +2057,7 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
         if (v && routed && t < E) v = false;  // k_scatter put it in its partition
         if (v) {
             const uint32_t slot = wave_slot(&sh.nloc);
-            if (slot < d.ECAP) st_stream(&d.loc[(size_t)part * d.ECAP + slot], Rec{((uint64_t)dl << 40) | (t - S), k});
+            if (slot < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (t - S), k);
             else ovf = true;
             count(t);
             mn = t < mn ? t : mn;
@@ -2537,9 +2578,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             commit_two(d, S, E, p, c, a, sh, nsd, S + t0, c0, dst0, vd0, pr0, S + t1, c1, dst1, vd1, pr1,
                                        count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
-                            st_stream2(&hp[0], hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
+                            st_wt(d.wt, d.hs, (size_t)lh * 32, hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
                             if (st0) stamp[19] = wait_stamp();
-                            st_stream2(&hp[1], c.s.digest, c.s.evc);
+                            st_wt(d.wt, d.hs, (size_t)lh * 32 + 16, c.s.digest, c.s.evc);
                             ns = 0;
                         } else {
                             go = true;
@@ -2712,8 +2753,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if ((f.flags & F_LAST) && !(SG_ABL & 2)) {  // the host's last event: its state after the round
                 const uint64_t evc = f.sq + (kept ? 1u : 0u);
                 ulonglong2* hw = reinterpret_cast<ulonglong2*>(hp);
-                st_stream2(&hw[0], hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
-                if (!(f.flags & F_MULTI)) st_stream2(&hw[1], f.term, evc);
+                st_wt(d.wt, d.hs, (size_t)(sbase + f.hl) * 32, hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
+                if (!(f.flags & F_MULTI)) st_wt(d.wt, d.hs, (size_t)(sbase + f.hl) * 32 + 16, f.term, evc);
                 else hp->evc = evc;  // the digest after the barrier below
             } else if (!(SG_ABL & 1)) {  // an earlier event of a multi-event host (ok: F_MULTI)
                 atomicAdd(&s_dig[f.hl], (unsigned long long)f.term);
@@ -3125,7 +3166,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (!write[q] || (pos[q] >> CH_SHIFT) >= d.NCH || id[q] >= d.NCH) continue;
         Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
         ntomb += due[q];
-        d.pool[((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))] = r;
+        st_wt(d.wt, d.pool, (((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))) * 16, r.a, r.k);
     }
     if (!ro.listed) return;  // launch-uniform
     // due events: one reservation per (workgroup, partition), then the copies.
@@ -3148,7 +3189,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         const uint32_t p = part_of(d, dl[q]);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
         if (slot < d.CAPP)
-            d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]};
+            st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
     }
     lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
@@ -3467,7 +3508,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (!recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
         const uint32_t p = part_of(d, dl);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPP) d.part[(size_t)p * d.CAPP + slot] = Rec{((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k};
+        if (slot < d.CAPP) st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
     }
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
@@ -4017,6 +4058,12 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.extras, P * K2_T * XCAP);
     ALLOC(D.rcnt, P);
     ALLOC(D.loc, P * D.ECAP);
+    {  // write-through stores take 32-bit byte offsets from each array's start (SG_WT)
+        const uint64_t lim = 1ull << 32;
+        D.wt = (uint64_t)L * sizeof(HostState) < lim && (uint64_t)D.NCH * CH * sizeof(Rec) < lim &&
+               (uint64_t)P * D.CAPP * sizeof(Rec) < lim && (uint64_t)P * D.ECAP * sizeof(Rec) < lim &&
+               env_u32z("SG_WT", 1) != 0;
+    }
     ALLOC(D.sends, P * D.ECAP);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
