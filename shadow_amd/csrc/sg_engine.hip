@@ -124,7 +124,10 @@ struct Slot {
 // evict the randomly read tables (destination vertices, path records) from
 // an XCD's 4 MB L2.  SG_NT is a mask: 1 loads, 2 stores.  Measured on
 // configs[3] (profiles/r02/knobs/nt.log): 3 (both) 3.67e9 events/s against
-// 4.60e9 plain — the next kernel re-reads the streamed records from HBM.
+// 4.60e9 plain — the next kernel re-reads the streamed records from HBM; 2
+// alone, round 4: 66.8 against 52.5 us per round (profiles/r04/flatb).  Write-
+// through (sc1) stores were worse still (profiles/r04/wt): L2 merges the 16-B
+// records into whole lines only when they are written back, not through.
 #ifndef SG_NT
 #define SG_NT 0
 #endif
@@ -137,16 +140,6 @@ __device__ __forceinline__ Rec ld_stream(const Rec* p) {
     return *p;
 #endif
 }
-__device__ __forceinline__ void st_stream(Rec* p, const Rec& r) {
-#if SG_NT & 2
-    u64x2_t v;
-    v.x = r.a;
-    v.y = r.k;
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2_t*>(p));
-#else
-    *p = r;
-#endif
-}
 __device__ __forceinline__ ulonglong2 ld_stream2(const ulonglong2* p) {
 #if SG_NT & 1
     const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
@@ -155,38 +148,16 @@ __device__ __forceinline__ ulonglong2 ld_stream2(const ulonglong2* p) {
     return *p;
 #endif
 }
-__device__ __forceinline__ void st_stream2(ulonglong2* p, uint64_t a, uint64_t b) {
+// A streamed 16-B record store at a byte offset from a wave-uniform array start.
+__device__ __forceinline__ void st_rec(void* base, uint64_t off, uint64_t a, uint64_t b) {
 #if SG_NT & 2
     u64x2_t v;
     v.x = a;
     v.y = b;
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2_t*>(p));
+    __builtin_nontemporal_store(v, reinterpret_cast<u64x2_t*>(static_cast<char*>(base) + off));
 #else
-    *p = make_ulonglong2(a, b);
+    *reinterpret_cast<ulonglong2*>(static_cast<char*>(base) + off) = make_ulonglong2(a, b);
 #endif
-}
-// Write-through 16-B stores of the streamed records (SG_WT): a buffer store
-// with the sc1 policy sends the line to memory now and drops it from the XCD's
-// L2, instead of leaving it dirty for the write-back at the kernel boundary
-// (MI355X_MICROARCH.md, boundary row: + B / 6 TB/s for B bytes left dirty).
-// base: a wave-uniform array start; the byte offset fits 32 bits when d.wt
-// (host-checked), else a plain store.
-#ifndef SG_WT
-#define SG_WT 0
-#endif
-__device__ __forceinline__ void st_wt(bool wt, const void* base, uint64_t off, uint64_t a, uint64_t b) {
-#if SG_WT
-    if (wt) {
-        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
-        const u32x4_t v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(uint32_t)off, 0, 16 /* sc1 */);
-        return;
-    }
-#else
-    (void)wt;
-#endif
-    *reinterpret_cast<ulonglong2*>(static_cast<char*>(const_cast<void*>(base)) + off) = make_ulonglong2(a, b);
 }
 struct DueEnt {
     uint32_t id;      // chunk
@@ -331,7 +302,6 @@ struct Dev {
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
-    bool wt;                      // SG_WT builds: the streamed arrays fit 32-bit byte offsets (write-through stores)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
@@ -863,7 +833,7 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
             if (slot < d.CAPP)
-                st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
+                st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
                 ++ntomb;
@@ -1092,7 +1062,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPP) st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, r[q].a, r[q].k);
+            if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, r[q].a, r[q].k);
             const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             if (de.nflags & RETAINED) {
@@ -1249,7 +1219,7 @@ __device__ __forceinline__ bool stage_event(const Dev& d, uint64_t S, uint32_t p
     ++a.ctr[C_EMIT];
     if (dl < d.L) {
         const uint32_t slot = wave_slot(&sh.nloc);
-        if (slot < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (tn - S), key);
+        if (slot < d.ECAP) st_rec(d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (tn - S), key);
         else a.overflow = true;
         return true;
     }
@@ -1399,13 +1369,13 @@ __device__ __forceinline__ void commit_two(const Dev& d, uint64_t S, uint64_t E,
     const uint32_t base = wave_slots(&sh.nloc, (uint32_t)l0 + (uint32_t)l1);
     Rec* loc = d.loc + (size_t)part * d.ECAP;
     if (l0) {
-        if (base < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + base) * 16, ((uint64_t)dl0 << 40) | (tn0 - S), k0);
+        if (base < d.ECAP) st_rec(d.loc, ((size_t)part * d.ECAP + base) * 16, ((uint64_t)dl0 << 40) | (tn0 - S), k0);
         else a.overflow = true;
         count(tn0);
     }
     if (l1) {
         const uint32_t sl = base + (l0 ? 1u : 0u);
-        if (sl < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + sl) * 16, ((uint64_t)dl1 << 40) | (tn1 - S), k1);
+        if (sl < d.ECAP) st_rec(d.loc, ((size_t)part * d.ECAP + sl) * 16, ((uint64_t)dl1 << 40) | (tn1 - S), k1);
         else a.overflow = true;
         count(tn1);
     }
@@ -2057,7 +2027,7 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
         if (v && routed && t < E) v = false;  // k_scatter put it in its partition
         if (v) {
             const uint32_t slot = wave_slot(&sh.nloc);
-            if (slot < d.ECAP) st_wt(d.wt, d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (t - S), k);
+            if (slot < d.ECAP) st_rec(d.loc, ((size_t)part * d.ECAP + slot) * 16, ((uint64_t)dl << 40) | (t - S), k);
             else ovf = true;
             count(t);
             mn = t < mn ? t : mn;
@@ -2578,9 +2548,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             commit_two(d, S, E, p, c, a, sh, nsd, S + t0, c0, dst0, vd0, pr0, S + t1, c1, dst1, vd1, pr1,
                                        count_local);
                             ulonglong2* hp = reinterpret_cast<ulonglong2*>(d.hs + lh);
-                            st_wt(d.wt, d.hs, (size_t)lh * 32, hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
+                            st_rec(d.hs, (size_t)lh * 32, hs_w0(c.s.rng, c.h), hs_w1(c.s.pops, c.vh));
                             if (st0) stamp[19] = wait_stamp();
-                            st_wt(d.wt, d.hs, (size_t)lh * 32 + 16, c.s.digest, c.s.evc);
+                            st_rec(d.hs, (size_t)lh * 32 + 16, c.s.digest, c.s.evc);
                             ns = 0;
                         } else {
                             go = true;
@@ -2753,8 +2723,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if ((f.flags & F_LAST) && !(SG_ABL & 2)) {  // the host's last event: its state after the round
                 const uint64_t evc = f.sq + (kept ? 1u : 0u);
                 ulonglong2* hw = reinterpret_cast<ulonglong2*>(hp);
-                st_wt(d.wt, d.hs, (size_t)(sbase + f.hl) * 32, hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
-                if (!(f.flags & F_MULTI)) st_wt(d.wt, d.hs, (size_t)(sbase + f.hl) * 32 + 16, f.term, evc);
+                st_rec(d.hs, (size_t)(sbase + f.hl) * 32, hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
+                if (!(f.flags & F_MULTI)) st_rec(d.hs, (size_t)(sbase + f.hl) * 32 + 16, f.term, evc);
                 else hp->evc = evc;  // the digest after the barrier below
             } else if (!(SG_ABL & 1)) {  // an earlier event of a multi-event host (ok: F_MULTI)
                 atomicAdd(&s_dig[f.hl], (unsigned long long)f.term);
@@ -3166,7 +3136,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (!write[q] || (pos[q] >> CH_SHIFT) >= d.NCH || id[q] >= d.NCH) continue;
         Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
         ntomb += due[q];
-        st_wt(d.wt, d.pool, (((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))) * 16, r.a, r.k);
+        st_rec(d.pool, (((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))) * 16, r.a, r.k);
     }
     if (!ro.listed) return;  // launch-uniform
     // due events: one reservation per (workgroup, partition), then the copies.
@@ -3189,7 +3159,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         const uint32_t p = part_of(d, dl[q]);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
         if (slot < d.CAPP)
-            st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
+            st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
     }
     lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
@@ -3508,7 +3478,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (!recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
         const uint32_t p = part_of(d, dl);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPP) st_wt(d.wt, d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
+        if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
     }
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
@@ -4058,12 +4028,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.extras, P * K2_T * XCAP);
     ALLOC(D.rcnt, P);
     ALLOC(D.loc, P * D.ECAP);
-    {  // write-through stores take 32-bit byte offsets from each array's start (SG_WT)
-        const uint64_t lim = 1ull << 32;
-        D.wt = (uint64_t)L * sizeof(HostState) < lim && (uint64_t)D.NCH * CH * sizeof(Rec) < lim &&
-               (uint64_t)P * D.CAPP * sizeof(Rec) < lim && (uint64_t)P * D.ECAP * sizeof(Rec) < lim &&
-               env_u32z("SG_WT", 1) != 0;
-    }
     ALLOC(D.sends, P * D.ECAP);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
