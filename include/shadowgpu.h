@@ -352,6 +352,12 @@ int sg_engine_active_hosts(sg_engine* e, uint64_t* active_host_rounds, uint64_t*
  * routed into host partitions (several shards; the received events it leaves
  * for the next k_proc to stage are not counted). */
 int sg_engine_event_moves(sg_engine* e, uint64_t* emitted, uint64_t* gathered, uint64_t* received);
+/* k_scatter launches whose gather took the due list guessed by the k_proc
+ * before (GSpec: the window is one whole bucket, the one after the executed
+ * window) and launches that derived it from the bucket words.  SG_GSPEC=0
+ * turns the guess off, SG_GSPEC=2 guesses a wrong bucket (the check must
+ * reject it); both exist for tests. */
+int sg_engine_gather_paths(sg_engine* e, uint64_t* guessed, uint64_t* listed);
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
 /* Executed windows {start, end} per round (recorded when trace_capacity > 0). */
 int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);

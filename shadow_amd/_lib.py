@@ -97,7 +97,7 @@ EXPORTS = [
     "sg_topology_lognormal", "sg_graphml_load", "sg_graph_free", "sg_graph_info", "sg_graph_vertex",
     "sg_graph_edge", "sg_graph_attach", "sg_graph_paths", "sg_build_path_tables", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
-    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_event_moves", "sg_engine_trace", "sg_engine_windows",
+    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_event_moves", "sg_engine_gather_paths", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
     "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv",
     "sg_engine_enqueue_rounds", "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy",
@@ -149,6 +149,7 @@ def lib():
     L.sg_engine_host_range.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.sg_engine_active_hosts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sg_engine_event_moves.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 3
+    L.sg_engine_gather_paths.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 2
     L.sg_engine_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_stream.argtypes = [C.c_void_p]

@@ -108,6 +108,8 @@ enum Ctr {
     NPCTR,                  // counters k_proc accumulates; k_scatter's follow
     C_GATHER = NPCTR,       // events the gather role moved from the calendar into partitions
     C_RECV,                 // received events the receive role wrote into partitions (several shards)
+    C_GSPEC,                // k_scatter launches whose gather took the GSpec guess
+    C_GLIST,                // k_scatter launches whose gather derived the due list (the guess missed)
     NCTR
 };
 
@@ -332,6 +334,7 @@ struct Dev {
     uint32_t* stn;            // [P + G3] ids in the row's stash
     uint32_t* wbase;          // [P + G3][R] reserved base per (row, bucket) in the row's sub-list
     GSpec* gspec;             // the next gather's guessed due list (k_proc -> k_scatter)
+    uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
     uint32_t* pcnt;           // [P] due events of the partition this round
     Rec* part;                // [P][CAPP]
@@ -1086,7 +1089,10 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
         if (st) st[1] = __builtin_amdgcn_s_memrealtime();
         one_pass(GSPEC_N, [&]() __attribute__((always_inline)) {
             const uint32_t nd = (hi + CH - 1) >> CH_SHIFT;
-            if (w == 0 && threadIdx.x == 0) d.rs->nfree2[sv.cur ^ 1] = nd;
+            if (w == 0 && threadIdx.x == 0) {
+                d.rs->nfree2[sv.cur ^ 1] = nd;
+                atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
+            }
             if (st) {
                 st[5] = nd;
                 st[7] = 1;
@@ -1102,7 +1108,10 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     DueList dl;
     uint64_t nfree;
     const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree);  // barriers inside
-    if (w == 0 && threadIdx.x == 0) d.rs->nfree2[sv.cur ^ 1] = nfree;
+    if (w == 0 && threadIdx.x == 0) {
+        d.rs->nfree2[sv.cur ^ 1] = nfree;
+        atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GLIST * d.P], 1ull);
+    }
     if (st) {  // the list's shape (SG_STAMPS)
         st[5] = nd;
         st[7] = dl.nseg;
@@ -2049,8 +2058,8 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
 // now (this launch's reservations append beyond them).  One workgroup, every
 // thread; the loads go out together.
 __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_t E) {
-    const uint64_t b = E / d.W;
-    const bool guess = XS == 1 && b * d.W == E;
+    const uint64_t b = E / d.W + (d.gspec_mode == 2 ? 1u : 0u);
+    const bool guess = XS == 1 && (b - (d.gspec_mode == 2 ? 1u : 0u)) * d.W == E && d.gspec_mode != 0;
     const uint32_t row = (uint32_t)(b % d.R), i = threadIdx.x;
     const uint32_t lo = d.bw[(size_t)(fold & 1) * XS * d.R + row];
     const uint32_t id = d.btab[(size_t)row * d.NCH + (i < d.NCH ? i : 0u)];
@@ -2070,6 +2079,11 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 // barrier, with the state loads issued as soon as the records arrive.
 #ifndef SG_SORT_LDS
 #define SG_SORT_LDS 0
+#endif
+// SG_INS_PRE: k_scatter's insert role loads its first staged events and its
+// reservation bases at launch, beside the plan (1), or after it (0).
+#ifndef SG_INS_PRE
+#define SG_INS_PRE 1
 #endif
 // SG_FLAT_LDSB: the barrier after the flat pass orders LDS only (default;
 // profiles/r04/flatb: 52.2 against 52.5-53.3 us/round, interleaved).
@@ -3220,16 +3234,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // its first SU staged events per thread and its reservation bases.
     Rec pre[SU];
     uint32_t pre_n = 0;
-    if (blk < d.P) {  // uniform
-        const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
-        pre_n = d.rcnt[blk];
-#pragma unroll
-        for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[threadIdx.x + q * K3_T]);
+    // the partition's reservation bases into LDS (every load in flight at once, R <= RMAX)
+    auto load_bases = [&]() __attribute__((always_inline)) {
         uint32_t* s_cur = (uint32_t*)lds;
         uint32_t* s_pc = s_cur + RMAX;
         const uint32_t* wb = d.wbase + (size_t)blk * R;
         constexpr uint32_t WPT = RMAX / K3_T;
-        uint32_t wv[WPT];  // every base load in flight at once (R <= RMAX)
+        uint32_t wv[WPT];
 #pragma unroll
         for (uint32_t q = 0; q < WPT; ++q) {
             const uint32_t rb = tid + q * K3_T;
@@ -3239,6 +3250,15 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
 #pragma unroll
         for (uint32_t q = 0; q < WPT; ++q)
             if (tid + q * K3_T < R) s_cur[tid + q * K3_T] = wv[q];
+    };
+    if (blk < d.P) {  // uniform
+        pre_n = d.rcnt[blk];
+#if SG_INS_PRE
+        const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
+#pragma unroll
+        for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[threadIdx.x + q * K3_T]);
+        load_bases();
+#endif
     }
     lds_barrier();  // the plan, the headers, the guess and the bases are in LDS
     if (sv.quit) return;  // uniform: the run ended (no workgroup took a ticket)
@@ -3410,8 +3430,12 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             st[1] = __builtin_amdgcn_s_memrealtime();
             st[5] = n;
         }
+#if !SG_INS_PRE
+        load_bases();  // after the plan: the gather's first loads go out ahead of these
+        lds_barrier();
+#endif
         for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
-#ifndef SG_X_NOPRE
+#if SG_INS_PRE
             if (i0 == 0) {  // uniform
 #pragma unroll
                 for (int q = 0; q < SU; ++q) r[q] = pre[q];
@@ -3804,6 +3828,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         return SG_ERR_INVAL;
     }
     d.G1 = env_u32("SG_GATHER_GRID", 128);
+    d.gspec_mode = env_u32z("SG_GSPEC", 1);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
     // host partitions: HP hosts per k_proc workgroup (power of two), about
@@ -4389,6 +4414,16 @@ int sg_engine_active_hosts(sg_engine* e, uint64_t* active, uint64_t* emitted) {
     if (rc) return rc;
     if (active) *active = e->h_rs->ctr[C_ACTIVE];
     if (emitted) *emitted = e->h_rs->ctr[C_EMIT];
+    return SG_OK;
+}
+
+int sg_engine_gather_paths(sg_engine* e, uint64_t* guessed, uint64_t* listed) {
+    if (!e) return SG_ERR_INVAL;
+    sg_round_stats s;
+    int rc = sg_engine_stats(e, &s);
+    if (rc) return rc;
+    if (guessed) *guessed = e->h_rs->ctr[C_GSPEC];
+    if (listed) *listed = e->h_rs->ctr[C_GLIST];
     return SG_OK;
 }
 

@@ -107,6 +107,13 @@ class Engine:
         L.check(L.lib().sg_engine_event_moves(self.h, *[C.byref(x) for x in v]))
         return dict(zip(("emitted", "gathered", "received"), (x.value for x in v)))
 
+    def gather_paths(self) -> dict:
+        """k_scatter launches whose gather took the due list the k_proc before
+        guessed (GSpec) and launches that derived it from the bucket words."""
+        v = [C.c_uint64() for _ in range(2)]
+        L.check(L.lib().sg_engine_gather_paths(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(("guessed", "listed"), (x.value for x in v)))
+
     def host_state(self) -> dict:
         n = self.n_local
         d, p, e = (np.zeros(n, np.uint64) for _ in range(3))

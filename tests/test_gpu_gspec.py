@@ -1,0 +1,44 @@
+"""The gather's guessed due list (GSpec) pinned directly.
+
+k_proc copies the chunk ids of the bucket it expects the next window to cover
+whole; k_scatter's gather uses them only after checking the guess against the
+window it planned (same step, one whole bucket, nothing straddling or spent),
+and derives the due list from the bucket words otherwise.  Here configs[3]
+(1M hosts, the bench's rounds) runs with the guess on, off (SG_GSPEC=0) and
+deliberately wrong (SG_GSPEC=2: the bucket after the right one, which the
+check must reject) against the oracle's per-round fixture, and the launch
+counters show which path each run took."""
+import json
+import os
+
+import pytest
+
+from shadow_amd import phold
+from shadow_amd.engine import Engine
+from shadow_amd.trace import state_fingerprint
+
+pytestmark = pytest.mark.gpu
+FIX = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_fixtures.json")))
+ROWS = {r[0]: r for r in FIX["c4_1m"]["rounds"]}
+
+
+@pytest.mark.parametrize("mode", ["1", "0", "2"])
+def test_c4_gspec_modes_match_the_oracle(mode, monkeypatch):
+    monkeypatch.setenv("SG_GSPEC", mode)  # read when the engine is created
+    eng = Engine(phold.c4_config(n_hosts=1_000_000))
+    eng.boot()
+    done = 0
+    for r in (25, 120):
+        eng.run(r - done)
+        done = r
+        st = eng.stats()
+        assert st["rounds"] == r and st["overflow"] == 0
+        assert (st["pops"], st["window_start"], st["window_end"]) == (ROWS[r][1], ROWS[r][3], ROWS[r][4]), r
+        hs = eng.host_state()
+        assert state_fingerprint(eng.first_host, hs["digest"], hs["pops"], hs["rng"], hs["ev"]) == ROWS[r][2], r
+    g = eng.gather_paths()
+    assert g["guessed"] + g["listed"] >= 119  # every round but the boot's gathers
+    if mode == "1":
+        assert g["guessed"] >= 100, g  # steady rounds are one whole bucket each
+    else:
+        assert g["guessed"] == 0, g
