@@ -86,7 +86,10 @@ constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
 constexpr uint32_t G3MAX = 512;          // k_scatter receive-role workgroups (received-block split)
 constexpr uint32_t XCAP = 32;            // same-round self events in flight per lane
-constexpr int K2_T = 1024, K3_T = 512;
+#ifndef SG_K3T
+#define SG_K3T 512  // k_scatter's workgroup size
+#endif
+constexpr int K2_T = 1024, K3_T = SG_K3T;
 constexpr uint32_t RETAINED = 1u << 31;
 constexpr uint32_t ST = 16;           // chunk ids in a reserving row's stash
 constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (bucket width set to fit)
@@ -2081,9 +2084,11 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #define SG_SORT_LDS 0
 #endif
 // SG_INS_PRE: k_scatter's insert role loads its first staged events and its
-// reservation bases at launch, beside the plan (1), or after it (0).
+// reservation bases at launch, beside the plan (1), or after it (0, default:
+// the gather's first loads go out ahead of them; 51.1-51.4 against 51.6-52.0
+// us per round, profiles/r04/insert_pre).
 #ifndef SG_INS_PRE
-#define SG_INS_PRE 1
+#define SG_INS_PRE 0
 #endif
 // SG_FLAT_LDSB: the barrier after the flat pass orders LDS only (default;
 // profiles/r04/flatb: 52.2 against 52.5-53.3 us/round, interleaved).
@@ -2335,10 +2340,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
-    const uint32_t h0 = tid * per;
+    const uint32_t h0 = tid * per, hs = 1;  // (strided hosts measured: no change, profiles/r04/insert_pre)
     uint64_t mine = 0;
     for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t h = h0 + j;
+        const uint32_t h = h0 + j * hs;
         if (h < HP) {
             const uint32_t c = s_n[h];
             mine += ((uint64_t)c << 32) | (c ? 1u : 0u);
@@ -2347,7 +2352,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t tot;
     uint64_t run = block_excl_scan_2x32<(SG_SORT_LDS >= 1)>(mine, s16, &tot);
     for (uint32_t j = 0; j < per; ++j) {
-        const uint32_t h = h0 + j;
+        const uint32_t h = h0 + j * hs;
         if (h < HP) {
             const uint32_t c = s_n[h];
             s_c[h] = (uint32_t)(run >> 32);
@@ -3087,7 +3092,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 // becomes a tombstone in the straddling bucket.  Events that stay in the
 // straddling bucket add to the carry min (the next MIN term), as the
 // gather's leftovers do.
-constexpr int SU = 4;  // events per thread in flight
+constexpr int SU = 2048 / K3_T;  // events per thread in flight (2048 per insert batch)
 constexpr size_t INS_LDS = (RMAX + 2 * PMAX) * 4 + 16 * 8 + MAXG * 4;
 constexpr size_t REFILL_LDS = 16 * 8 + 8 + 2 * (PMAX + G3MAX) * 4;
 constexpr size_t SCAT_LDS0 = INS_LDS > GATHER_LDS ? INS_LDS : GATHER_LDS;
