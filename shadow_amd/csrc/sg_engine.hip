@@ -3836,12 +3836,17 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
-    // host partitions: HP hosts per k_proc workgroup (power of two), about
-    // one partition per CU
+    // host partitions: HP hosts per k_proc workgroup, about one partition per
+    // CU: HP = ceil(L / 256) rounded up to a multiple of 16 (P = 245 at 1M
+    // hosts with powers of two left 11 CUs idle).  A shard above 64k hosts
+    // keeps at least 1024 hosts per partition: at 125k hosts (one of eight
+    // shards of configs[3]) every kernel is at its latency floor, and half as
+    // many workgroups halve the contention on the shared bucket and partition
+    // counters: 44.8-45.7 -> 39.7-39.9 us per world-1 step (profiles/r04/hp125k)
     const uint32_t hp_env = env_u32("SG_HP", 0);
-    // one partition per CU: HP = ceil(L / 256) rounded up to a multiple of 16
-    // (P = 245 at 1M hosts with powers of two left 11 CUs idle)
-    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, hp_env ? hp_env : ((d.L + 255) / 256 + 15) / 16 * 16));
+    uint32_t hp_auto = ((d.L + 255) / 256 + 15) / 16 * 16;
+    if (d.L > 65536 && hp_auto < 1024) hp_auto = 1024;
+    d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, hp_env ? hp_env : hp_auto));
     d.hpdiv = make_div32(d.HP);
     d.P = (d.L + d.HP - 1) / d.HP;
     if (d.P > PMAX) {
