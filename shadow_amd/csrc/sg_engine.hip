@@ -3839,13 +3839,15 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // host partitions: HP hosts per k_proc workgroup, about one partition per
     // CU: HP = ceil(L / 256) rounded up to a multiple of 16 (P = 245 at 1M
     // hosts with powers of two left 11 CUs idle).  A shard above 64k hosts
-    // keeps at least 1024 hosts per partition: at 125k hosts (one of eight
-    // shards of configs[3]) every kernel is at its latency floor, and half as
-    // many workgroups halve the contention on the shared bucket and partition
-    // counters: 44.8-45.7 -> 39.7-39.9 us per world-1 step (profiles/r04/hp125k)
+    // keeps at least 2048 hosts per partition: at 125k and 250k hosts (one of
+    // eight or four shards of configs[3]) every kernel is at its latency
+    // floor, and fewer workgroups cut the contention on the shared bucket and
+    // partition counters: world-1 steps 44.8-45.7 -> 39.5-40.2 us at 125k,
+    // 48.9-49.1 -> 44.8-46.2 us at 250k; 500k keeps 1968 (3907 was slower)
+    // (profiles/r04/hp125k)
     const uint32_t hp_env = env_u32("SG_HP", 0);
     uint32_t hp_auto = ((d.L + 255) / 256 + 15) / 16 * 16;
-    if (d.L > 65536 && hp_auto < 1024) hp_auto = 1024;
+    if (d.L > 65536 && hp_auto < 2048) hp_auto = 2048;
     d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, hp_env ? hp_env : hp_auto));
     d.hpdiv = make_div32(d.HP);
     d.P = (d.L + d.HP - 1) / d.HP;
