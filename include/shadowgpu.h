@@ -388,16 +388,17 @@ int sg_engine_stamps(sg_engine* e, uint64_t* out, uint64_t capacity, uint64_t* n
  *   step_send(e, send) — on a process step: pops + PHOLD body + local MIN;
  *       events for other shards go to a per-peer outbox.  On every step: up to
  *       exchange_cap outbox events per peer are written into send, which is
- *       [G][rows][3] int64 (rows = sg_engine_exchange_rows): per peer block two
+ *       [G][rows][2] int64 (rows = sg_engine_exchange_rows): per peer block four
  *       header rows {n, sender has more, local MIN next time, local min jump ms,
- *       overflow flags, round} then n triples {time, src << 40 | srcHostEventID,
- *       dst};
- *   (caller) all_to_all of send → recv, equal [rows][3] blocks per peer;
- *   step_recv(e, recv) — local new events into the queues, received triples
+ *       overflow flags, round, time base (the step's window start), 0} then n
+ *       16-B event rows {time - time base | destination's index in the
+ *       receiving shard << 40, src << 40 | srcHostEventID};
+ *   (caller) all_to_all of send → recv, equal [rows][2] blocks per peer;
+ *   step_recv(e, recv) — local new events into the queues, received events
  *       due in the new window straight into their hosts' partitions; the next
  *       window from the G received headers (the MIN all-reduce of
  *       scheduler.c:386-408 / master.c:450-480, carried by the all-to-all).
- *       The other received triples are queued by the next step_send's kernel,
+ *       The other received events are queued by the next step_send's kernel,
  *       so recv must stay intact until the next step_send has been enqueued
  *       (the next all-to-all overwrites it only after that).  When any sender
  *       still has outbox leftovers the next step is a drain step (same window,

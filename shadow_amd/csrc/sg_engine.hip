@@ -96,9 +96,14 @@ constexpr uint32_t NBMAX = 2046;      // buckets one window spans, at most (buck
 constexpr uint64_t HDR_REC = 1ull << 63;  // k_proc send list: a host's header record
                                           // {evc, HDR_REC | active index << 32 | host}
 constexpr uint64_t PAD_REC = 1ull << 62;  // with HDR_REC: a skip record (a draw that selected no host)
-// exchange block = HDR header rows + exchange_cap event rows, 3 x int64 per row
-constexpr int HDR = 2;
-enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND };
+// exchange block = HDR header rows + exchange_cap event rows, RW x int64 per
+// row.  An event row is 16 B: {time - the sender's window start (40 bits) |
+// destination's index in the receiving shard << 40, src << 40 |
+// srcHostEventID}; the window start rides in the header (H_BASE), so the
+// all-to-all moves two thirds of the bytes of {time, key, destination} rows.
+constexpr int HDR = 4;
+constexpr int RW = 2;
+enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND, H_BASE };
 // overflow flags
 enum Ovf : uint64_t {
     OV_PROC = 1, OV_PART = 2, OV_POOL = 4, OV_XCHG = 8, OV_STEP = 16, OV_HORIZON = 32,
@@ -353,11 +358,11 @@ struct Dev {
     uint32_t* remn;           // [P] staged events for other shards
     Slot* rem;                // [P][ECAP]
     uint32_t* rem_dst;        // [P][ECAP]
-    int64_t* xsend;           // [G][xrows][3] this step's exchange blocks (set by step_send)
-    const int64_t* xrecv;     // [G][xrows_in][3] the previous step's received blocks (k_proc stages
+    int64_t* xsend;           // [G][xrows][RW] this step's exchange blocks (set by step_send)
+    const int64_t* xrecv;     // [G][xrows_in][RW] the previous step's received blocks (k_proc stages
                               // what k_scatter did not route), or null
     uint64_t xrows_in, xcap_in;  // their layout (the exchange cap may have changed since)
-    int64_t* outq;            // [G][oreg][3] per-peer outbox regions (rows < xcap go
+    int64_t* outq;            // [G][oreg][RW] per-peer outbox regions (rows < xcap go
                               // straight into xsend on a process step)
     uint64_t oreg;            // rows per peer region (P * ECAP: every staged event fits)
     uint64_t* outn;           // [G]
@@ -1625,7 +1630,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
 // (hdr: the G blocks' HDR_W header words, LDS); 2: boot (the first window is
 // listed already).  One thread, from the LDS copy of the round state
 // (load_round_state), so no load of it waits for another.
-constexpr uint32_t HDR_W = HDR * 3;  // header words per exchange block
+constexpr uint32_t HDR_W = HDR * RW;  // header words per exchange block
 constexpr uint32_t RSW = sizeof(RoundState) / 8;
 static_assert(sizeof(RoundState) % 8 == 0 && RSW <= 64, "one word per lane of a wave");
 __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const int64_t* hdr, StepView& sv) {
@@ -1734,7 +1739,7 @@ __device__ __forceinline__ void load_round_state(const Dev& d, int mode, const i
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q) {
             const uint32_t i = lane + q * 64, j = i < nh ? i : 0u;
-            h[q] = recv[(size_t)(j / HDR_W) * d.xrows * 3 + j % HDR_W];
+            h[q] = recv[(size_t)(j / HDR_W) * d.xrows * RW + j % HDR_W];
         }
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q)
@@ -1770,7 +1775,7 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
             lm = sv.rmin0 < lm ? sv.rmin0 : lm;
             lm = lm < SIMTIME_MAX ? lm : SIMTIME_MAX;
             lj = rs->jmin < lj ? rs->jmin : lj;
-            const int64_t* own = recv + (size_t)d.g * d.xrows * 3;
+            const int64_t* own = recv + (size_t)d.g * d.xrows * RW;
             if ((uint64_t)own[H_MIN] != lm || (uint64_t)own[H_JMIN] != lj) flag(d, OV_BUG);
         }
         rs->steps += 1;
@@ -1886,8 +1891,9 @@ __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t
     if (threadIdx.x < d.G) {
         const uint32_t p = threadIdx.x;
         const uint64_t left = atomic_read(&d.outn[p]) - d.sent[p];
-        int64_t* blk = d.xsend + (size_t)p * d.xrows * 3;
+        int64_t* blk = d.xsend + (size_t)p * d.xrows * RW;
         blk[H_N] = (int64_t)(left < d.xcap ? left : d.xcap);
+        blk[H_BASE] = (int64_t)rs->S;  // the rows' time base: the step's window start
         blk[H_MIN] = (int64_t)m;
         blk[H_JMIN] = (int64_t)j;
         blk[H_OVF] = (int64_t)atomic_read(&rs->overflow);
@@ -1900,7 +1906,7 @@ __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t
             more |= (on - d.sent[q] > d.xcap) ? 1u : 0u;
             peak = q != d.g && on > peak ? on : peak;
         }
-        for (uint32_t q = 0; q < d.G; ++q) d.xsend[(size_t)q * d.xrows * 3 + H_MORE] = (int64_t)more;
+        for (uint32_t q = 0; q < d.G; ++q) d.xsend[(size_t)q * d.xrows * RW + H_MORE] = (int64_t)more;
         rs->peak_peer = peak;
     }
 }
@@ -1910,9 +1916,9 @@ __device__ __forceinline__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t
     for (uint32_t p = 0; p < d.G; ++p) {
         const uint64_t left = d.outn[p] - d.sent[p];
         const uint64_t n = left < d.xcap ? left : d.xcap;
-        int64_t* dst = d.xsend + ((size_t)p * d.xrows + HDR) * 3;
-        const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * 3;
-        for (uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x; i < n * 3; i += (uint64_t)nblk * blockDim.x)
+        int64_t* dst = d.xsend + ((size_t)p * d.xrows + HDR) * RW;
+        const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * RW;
+        for (uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x; i < n * RW; i += (uint64_t)nblk * blockDim.x)
             dst[i] = src[i];
     }
     if (blk == 0) {
@@ -1952,37 +1958,43 @@ __device__ __forceinline__ void near_resolve(const Dev& d, int32_t x, uint2 a, u
 // EXACT: d.dst_near (a destination is two adjacent 8-byte records per send);
 // the other instantiation resolves destinations through the weight probes
 // (and bisection).  ROWS: d.lds_rows (path records from the partition's LDS rows).
-// Exclusive offsets of the received blocks' event counts (own block: 0).
-// rows / cap: the blocks' layout (HDR + cap rows per peer).
+// Exclusive offsets of the received blocks' event counts (own block: 0) and
+// the blocks' time bases.  rows / cap: the blocks' layout (HDR + cap rows per peer).
 __device__ __forceinline__ uint64_t recv_offsets(const Dev& d, const int64_t* recv, uint64_t rows, uint64_t cap,
-                                                 uint32_t* s_off, uint64_t* s16,
-                                 bool check) {
+                                                 uint32_t* s_off, uint64_t* s_rbase, uint64_t* s16, bool check) {
     const uint32_t s = threadIdx.x;
-    uint64_t c = 0;
+    uint64_t c = 0, base = 0;
     if (s < d.G && s != d.g) {
-        const uint64_t n = (uint64_t)recv[(size_t)s * rows * 3 + H_N];
+        const int64_t* blk = recv + (size_t)s * rows * RW;
+        const uint64_t n = (uint64_t)blk[H_N];
+        base = (uint64_t)blk[H_BASE];
         if (n <= cap) c = n;
         else if (check) flag(d, OV_XCHG);
     }
     uint64_t total;
     const uint64_t run = block_excl_scan(c, s16, &total);
-    if (s < d.G) s_off[s] = (uint32_t)run;
+    if (s < d.G) {
+        s_off[s] = (uint32_t)run;
+        s_rbase[s] = base;
+    }
     __syncthreads();
     return total;
 }
 
 // Received event `idx` of the concatenated blocks: t, key, dst_local.
 __device__ __forceinline__ bool recv_event(const Dev& d, const int64_t* recv, uint64_t rows, const uint32_t* s_off,
-                                           uint32_t idx, uint64_t& t, uint64_t& k, uint32_t& dl) {
+                                           const uint64_t* s_rbase, uint32_t idx, uint64_t& t, uint64_t& k,
+                                           uint32_t& dl) {
     uint32_t lo = 0, hi = d.G - 1;  // last block with s_off <= idx
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (s_off[mid] <= idx) lo = mid; else hi = mid - 1;
     }
-    const int64_t* row = recv + ((size_t)lo * rows + HDR + (idx - s_off[lo])) * 3;
-    t = (uint64_t)row[0];
+    const int64_t* row = recv + ((size_t)lo * rows + HDR + (idx - s_off[lo])) * RW;
+    const uint64_t w0 = (uint64_t)row[0];
+    t = s_rbase[lo] + (w0 & M40);
     k = (uint64_t)row[1];
-    dl = (uint32_t)row[2] - d.lo;
+    dl = (uint32_t)(w0 >> 40);
     return dl < d.L;
 }
 
@@ -2024,7 +2036,8 @@ template <class Count>
 __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* recv, uint32_t part, uint32_t nparts,
                                                    bool routed, uint64_t S, uint64_t E, ProcShared& sh, bool& ovf,
                                                    uint32_t* s_off, uint64_t* s16, Count count) {
-    const uint64_t total = recv_offsets(d, recv, d.xrows_in, d.xcap_in, s_off, s16, true);  // barrier inside
+    __shared__ uint64_t s_rbase[MAXG];  // the received blocks' time bases
+    const uint64_t total = recv_offsets(d, recv, d.xrows_in, d.xcap_in, s_off, s_rbase, s16, true);  // barrier inside
     const uint64_t lo = total * part / nparts, hi = total * (part + 1) / nparts;
     uint64_t mn = UINT64_MAX;
     for (uint64_t i0 = lo; i0 < hi; i0 += blockDim.x) {
@@ -2032,7 +2045,7 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
         uint64_t t = 0, k = 0;
         uint32_t dl = 0;
         bool v = idx < hi;
-        if (v && !recv_event(d, recv, d.xrows_in, s_off, (uint32_t)idx, t, k, dl)) {
+        if (v && !recv_event(d, recv, d.xrows_in, s_off, s_rbase, (uint32_t)idx, t, k, dl)) {
             flag(d, OV_XCHG);
             v = false;
         }
@@ -2973,11 +2986,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t q = owner_of(d, dst);
             const uint64_t r = s_obase[q] + atomicAdd(&s_oslot[q], 1u);
             const Slot ev = d.rem[so];
-            int64_t* o = r < d.xcap ? d.xsend + ((uint64_t)q * d.xrows + HDR + r) * 3
-                                    : d.outq + ((uint64_t)q * d.oreg + r) * 3;
-            o[0] = (int64_t)ev.t;
+            int64_t* o = r < d.xcap ? d.xsend + ((uint64_t)q * d.xrows + HDR + r) * RW
+                                    : d.outq + ((uint64_t)q * d.oreg + r) * RW;
+            const uint64_t rel = ev.t - S;  // new events are at or after the window's end
+            if (rel >> 40) a.overflow = true;  // beyond 2^40 ns (18 min) of the window start
+            o[0] = (int64_t)((rel & M40) | ((uint64_t)(dst - d.bounds[q]) << 40));
             o[1] = (int64_t)ev.k;
-            o[2] = (int64_t)dst;
         }
     }
     if (stamp && tid == 0) stamp[13] = __builtin_amdgcn_s_memrealtime();
@@ -3215,6 +3229,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     __shared__ int64_t s_hdr[MAXG * HDR_W];      // several shards: the received blocks' headers
     __shared__ uint64_t s_gsw[3];                // gather: the GSpec header
     __shared__ uint32_t s_routed;
+    __shared__ uint64_t s_rbase[MAXG];           // receive role: the received blocks' time bases
     const uint32_t R = d.R, blk = blockIdx.x, tid = threadIdx.x;
     const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = gridDim.x - 2;  // gather workgroups [g0, gx)
     // wave 0: the round state (and headers) in one batch of loads, then thread
@@ -3480,13 +3495,14 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         s_pc[p] = 0;
         s_pk[p] = 0;
     }
-    const uint64_t total = recv_offsets(d, recv, d.xrows, d.xcap, s_off, s16, false);  // barrier inside
+    const uint64_t total = recv_offsets(d, recv, d.xrows, d.xcap, s_off, s_rbase, s16, false);  // barrier inside
     const uint64_t lo = total * w / g3, hi = total * (w + 1) / g3;
     if (!ro.listed) break;  // uniform: no new window, nothing is due
     for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
         uint64_t t, k;
         uint32_t dl;
-        if (recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) && t < ro.E) atomicAdd(&s_pc[part_of(d, dl)], 1u);
+        if (recv_event(d, recv, d.xrows, s_off, s_rbase, (uint32_t)i, t, k, dl) && t < ro.E)
+            atomicAdd(&s_pc[part_of(d, dl)], 1u);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
@@ -3504,7 +3520,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     for (uint64_t i = lo + threadIdx.x; i < hi; i += K3_T) {
         uint64_t t, k;
         uint32_t dl;
-        if (!recv_event(d, recv, d.xrows, s_off, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
+        if (!recv_event(d, recv, d.xrows, s_off, s_rbase, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
         const uint32_t p = part_of(d, dl);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
         if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
@@ -3762,6 +3778,12 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         sg_set_error("sg_engine_create: shard has no hosts");
         return SG_ERR_INVAL;
     }
+    for (uint32_t i = 0; G > 1 && i < G; ++i)
+        if (d.bounds[i + 1] - d.bounds[i] >= (1u << 24)) {  // a 16-B exchange row keeps 24 bits of it
+            sg_set_error("sg_engine_create: shard %u has %u hosts, at most 2^24 with several shards", i,
+                         d.bounds[i + 1] - d.bounds[i]);
+            return SG_ERR_INVAL;
+        }
     d.load = p.load;
     d.workload = p.workload;
     if (p.workload == SG_WORKLOAD_GOSSIP) {
@@ -4073,7 +4095,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         ALLOC(D.rem, P * D.ECAP);
         ALLOC(D.rem_dst, P * D.ECAP);
         D.oreg = (uint64_t)P * D.ECAP;
-        ALLOC(D.outq, (size_t)G * D.oreg * 3);
+        ALLOC(D.outq, (size_t)G * D.oreg * RW);
         ALLOC(D.outn, G);
         ALLOC(D.sent, G);
     }
@@ -4522,7 +4544,7 @@ int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap) {
     // k_proc, and the caller reallocates its buffers for the new cap: keep a
     // copy (in the old layout, which the next k_proc decodes)
     if (e->last_recv && e->last_recv != e->recv_hold) {
-        const size_t bytes = (size_t)e->d.G * e->last_rows * 3 * sizeof(int64_t);
+        const size_t bytes = (size_t)e->d.G * e->last_rows * RW * sizeof(int64_t);
         if (bytes > e->recv_hold_bytes) {
             if (e->recv_hold) HIPCHK(hipFree(e->recv_hold));
             e->recv_hold = nullptr;
@@ -4807,7 +4829,7 @@ int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, 
                      c->world, e->d.g, e->d.G);
         return SG_ERR_INVAL;
     }
-    const size_t per_peer = (size_t)e->d.xrows * 3;  // int64 elements per peer block
+    const size_t per_peer = (size_t)e->d.xrows * RW;  // int64 elements per peer block
     auto step = [&]() -> int {
         int r = sg_engine_step_send(e, send);
         if (r) return r;

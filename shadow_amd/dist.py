@@ -8,7 +8,7 @@ A step:
                  per peer into a fixed-size block behind a header that carries
                  the shard's MIN next time, its min discovered latency and its
                  overflow flags;
-  2. all-to-all  one all_to_all_single of equal [rows, 3] int64 blocks —
+  2. all-to-all  one all_to_all_single of equal [rows, 2] int64 blocks —
                  RCCL over xGMI on GPUs (torch.distributed "nccl"), gloo on CPU;
   3. step_recv   local + received events into the destination queues, then the
                  window from the G headers: the MIN "all-reduce" of the window
@@ -66,10 +66,12 @@ class EngineShard:
                           trace_capacity=trace_capacity, stream=self.stream.cuda_stream)
         self._alloc()
 
+    row_words = 2  # int64 words per exchange row (include/shadowgpu.h, step_send)
+
     def _alloc(self):
         rows = self.eng.exchange_rows()
         self.rows = rows
-        self.send = torch.zeros((self.world, rows, 3), dtype=torch.int64, device=self.dev)
+        self.send = torch.zeros((self.world, rows, self.row_words), dtype=torch.int64, device=self.dev)
         self.recv = torch.zeros_like(self.send)
 
     def _all_ok(self, ok: bool) -> bool:
@@ -371,7 +373,7 @@ def bench(args, make_shard=None):
         vals = [kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES]  # us per step per class
         vals += [kt["process"][1], proc_bytes(sb["pops"] - sa["pops"], a2 - a1),
                  kt["insert"][1], scatter_bytes(moves), kt["exchange"][1],
-                 float(world * shard.rows * 3 * 8)]  # exchange bytes this rank sends per step
+                 float(world * shard.rows * getattr(shard, "row_words", 3) * 8)]  # exchange bytes this rank sends per step
         rows = _gather_rows(vals, cdev)
     else:
         rows = None
