@@ -3840,7 +3840,9 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.W = W;
     d.R = (uint32_t)(span / W + 3);
-    d.ring32 = (uint64_t)d.R * W < (1ull << 32);
+    // SG_NO_RING32=1 (tests): the 64-bit bucket arithmetic everywhere, as for a
+    // calendar whose horizon passes 2^32 ns
+    d.ring32 = (uint64_t)d.R * W < (1ull << 32) && env_u32("SG_NO_RING32", 0) == 0;
     d.wdiv = make_div32(W);
     // the receive role's workgroups: none on one shard (a world-1 step receives
     // only its own header block)

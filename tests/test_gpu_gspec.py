@@ -42,3 +42,19 @@ def test_c4_gspec_modes_match_the_oracle(mode, monkeypatch):
         assert g["guessed"] >= 100, g  # steady rounds are one whole bucket each
     else:
         assert g["guessed"] == 0, g
+
+
+def test_c4_64bit_bucket_arithmetic_matches_the_oracle(monkeypatch):
+    """The calendar's bucket indices by 64-bit division (the path a calendar
+    whose horizon passes 2^32 ns takes: k_scatter's planner, the insert and the
+    bucket bins), forced on configs[3] with SG_NO_RING32=1, against the
+    per-round fixture."""
+    monkeypatch.setenv("SG_NO_RING32", "1")
+    eng = Engine(phold.c4_config(n_hosts=1_000_000))
+    eng.boot()
+    eng.run(60)
+    st = eng.stats()
+    assert st["rounds"] == 60 and st["overflow"] == 0
+    assert (st["pops"], st["window_start"], st["window_end"]) == (ROWS[60][1], ROWS[60][3], ROWS[60][4])
+    hs = eng.host_state()
+    assert state_fingerprint(eng.first_host, hs["digest"], hs["pops"], hs["rng"], hs["ev"]) == ROWS[60][2]
