@@ -3142,8 +3142,9 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
             b = ro.bS + o;
             off[q] = (uint32_t)rel - o * (uint32_t)W;
             const uint32_t r0 = ro.bSr + o;
-            rb[q] = v[q] ? (r0 >= R ? r0 - R : r0) : 0u;
-            if (v[q] && (t[q] < ro.bSW || (rel >> 32) || o >= R)) flag(d, OV_BUG);
+            if (v[q] && (t[q] < ro.bSW || (rel >> 32) || o >= R)) flag(d, OV_BUG);  // beyond k_proc's horizon
+            const uint32_t r1 = r0 >= R ? r0 - R : r0;
+            rb[q] = v[q] && r1 < R ? r1 : 0u;  // clamped: a bad record writes in bounds, flagged
         } else {
             b = t[q] / W;
             off[q] = (uint32_t)(t[q] - b * W);
@@ -3477,6 +3478,10 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
                 t[q] = S + (r[q].a & M40);
                 k[q] = r[q].k;
                 dl[q] = (uint32_t)(r[q].a >> 40);
+                if (v[q] && dl[q] >= d.L) {  // a staged record is always a local host: clamped, flagged
+                    flag(d, OV_BUG);
+                    dl[q] = 0;
+                }
             }
             insert_batch(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
