@@ -172,6 +172,7 @@ def run_single(args):
     eng.boot()
     eng.set_graph(args.graph)
     eng.run(args.warmup, batch=args.graph or args.batch)
+    eng.prepare_graph()  # graphs on: the first timed batch replays, it does not capture
     s0 = eng.stats()
     eng.sync()
     # timed region: K rounds, nothing but the rounds on the stream (at most two

@@ -338,6 +338,10 @@ int sg_engine_enqueue_round(sg_engine* e);
 /* n rounds without reading the round state back (graph-batched when
  * sg_engine_set_graph is on); at most two batches stay queued on the stream. */
 int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds);
+/* Graphs on (sg_engine_set_graph): capture one batch of rounds into the graph
+ * now without running it, so that the first replay pays no capture and
+ * instantiation (a timed region's first batch).  No-op with graphs off. */
+int sg_engine_graph_prepare(sg_engine* e);
 int sg_engine_sync(sg_engine* e);
 int sg_engine_stats(sg_engine* e, sg_round_stats* out);   /* synchronises */
 /* Per local host (index - first_host): trace digest, pops, rng state, event counter. */
@@ -419,7 +423,7 @@ int sg_engine_step_recv(sg_engine* e, const int64_t* recv);
  * creates (sg_comm_unique_id) and the caller broadcasts; RCCL is opened with
  * dlopen, so the library the process already loaded (e.g. torch's) is the one
  * used.  run_steps enqueues n steps without synchronising; send / recv are
- * device buffers of [G][rows][3] int64.  With sg_engine_set_graph(e, b > 0)
+ * device buffers of [G][rows][2] int64.  With sg_engine_set_graph(e, b > 0)
  * (and for sg_engine_run in round mode) every b steps / rounds are captured once
  * into a hipGraph and replayed; a graph is rebuilt when the buffers, the
  * communicator, exchange_cap or the path-counter table change.  set_graph

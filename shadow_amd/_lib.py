@@ -101,7 +101,7 @@ EXPORTS = [
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
     "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv",
     "sg_engine_enqueue_rounds", "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy",
-    "sg_engine_run_steps", "sg_engine_set_graph", "sg_engine_kernel_times",
+    "sg_engine_run_steps", "sg_engine_set_graph", "sg_engine_graph_prepare", "sg_engine_kernel_times",
     "sg_engine_set_timing", "sg_engine_set_timing_mask", "sg_comm_available", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_barrier_timers", "sg_engine_barrier_times", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
@@ -175,6 +175,7 @@ def lib():
     L.sg_comm_destroy.argtypes = [C.c_void_p]
     L.sg_engine_run_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     L.sg_engine_set_graph.argtypes = [C.c_void_p, C.c_uint32]
+    L.sg_engine_graph_prepare.argtypes = [C.c_void_p]
     _lib = L
     return L
 

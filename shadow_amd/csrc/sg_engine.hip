@@ -4318,7 +4318,7 @@ int sg_engine_enqueue_round(sg_engine* e) {
 // iterations are captured once into a hipGraph and the graph is replayed while
 // its key (buffers, communicator, captured kernel arguments) is unchanged.
 extern "C++" template <typename F>
-static int enqueue_batch(sg_engine* e, const sg_engine::GraphKey& key, uint32_t n, F&& body) {
+static int enqueue_batch(sg_engine* e, const sg_engine::GraphKey& key, uint32_t n, F&& body, bool launch = true) {
     const bool use = e->graph_batch && n == e->graph_batch && !e->timing && !e->debug_sync;
     if (!use) {
         for (uint32_t i = 0; i < n; ++i)
@@ -4349,8 +4349,23 @@ static int enqueue_batch(sg_engine* e, const sg_engine::GraphKey& key, uint32_t 
         }
         e->gkey = key;
     }
-    HIPCHK(hipGraphLaunch(e->gexec, e->stream));
+    if (launch) HIPCHK(hipGraphLaunch(e->gexec, e->stream));
     return SG_OK;
+}
+
+int sg_engine_graph_prepare(sg_engine* e) {
+    if (!e || !e->booted) {
+        sg_set_error("sg_engine_graph_prepare: engine not booted");
+        return SG_ERR_STATE;
+    }
+    if (e->d.G != 1 || e->d.outn) {
+        sg_set_error("sg_engine_graph_prepare: step-mode engine, the step loop captures its own graph");
+        return SG_ERR_STATE;
+    }
+    const uint32_t n = e->graph_batch;
+    if (!n) return SG_OK;  // graphs off: nothing to capture
+    const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, nullptr, n};
+    return enqueue_batch(e, key, n, [&] { return sg_engine_enqueue_round(e); }, false);
 }
 
 int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds) {

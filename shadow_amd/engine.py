@@ -81,6 +81,10 @@ class Engine:
         """Capture every `batch` rounds / steps into a hipGraph and replay it (0: off)."""
         L.check(L.lib().sg_engine_set_graph(self.h, batch))
 
+    def prepare_graph(self):
+        """Capture one batch of rounds now without running it (graphs on)."""
+        L.check(L.lib().sg_engine_graph_prepare(self.h))
+
     def sync(self):
         L.check(L.lib().sg_engine_sync(self.h))
 

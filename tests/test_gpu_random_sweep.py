@@ -1,5 +1,6 @@
 """GPU: a seeded sweep of randomly drawn small PHOLD configurations, each run
-through the unsharded engine and through 1-3 in-process shards, against the CPU
+through the unsharded engine, through 1-3 in-process shards and through the
+drop-in `gpu` policy at 1-8 workers, against the CPU
 oracle (bit-exact: per-host digests, pop counts, rand_r states, event-id
 counters and the global counters).
 
@@ -12,7 +13,7 @@ failure names its seed and reproduces exactly."""
 import numpy as np
 import pytest
 
-from shadow_amd import phold
+from shadow_amd import phold, policy
 from shadow_amd import _lib as L
 from oracle import oracle as O
 
@@ -44,6 +45,25 @@ def _draw(seed):
     world = int(r.integers(1, 4))
     xcap = int(r.choice([7, 64, 4096]))
     return cfg, queue_cap, world, xcap
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_config_gpu_policy(seed):
+    """The same draws through the drop-in `gpu` SchedulerPolicy (Mode P: CPU
+    workers, device queues) under the Shadow-style round driver, at a drawn
+    worker count (more workers than hosts included)."""
+    cfg, *_ = _draw(seed)
+    workers = int(np.random.default_rng(seed + 7).choice([1, 2, 3, 5, 8]))
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs, st = ref.host_state(), ref.stats()
+    r = policy.run_phold(cfg, workers, policy.gpu_ops(workers, cfg["n_hosts"]))
+    for k, rk in (("digest", "digest"), ("pops_per_host", "pops"), ("rng", "rng"), ("ev", "ev")):
+        assert np.array_equal(r[k], rs[rk]), (seed, workers, k)
+    for k in ("rounds", "pops", "sends", "drop_reliability", "drop_endtime", "bumped"):
+        assert r[k] == st[k], (seed, workers, k)
 
 
 LARGE_SEEDS = list(range(201, 209))

@@ -115,15 +115,21 @@ def test_native_rccl_steps_world1_match_oracle(graph):
     sh.close_native()
 
 
-@pytest.mark.parametrize("graph", [3, 8])
-def test_graph_rounds_match_oracle(graph):
+@pytest.mark.parametrize("graph,prepare", [(3, False), (8, False), (8, True)])
+def test_graph_rounds_match_oracle(graph, prepare):
     """Round mode replayed from captured hipGraphs (sg_engine_run and
-    sg_engine_enqueue_rounds), including a partial last batch."""
+    sg_engine_enqueue_rounds), including a partial last batch; prepare: the
+    graph captured ahead by sg_engine_graph_prepare, which must run nothing."""
     from shadow_amd.engine import Engine
     cfg = phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)
     eng = Engine(cfg, device=0)
     eng.boot()
     eng.set_graph(graph)
+    if prepare:
+        r0 = eng.stats()["rounds"]
+        eng.prepare_graph()
+        eng.prepare_graph()  # the same key: kept
+        assert eng.stats()["rounds"] == r0
     eng.enqueue_rounds(2 * graph + 1)
     eng.run(batch=graph)
     ref = O.Sim(cfg)
