@@ -2100,6 +2100,9 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 // reservation bases at launch, beside the plan (1), or after it (0, default:
 // the gather's first loads go out ahead of them; 51.1-51.4 against 51.6-52.0
 // us per round, profiles/r04/insert_pre).
+#ifndef SG_GFIRST
+#define SG_GFIRST 1
+#endif
 #ifndef SG_INS_PRE
 #define SG_INS_PRE 0
 #endif
@@ -3231,8 +3234,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     __shared__ uint64_t s_gsw[3];                // gather: the GSpec header
     __shared__ uint32_t s_routed;
     __shared__ uint64_t s_rbase[MAXG];           // receive role: the received blocks' time bases
-    const uint32_t R = d.R, blk = blockIdx.x, tid = threadIdx.x;
     const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = gridDim.x - 2;  // gather workgroups [g0, gx)
+    // role order [insert P][receive G3][gather][refill][rmin]; SG_GFIRST
+    // dispatches the gather workgroups (the launch's long pole) first
+    const uint32_t blk = SG_GFIRST ? (blockIdx.x < gx - g0 ? g0 + blockIdx.x
+                                      : blockIdx.x < gx ? blockIdx.x - (gx - g0) : blockIdx.x)
+                                   : blockIdx.x;
+    const uint32_t R = d.R, tid = threadIdx.x;
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
     // waited for until the workgroup's end: the last to arrive publishes then.
