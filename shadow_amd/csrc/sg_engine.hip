@@ -2097,14 +2097,16 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #define SG_SORT_LDS 0
 #endif
 // SG_INS_PRE: k_scatter's insert role loads its first staged events and its
-// reservation bases at launch, beside the plan (1), or after it (0, default:
-// the gather's first loads go out ahead of them; 51.1-51.4 against 51.6-52.0
-// us per round, profiles/r04/insert_pre).
+// reservation bases at launch, beside the plan (1, default), or after it (0).
+// With the gather dispatched after the inserts, 0 was faster (51.1-51.4
+// against 51.6-52.0 us per round, profiles/r04/insert_pre); with the gather
+// first (SG_GFIRST) the insert role is the long pole and 1 wins (48.9-49.1
+// against 49.7-50.0, profiles/r04/inspre2).
 #ifndef SG_GFIRST
 #define SG_GFIRST 1
 #endif
 #ifndef SG_INS_PRE
-#define SG_INS_PRE 0
+#define SG_INS_PRE 1
 #endif
 // SG_FLAT_LDSB: the barrier after the flat pass orders LDS only (default;
 // profiles/r04/flatb: 52.2 against 52.5-53.3 us/round, interleaved).
