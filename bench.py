@@ -1,6 +1,8 @@
 """bench.py — committed events/s of the MI355X event-scheduling core on the
 BASELINE.json metric's workload: synthetic PHOLD, 1M hosts x 16 events,
 log-normal latency over 1024 vertices, runahead 1 ms (configs[3]).
+--workload c2 / c5 measures configs[1] (10k-host PHOLD, 50 ms mesh) / configs[4]
+(100k-host lossy gossip) the same way (shadow_amd/workloads.py).
 
 A step is one conservative round (k_proc: pop + execute + stage; k_scatter:
 insert + gather + next window) over the whole host population.  W warmup rounds (the boot round included) run untimed; K
@@ -19,7 +21,9 @@ Also reported:
                moves).
   cpu_baseline the CPU reference policy (oracle/host_steal.c, the host_steal
                restatement) on the same workload, timed on this machine's host
-               cores over a bounded sample of rounds (rank 0, N=1).
+               cores over a bounded sample of rounds (rank 0, N=1): value with
+               priority_queue.c's heap and its GLib position map (the
+               reference's cost), plain_heap_value with plain binary heaps.
 """
 from __future__ import annotations
 
@@ -32,32 +36,36 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from shadow_amd import workloads as WL  # noqa: E402
 from shadow_amd.roofline import HBM_PEAK_GBS, kernel_line, proc_bytes, scatter_bytes  # noqa: E402
-# PMC HBM bytes per launch of the dominant kernel for this default workload:
-# rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
+# PMC HBM bytes per launch of each kernel for each workload: rocprofv3
+# FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = os.path.join(ROOT, "profiles", "r04", "bench", "pmc.json")
+PMC_JSON = {"c4": os.path.join(ROOT, "profiles", "r04", "bench", "pmc.json"),
+            "c2": os.path.join(ROOT, "profiles", "r05", "workloads", "c2", "pmc.json"),
+            "c5": os.path.join(ROOT, "profiles", "r05", "workloads", "c5", "pmc.json")}
 DOMINANT = "k_proc"
 
 
-def pmc_traffic(n_hosts, kernel=DOMINANT):
+def pmc_traffic(workload, n_hosts, kernel=DOMINANT):
     """(corrected PMC bytes per launch of `kernel`, the bytes with FETCH_SIZE as
     counted, source) from the committed profile of this workload, or Nones."""
-    if n_hosts != 1_000_000 or not os.path.exists(PMC_JSON):
+    path = PMC_JSON.get(workload)
+    if (workload == "c4" and n_hosts != 1_000_000) or not path or not os.path.exists(path):
         return None, None, None
-    ks = json.load(open(PMC_JSON))["kernels"]
+    ks = json.load(open(path))["kernels"]
     k = next((v for n, v in ks.items() if n == kernel or n.startswith(kernel + "<")), None)
     if not k:
         return None, None, None
-    return k["traffic_bytes"], k.get("traffic_bytes_lower"), os.path.relpath(PMC_JSON, ROOT)
+    return k["traffic_bytes"], k.get("traffic_bytes_lower"), os.path.relpath(path, ROOT)
 
 
-def kernel_roofline(name, alg_bytes, avg_s, n_hosts):
+def kernel_roofline(workload, name, alg_bytes, avg_s, n_hosts):
     """One kernel's line of roofline.per_kernel: algorithmic bytes per launch
     over its average launch time against HBM peak, beside the committed PMC
     traffic per launch."""
-    traffic, lower, src = pmc_traffic(n_hosts, name)
+    traffic, lower, src = pmc_traffic(workload, n_hosts, name)
     out = kernel_line(alg_bytes, avg_s)
     out.update(traffic=traffic, traffic_lower=lower,
                traffic_gbs=traffic / avg_s / 1e9 if traffic and avg_s else None, traffic_source=src)
@@ -67,13 +75,15 @@ def kernel_roofline(name, alg_bytes, avg_s, n_hosts):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--hosts", type=int, default=1_000_000)
+    ap.add_argument("--workload", default="c4", choices=sorted(WL.WORKLOADS),
+                    help="c4: configs[3] (the BASELINE metric's, default); c2: configs[1]; c5: configs[4]")
+    ap.add_argument("--steps", type=int, default=None, help="timed rounds (default: the workload's)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed rounds (default: the workload's)")
+    ap.add_argument("--hosts", type=int, default=None, help="c4 only: the host count (default 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-drop-in", action="store_true",
                     help="skip the Mode P (drop-in gpu SchedulerPolicy) leg")
-    ap.add_argument("--cpu-rounds", type=int, default=12)
+    ap.add_argument("--cpu-rounds", type=int, default=12, help="CPU legs: rounds timed")
     ap.add_argument("--cpu-workers", type=int,
                     default=min(16, len(os.sched_getaffinity(0))),
                     help="CPU baseline worker threads (the GPU box's share is 16 cores)")
@@ -92,7 +102,15 @@ def parse():
                          "rehearses the collective path on a one-GPU box)")
     ap.add_argument("--same-device", action="store_true",
                     help="N > 1 rehearsal: every rank on GPU 0 (needs --dist-backend gloo)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WL.get(a.workload)
+    if a.hosts is not None and a.workload != "c4":
+        ap.error("--hosts applies to --workload c4 only")
+    a.warmup = w["warmup"] if a.warmup is None else a.warmup
+    a.steps = w["steps"] if a.steps is None else a.steps
+    a.cfg = w["build"](a.hosts)
+    a.hosts = a.cfg["n_hosts"]
+    return a
 
 
 def _cpu_model() -> str:
@@ -108,30 +126,38 @@ def _cpu_model() -> str:
 def cpu_baseline(cfg, warmup, rounds, workers):
     """The CPU reference policy: oracle/host_steal.c — the
     C restatement of scheduler_policy_host_steal.c — under the Shadow-style
-    round driver (sg_sched.c, worker.c:149-216 semantics), same PHOLD workload.
-    Boot + `warmup` rounds untimed, the next `rounds` rounds timed, at
-    -w `workers` and at -w 1."""
+    round driver (sg_sched.c, worker.c:149-216 semantics), same workload.
+    Boot + `warmup` rounds untimed, the next `rounds` rounds timed.  value and
+    single_thread_value (-w `workers`, -w 1): the per-host queues are
+    priority_queue.c's heap with its GLib hash-table position map, updated on
+    every swap (oracle/libhsglib.so), i.e. the reference's own cost;
+    plain_heap_value: the same policy on plain binary heaps (liborc.so), a
+    lower bound on it."""
     from oracle import oracle as O
     from shadow_amd import policy
 
-    def one(w):
-        ops = O.cpu_policy_ops(True, w, cfg["n_hosts"])
+    def one(w, faithful):
+        ops = O.cpu_policy_ops(True, w, cfg["n_hosts"], faithful=faithful)
         r = policy.run_phold(cfg, w, ops, max_rounds=warmup + rounds, mark_round=warmup)
         return r["marked_pops"] / r["marked_seconds"], r
 
-    v, r = one(workers)
-    v1, _ = one(1) if workers > 1 else (v, r)
+    faithful = O.faithful_available()
+    v, r = one(workers, faithful)
+    v1, _ = one(1, faithful) if workers > 1 else (v, r)
+    vp, _ = one(workers, False) if faithful else (v, r)
+    heap = ("priority_queue.c's heap with its GLib hash-table position map (oracle/libhsglib.so)"
+            if faithful else "plain binary heaps (GLib absent: libhsglib.so not built)")
     return {"value": v, "unit": "events/s", "cores": workers, "kind": "port",
-            "single_thread_value": v1, "cpu_model": _cpu_model(),
-                "sample": f"oracle/host_steal.c (a simplified C restatement of host_steal: plain binary "
-                      f"heaps without the GHashTable index update per swap of priority_queue.c:78-85, "
-                      f"so likely faster than the GLib original) -w {workers} under the "
-                      f"Shadow round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} "
-                      f"timed ({r['marked_pops']} events, {r['marked_seconds']:.2f} s); "
-                      f"single_thread_value is -w 1 on the same rounds"}
+            "single_thread_value": v1, "plain_heap_value": vp, "faithful_heap": faithful,
+            "cpu_model": _cpu_model(),
+            "sample": f"oracle/host_steal.c (the C restatement of host_steal) -w {workers} under the "
+                      f"Shadow round driver, per-host queues: {heap}; same config, rounds "
+                      f"{warmup}..{warmup + rounds} timed ({r['marked_pops']} events, "
+                      f"{r['marked_seconds']:.2f} s); single_thread_value is -w 1 on the same rounds; "
+                      f"plain_heap_value is -w {workers} with plain binary heaps"}
 
 
-def drop_in_policy(cfg, warmup, rounds, workers):
+def drop_in_policy(cfg, warmup, rounds, workers, fixture=None):
     """The drop-in `gpu` SchedulerPolicy (Mode P, sg_policy.c + sg_policy_dev.hip)
     under the same Shadow-style round driver and sample as cpu_baseline: CPU
     workers execute the PHOLD bodies and push/pop through the C-ABI, the GPU
@@ -140,22 +166,46 @@ def drop_in_policy(cfg, warmup, rounds, workers):
     from shadow_amd import policy
     from shadow_amd.trace import state_fingerprint
 
-    def one(w):
-        return policy.run_phold(cfg, w, policy.gpu_ops(w, cfg["n_hosts"]),
-                                max_rounds=warmup + rounds, mark_round=warmup)
+    def one(w, kstats=None):
+        ops = policy.gpu_ops(w, cfg["n_hosts"])
+        if kstats is not None:  # the device half's kernels, timed rounds only
+            policy.kernel_profile(ops, True, warmup)
+        try:
+            r = policy.run_phold(cfg, w, ops, max_rounds=warmup + rounds, mark_round=warmup, free_ops=False)
+            if kstats is not None:
+                kstats.update(policy.kernel_stats(ops))
+        finally:
+            ops.free(ops.data)
+        return r
 
-    r = one(workers)
+    ks = {}
+    r = one(workers, ks)
     r1 = one(1) if workers > 1 else r
     out = {"value": r["marked_pops"] / r["marked_seconds"], "unit": "events/s",
            "workers": workers, "single_thread_value": r1["marked_pops"] / r1["marked_seconds"],
            "sample": f"gpu SchedulerPolicy (Mode P) with {workers} CPU workers under the Shadow "
-                     f"round driver, same 1M-host config, rounds {warmup}..{warmup + rounds} timed "
+                     f"round driver, same config, rounds {warmup}..{warmup + rounds} timed "
                      f"({r['marked_pops']} events, {r['marked_seconds']:.2f} s); single_thread_value "
                      f"is -w 1 on the same rounds"}
+    # the device half's roofline: each kernel class's algorithmic bytes per
+    # launch over its average launch time (dispatch-packet
+    # timestamps) against 8 TB/s, over the timed rounds of the -w run
+    per = {}
+    for name, k in ks.items():
+        if not k["launches"]:
+            continue
+        line = kernel_line(k["alg_bytes"] / k["launches"], k["ms"] / 1e3 / k["launches"])
+        line["launches"] = k["launches"]
+        per[name] = line
+    dev_ms = sum(k["ms"] for k in ks.values())
+    out["roofline"] = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "per_kernel": per,
+                       "device_ms_per_round": dev_ms / max(rounds, 1),
+                       "timing_method": "hipExtLaunchKernelGGL dispatch-packet timestamps of every device "
+                                        "launch of the policy (sg_policy_kernel_profile), timed rounds only"}
     # the policy's end state against the oracle's per-round fixture (parity
     # checker only, after the timed rounds)
-    if cfg["n_hosts"] == 1_000_000 and os.path.exists(FIXTURES):
-        rows = {row[0]: row for row in json.load(open(FIXTURES))["c4_1m"]["rounds"]}
+    if fixture and os.path.exists(FIXTURES):
+        rows = {row[0]: row for row in json.load(open(FIXTURES))[fixture]["rounds"]}
         end = r["rounds"]
         if end in rows:
             fp = state_fingerprint(0, r["digest"], r["pops_per_host"], r["rng"], r["ev"])
@@ -164,10 +214,10 @@ def drop_in_policy(cfg, warmup, rounds, workers):
 
 
 def run_single(args):
-    from shadow_amd import phold
     from shadow_amd.engine import Engine
 
-    cfg = phold.c4_config(n_hosts=args.hosts)
+    cfg = args.cfg
+    wl = WL.get(args.workload)
     eng = Engine(cfg, device=0)
     eng.boot()
     eng.set_graph(args.graph)
@@ -212,17 +262,17 @@ def run_single(args):
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic, traffic_lower, traffic_src = pmc_traffic(args.hosts)
+    traffic, traffic_lower, traffic_src = pmc_traffic(args.workload, args.hosts)
     kus = {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]}
     ins_ms, ins_n = kt["insert"]
     moves = {k: mv2[k] - mv1[k] for k in mv2}
     per_kernel = {
-        DOMINANT: kernel_roofline(DOMINANT, per_launch_bytes, avg_launch_s, args.hosts),
-        "k_scatter": kernel_roofline("k_scatter", scatter_bytes(moves) / max(ins_n, 1),
+        DOMINANT: kernel_roofline(args.workload, DOMINANT, per_launch_bytes, avg_launch_s, args.hosts),
+        "k_scatter": kernel_roofline(args.workload, "k_scatter", scatter_bytes(moves) / max(ins_n, 1),
                                      ins_ms / 1e3 / max(ins_n, 1), args.hosts),
     }
     res = {
-        "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
+        "metric": wl["metric"](cfg),
         "value": pops / dt,
         "unit": "events/s",
         "n_gpus": 1,
@@ -234,9 +284,7 @@ def run_single(args):
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"PHOLD configs[3]: {args.hosts} hosts x 16, V=1024 log-normal "
-                               "latency (median 30 ms, sigma 0.9, min 1 ms), runahead 1 ms, "
-                               "weights rule, seed 1",
+        "config": {"workload": wl["describe"](cfg), "name": args.workload,
                    "n_hosts": args.hosts, "rounds_timed": rounds, "events_timed": pops,
                    "parallelism": "hosts sharded 1 way",
                    "round_loop": f"sg_engine_enqueue_rounds, hipGraph batch {args.graph}" if args.graph
@@ -257,18 +305,18 @@ def run_single(args):
                                       "the rest of ms_per_step is launch gaps"},
         "_end_round": s1["rounds"], "_fingerprint": fp,
     }
+    cw = wl["cpu_warmup"]
     if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)
+        res["cpu_baseline"] = cpu_baseline(cfg, cw, args.cpu_rounds, args.cpu_workers)
     if not args.no_drop_in:
-        res["drop_in_policy"] = drop_in_policy(cfg, args.cpu_rounds, args.cpu_rounds, args.cpu_workers)
+        res["drop_in_policy"] = drop_in_policy(cfg, cw, args.cpu_rounds, args.cpu_workers, wl["fixture"](cfg))
     return res
 
 
 FIXTURES = os.path.join(ROOT, "tests", "golden", "oracle_fixtures.json")
-METRIC = "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact"
 
 
-def parity_check(res, n_hosts):
+def parity_check(res, args):
     """The state at the end of the timed region against the oracle: the host
     state fingerprint (shadow_amd.trace.state_fingerprint over every host's
     trace digest, pops, rand_r state and event counter, summed over ranks) and
@@ -278,20 +326,22 @@ def parity_check(res, n_hosts):
     r, fp = res.pop("_end_round"), res.pop("_fingerprint")
     out = {"round": r, "fingerprint": f"{fp:016x}", "source": None, "match": None}
     fx = None
-    if n_hosts == 1_000_000 and os.path.exists(FIXTURES):
-        fx = json.load(open(FIXTURES)).get("c4_1m")
+    key = WL.get(args.workload)["fixture"](args.cfg)
+    metric = res["metric"]
+    if key and os.path.exists(FIXTURES):
+        fx = json.load(open(FIXTURES)).get(key)
     if fx:
-        out["source"] = f"{os.path.relpath(FIXTURES, ROOT)} c4_1m (oracle, rounds 1..{len(fx['rounds'])})"
+        out["source"] = f"{os.path.relpath(FIXTURES, ROOT)} {key} (oracle, rounds 1..{len(fx['rounds'])})"
         row = next((x for x in fx["rounds"] if x[0] == r), None)
         if row is not None:
             out["match"] = bool(row[2] == fp)
             out["oracle_fingerprint"] = f"{row[2]:016x}"
     res["parity"] = out
     if out["match"] is False:
-        res["metric"] = METRIC.replace("; bit-exact", "") + " (PARITY MISMATCH vs oracle)"
+        res["metric"] = metric.replace("; bit-exact", "") + " (PARITY MISMATCH vs oracle)"
         print("bench: end-of-region state differs from the oracle fixture", file=sys.stderr)
     elif out["match"] is None:
-        res["metric"] = METRIC.replace("; bit-exact", "") + " (parity unchecked)"
+        res["metric"] = metric.replace("; bit-exact", "") + " (parity unchecked)"
         out["note"] = "no oracle fixture for this round / host count: parity unchecked in this run"
     return out["match"] is not False
 
@@ -327,7 +377,7 @@ def main():
         res = run_single(args)
     if res is None:
         return
-    ok = parity_check(res, args.hosts)
+    ok = parity_check(res, args)
     print(json.dumps(res), flush=True)
     if not ok:
         sys.exit(3)

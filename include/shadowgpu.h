@@ -362,6 +362,12 @@ int sg_engine_event_moves(sg_engine* e, uint64_t* emitted, uint64_t* gathered, u
  * turns the guess off, SG_GSPEC=2 guesses a wrong bucket (the check must
  * reject it); both exist for tests. */
 int sg_engine_gather_paths(sg_engine* e, uint64_t* guessed, uint64_t* listed);
+/* Test only: between the next round's k_proc and k_scatter, corrupt two of
+ * partition 0's staged records (one names a host past the shard, one lies
+ * beyond the calendar's horizon).  k_scatter's insert role must clamp both in
+ * bounds and set SG overflow flag 128 (an internal inconsistency); the run
+ * then stops with SG_ERR_OVERFLOW.  Round-mode engines only. */
+int sg_engine_debug_inject(sg_engine* e);
 int sg_engine_trace(sg_engine* e, sg_trace_rec* out, uint64_t capacity, uint64_t* n_out);
 /* Executed windows {start, end} per round (recorded when trace_capacity > 0). */
 int sg_engine_windows(sg_engine* e, uint64_t* out_pairs, uint64_t capacity, uint64_t* n_out);
@@ -449,7 +455,8 @@ enum sg_kernel_class {
     SG_K_INSERT = 1,   /* k_scatter: events into their buckets, the next window planned
                           and gathered (sharded: received events due in it routed) */
     SG_K_PLAN = 2,     /* unused: planning is a k_scatter role now (class kept for ABI stability) */
-    SG_K_GATHER = 3,   /* unused: the gather is a k_scatter role now (class kept for ABI stability) */
+    SG_K_GATHER = 3,   /* k_spec: the split step's insert, stash refill and guessed gather,
+                        * on a second stream beside the all-to-all (several shards) */
     SG_K_EXCHANGE = 4, /* the step's RCCL all-to-all (sg_engine_run_steps): this shard's
                           wait for the slowest shard plus the transfer — the barrier
                           idle time of scheduler.c:380-389 */
@@ -538,6 +545,23 @@ int sg_policy_next_time(sg_policy* p, uint64_t thread_token, sg_simtime* next_ou
 /* Events still queued (for unref at free, host_single.c:104). */
 int sg_policy_remaining(sg_policy* p, uint64_t* handles_out, uint64_t capacity, uint64_t* n_out);
 
+/* Per-kernel profile of the policy's device half: every launch
+ * carries its dispatch packet's start / stop timestamps (no extra packets),
+ * and each kernel class accumulates its launches, time and algorithmic bytes
+ * (the record bytes its job needs to read and write, counted from the insert
+ * and extraction sizes).  skip_rounds: the first extractions (rounds) are not
+ * counted (a bench's warmup).  Kernel classes, in order: k_cins1 k_cneed
+ * k_calloc k_cins2 k_cmin k_xplan k_hist k_mscan k_part k_local k_xrank k_xlong. */
+typedef struct sg_kernel_stat {
+    char name[16];
+    uint64_t launches;
+    double ms;          /* summed kernel time */
+    double alg_bytes;   /* summed algorithmic bytes */
+} sg_kernel_stat;
+int sg_policy_kernel_profile(sg_policy* p, int enable, uint32_t skip_rounds);
+/* Up to `cap` classes into out; *n_out = the number of classes. */
+int sg_policy_kernel_stats(sg_policy* p, sg_kernel_stat* out, uint32_t cap, uint32_t* n_out);
+
 /* ------------------------------------------------------------------------ */
 /* 4. Shadow-style round driver for running a policy outside Shadow          */
 /* ------------------------------------------------------------------------ */
@@ -590,6 +614,8 @@ typedef struct sg_sched_result {
 int sg_policy_ops_gpu(uint32_t n_threads, uint32_t max_hosts, int device, sg_sched_policy_ops* out);
 /* First error the gpu vtable's callbacks hit (their signatures return void). */
 int sg_policy_ops_gpu_error(const sg_sched_policy_ops* ops);
+/* The sg_policy behind a vtable made by sg_policy_ops_gpu (NULL otherwise). */
+sg_policy* sg_policy_ops_gpu_policy(const sg_sched_policy_ops* ops);
 
 /* Run the PHOLD workload with n_workers threads (>= 1) under `ops` (not freed).
  * max_rounds bounds the run; per-host digests / pops / rng / event counters

@@ -16,6 +16,10 @@
  *
  * Used (a) to cross-check the gpu policy under real worker threads and
  * (b) as bench.py's timed CPU baseline ("port" of host_steal, all cores).
+ * Built twice (oracle/Makefile): liborc.so with plain binary heaps of event
+ * pointers (a lower bound on the reference's cost), and libhsglib.so with
+ * -DHS_GLIB_PQ, whose per-host queue is priority_queue.c's heap with its
+ * GLib hash-table position map (the reference's cost).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -24,12 +28,32 @@
 
 #include "../include/shadowgpu.h"
 
+#ifndef HS_GLIB_PQ
 typedef struct hq {            /* HostStealQueueData */
     pthread_mutex_t lock;
     sg_hevent** a;
     uint32_t n, cap;
     sg_simtime last;
 } hq;
+#else
+/* The faithful heap (bench.py's cpu_baseline "faithful" variant, built as
+ * libhsglib.so): priority_queue.c:17-175 restated with GLib itself.  The heap
+ * holds element pointers and a GHashTable maps every element to its heap slot;
+ * each swap re-inserts both elements (priority_queue.c:78-85), a push looks
+ * the element up first (:126), a pop removes it (:165) and the array starts at
+ * 100 slots, doubles when full and halves below a quarter, refreshing the
+ * whole map when realloc moves it (:115-124, :166-173).  The compare runs
+ * through a function pointer, as GCompareDataFunc does. */
+#include <glib.h>
+typedef struct hq {
+    pthread_mutex_t lock;
+    gpointer* heap;
+    GHashTable* map;
+    gsize n, cap;
+    GCompareDataFunc cmp;
+    sg_simtime last;
+} hq;
+#endif
 
 typedef struct dq {            /* GQueue of host indices */
     uint32_t* a;
@@ -61,6 +85,13 @@ static int ev_less(const sg_hevent* a, const sg_hevent* b) { /* event.c:110-153 
     if (a->src != b->src) return a->src < b->src;
     return a->seq < b->seq;
 }
+
+#ifndef HS_GLIB_PQ
+static void hq_init(hq* q) { pthread_mutex_init(&q->lock, NULL); }
+static uint32_t hq_len(const hq* q) { return q->n; }
+static sg_hevent* hq_top(const hq* q) { return q->a[0]; }
+static sg_hevent* hq_at(const hq* q, uint32_t i) { return q->a[i]; }
+static void hq_free(hq* q) { free(q->a); }
 
 static void hq_push(hq* q, sg_hevent* e) {
     if (q->n == q->cap) {
@@ -95,6 +126,79 @@ static sg_hevent* hq_pop(hq* q) {
     }
     return top;
 }
+#else
+enum { PQ_FIRST = 100 };  /* priority_queue.c:15 */
+static gint ev_cmp(gconstpointer a, gconstpointer b, gpointer unused) {  /* event_compare as a GCompareDataFunc */
+    (void)unused;
+    return ev_less((const sg_hevent*)a, (const sg_hevent*)b) ? -1 : ev_less((const sg_hevent*)b, (const sg_hevent*)a);
+}
+static void hq_init(hq* q) {
+    pthread_mutex_init(&q->lock, NULL);
+    q->heap = g_new(gpointer, PQ_FIRST);
+    q->map = g_hash_table_new(NULL, NULL);
+    q->cap = PQ_FIRST;
+    q->n = 0;
+    q->cmp = ev_cmp;
+}
+static uint32_t hq_len(const hq* q) { return (uint32_t)q->n; }
+static sg_hevent* hq_top(const hq* q) { return (sg_hevent*)q->heap[0]; }
+static sg_hevent* hq_at(const hq* q, uint32_t i) { return (sg_hevent*)q->heap[i]; }
+static void hq_free(hq* q) {
+    g_hash_table_destroy(q->map);
+    g_free(q->heap);
+}
+static void pq_remap(hq* q) {  /* every element's slot again after the array moved */
+    g_hash_table_remove_all(q->map);
+    for (gsize i = 0; i < q->n; i++) g_hash_table_insert(q->map, q->heap[i], q->heap + i);
+}
+static void pq_swap(hq* q, gsize i, gsize j) {
+    gpointer x = q->heap[i], y = q->heap[j];
+    q->heap[i] = y;
+    q->heap[j] = x;
+    g_hash_table_insert(q->map, x, q->heap + j);
+    g_hash_table_insert(q->map, y, q->heap + i);
+}
+static int pq_below(hq* q, gsize i, gsize j) { return q->cmp(q->heap[i], q->heap[j], NULL) < 0; }
+static gsize pq_up(hq* q, gsize i) {
+    for (; i > 0 && pq_below(q, i, (i - 1) / 2); i = (i - 1) / 2) pq_swap(q, i, (i - 1) / 2);
+    return i;
+}
+static gsize pq_down(hq* q, gsize i) {
+    for (gsize c; (c = 2 * i + 1) < q->n; i = c) {
+        if (c + 1 < q->n && pq_below(q, c + 1, c)) c++;
+        if (!pq_below(q, c, i)) break;
+        pq_swap(q, i, c);
+    }
+    return i;
+}
+static void pq_resize(hq* q, gsize cap) {
+    gpointer* old = q->heap;
+    q->cap = cap;
+    q->heap = g_renew(gpointer, q->heap, q->cap);
+    if (q->heap != old) pq_remap(q);
+}
+static void hq_push(hq* q, sg_hevent* e) {
+    if (q->n >= q->cap) pq_resize(q, 2 * q->cap);
+    gpointer* at = (gpointer*)g_hash_table_lookup(q->map, e);
+    if (at) {  /* already queued: only re-placed (never the case for fresh events) */
+        pq_up(q, pq_down(q, (gsize)(at - q->heap)));
+        return;
+    }
+    q->heap[q->n] = e;
+    g_hash_table_insert(q->map, e, q->heap + q->n);
+    q->n++;
+    pq_up(q, q->n - 1);
+}
+static sg_hevent* hq_pop(hq* q) {
+    gpointer top = q->heap[0];
+    pq_swap(q, 0, q->n - 1);
+    g_hash_table_remove(q->map, top);
+    q->n--;
+    pq_down(q, 0);
+    if (q->cap > PQ_FIRST && q->n * 4 < q->cap) pq_resize(q, q->cap / 2);
+    return (sg_hevent*)top;
+}
+#endif
 
 static void dq_init(dq* d, uint32_t cap) {
     d->a = (uint32_t*)malloc((cap ? cap : 1) * 4);
@@ -173,8 +277,8 @@ static sg_hevent* pop_from(pol* p, td* t, dq* assigned, sg_simtime barrier) {
         hq* q = &p->q[h];
         pthread_mutex_lock(&q->lock);
         sg_hevent* e = NULL;
-        if (q->n && q->a[0]->time < barrier) {
-            q->last = q->a[0]->time;
+        if (hq_len(q) && hq_top(q)->time < barrier) {
+            q->last = hq_top(q)->time;
             e = hq_pop(q);
             /* migrate iff the host was stolen (host_steal.c:172-196, 303): the
              * owner is read under the reader lock, written only on a change */
@@ -244,7 +348,7 @@ static sg_simtime p_next(void* data) {
         for (uint32_t i = 0; i < lists[l]->n; i++) {
             hq* q = &p->q[lists[l]->a[(lists[l]->head + i) % lists[l]->cap]];
             pthread_mutex_lock(&q->lock);
-            if (q->n && q->a[0]->time < m) m = q->a[0]->time;
+            if (hq_len(q) && hq_top(q)->time < m) m = hq_top(q)->time;
             pthread_mutex_unlock(&q->lock);
         }
     return m;
@@ -253,8 +357,8 @@ static sg_simtime p_next(void* data) {
 static void p_free(void* data) {
     pol* p = (pol*)data;
     for (uint32_t h = 0; h < p->nh; h++) {
-        for (uint32_t i = 0; i < p->q[h].n; i++) free(p->q[h].a[i]);
-        free(p->q[h].a);
+        for (uint32_t i = 0; i < hq_len(&p->q[h]); i++) free(hq_at(&p->q[h], i));
+        hq_free(&p->q[h]);
         pthread_mutex_destroy(&p->q[h].lock);
     }
     for (uint32_t i = 0; i < p->nt; i++) {
@@ -279,7 +383,7 @@ int orc_policy_ops_cpu(int steal, uint32_t n_threads, uint32_t n_hosts, sg_sched
     p->maxt = n_threads;
     p->t = (td*)calloc(n_threads, sizeof(td));
     if (!p->q || !p->owner || !p->t) return -1;
-    for (uint32_t h = 0; h < n_hosts; h++) pthread_mutex_init(&p->q[h].lock, NULL);
+    for (uint32_t h = 0; h < n_hosts; h++) hq_init(&p->q[h]);
     pthread_rwlock_init(&p->lock, NULL);
     out->data = p;
     out->add_host = p_add_host;

@@ -282,14 +282,39 @@ def digest_mix(pos, time, src, seq) -> int:
 
 
 # --------------------------------------------------- CPU policies (baseline) --
-def cpu_policy_ops(steal: bool, n_threads: int, n_hosts: int):
+_hsglib = None
+HSGLIB_PATH = os.path.join(_HERE, "libhsglib.so")
+
+
+def faithful_available() -> bool:
+    """libhsglib.so (host_steal.c with priority_queue.c's GLib heap) is built."""
+    if not os.path.exists(HSGLIB_PATH):
+        try:
+            build()
+        except Exception:  # noqa: BLE001 — no GLib on this machine
+            return False
+    return os.path.exists(HSGLIB_PATH)
+
+
+def cpu_policy_ops(steal: bool, n_threads: int, n_hosts: int, faithful: bool = False):
     """host_steal / host_single restatements (oracle/host_steal.c) as a
-    shadow_amd.policy.PolicyOps vtable, for the Shadow-style round driver."""
+    shadow_amd.policy.PolicyOps vtable, for the Shadow-style round driver.
+    faithful: the per-host queue is priority_queue.c's heap with its GLib
+    hash-table position map (libhsglib.so); otherwise plain binary heaps."""
+    global _hsglib
     from shadow_amd.policy import PolicyOps
-    L = lib()
+    if faithful:
+        if not faithful_available():
+            raise RuntimeError("oracle/libhsglib.so is not built (GLib headers absent)")
+        if _hsglib is None:
+            _hsglib = C.CDLL(HSGLIB_PATH)
+        L = _hsglib
+    else:
+        L = lib()
     L.orc_policy_ops_cpu.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(PolicyOps)]
     ops = PolicyOps()
     if L.orc_policy_ops_cpu(int(steal), n_threads, n_hosts, C.byref(ops)) != 0:
         raise RuntimeError("orc_policy_ops_cpu failed")
     ops._owner = "cpu"
+    ops._lib = L  # keeps the library that holds the vtable loaded
     return ops

@@ -97,14 +97,15 @@ EXPORTS = [
     "sg_topology_lognormal", "sg_graphml_load", "sg_graph_free", "sg_graph_info", "sg_graph_vertex",
     "sg_graph_edge", "sg_graph_attach", "sg_graph_paths", "sg_build_path_tables", "sg_engine_create", "sg_engine_destroy", "sg_engine_boot",
     "sg_engine_run", "sg_engine_enqueue_round", "sg_engine_sync", "sg_engine_stats",
-    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_event_moves", "sg_engine_gather_paths", "sg_engine_trace", "sg_engine_windows",
+    "sg_engine_host_state", "sg_engine_host_range", "sg_engine_active_hosts", "sg_engine_event_moves", "sg_engine_gather_paths", "sg_engine_debug_inject", "sg_engine_trace", "sg_engine_windows",
     "sg_engine_stream", "sg_engine_exchange_rows", "sg_engine_set_exchange_cap",
     "sg_engine_exchange_peak", "sg_engine_step_send", "sg_engine_step_recv",
     "sg_engine_enqueue_rounds", "sg_comm_unique_id", "sg_comm_create", "sg_comm_destroy",
     "sg_engine_run_steps", "sg_engine_set_graph", "sg_engine_graph_prepare", "sg_engine_kernel_times",
     "sg_engine_set_timing", "sg_engine_set_timing_mask", "sg_comm_available", "sg_engine_path_counters", "sg_engine_path_counts", "sg_engine_barrier_timers", "sg_engine_barrier_times", "sg_engine_geometry", "sg_engine_stamps", "sg_policy_create", "sg_policy_destroy", "sg_policy_add_host",
     "sg_policy_thread_hosts", "sg_policy_push", "sg_policy_pop", "sg_policy_next_time",
-    "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_sched_run_phold",
+    "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_policy_ops_gpu_policy",
+    "sg_policy_kernel_profile", "sg_policy_kernel_stats", "sg_sched_run_phold",
     "sg_sched_run_phold_paths", "sg_path_cache_create", "sg_path_cache_destroy", "sg_path_cache_lookup",
     "sg_path_cache_stats",
 ]
@@ -150,6 +151,7 @@ def lib():
     L.sg_engine_active_hosts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.sg_engine_event_moves.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 3
     L.sg_engine_gather_paths.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 2
+    L.sg_engine_debug_inject.argtypes = [C.c_void_p]
     L.sg_engine_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.sg_engine_stream.argtypes = [C.c_void_p]

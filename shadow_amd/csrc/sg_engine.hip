@@ -264,6 +264,12 @@ struct RoundState {
     uint64_t xacc[2];    // emitted min, discovery min of k_proc's workgroups (atomics)
     uint64_t recv_ok;    // a several-shard k_scatter read the receive buffer: the next k_proc stages it
     uint64_t tail_r, bS_r;  // fl_tail % NCH, bS % R, kept with them (the planner's 64-bit divisions)
+    // split step (several shards): k_spec runs beside the
+    // all-to-all and gathers the guessed bucket; k_post keeps it on a hit
+    uint64_t psel;        // the current window's partition counts are in pcnt (0) or pcnt2 (1)
+    uint64_t spec_fold;   // the fold k_spec gathered the guessed bucket for, else UINT64_MAX
+    uint64_t spec_nfree;  // chunks of that bucket k_spec put into the ring behind the planned tail
+    uint64_t spec_b;      // that bucket (absolute)
 };
 
 // The gather's due list, guessed one kernel ahead.  In steady state a window
@@ -344,6 +350,8 @@ struct Dev {
     GSpec* gspec;             // the next gather's guessed due list (k_proc -> k_scatter)
     uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
+    uint32_t split;           // several shards: the split step (k_spec beside the all-to-all, k_post after)
+    uint32_t* pcnt2;          // [P] the window's partition counts when k_post discarded k_spec's gather
     uint32_t* pcnt;           // [P] due events of the partition this round
     Rec* part;                // [P][CAPP]
     Rec* part2;               // [P][CAPP] sorted by host
@@ -748,6 +756,7 @@ __global__ void k_boot(Dev d) {
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
     if (i < d.P) {
         d.pcnt[i] = 0;
+        d.pcnt2[i] = 0;
         d.rcnt[i] = 0;
         if (d.remn) d.remn[i] = 0;
         for (int c = 0; c < NCTR; ++c) d.pcum[(size_t)c * d.P + i] = 0;
@@ -790,6 +799,10 @@ __global__ void k_boot(Dev d) {
         rs->ticket = 0;
         rs->xacc[0] = UINT64_MAX;
         rs->xacc[1] = UINT64_MAX;
+        rs->psel = 0;  // the boot k_scatter gathers into pcnt
+        rs->spec_fold = UINT64_MAX;
+        rs->spec_nfree = 0;
+        rs->spec_b = UINT64_MAX;
         rs->recv_ok = 0;
     }
     if (i < d.G && d.outn) {
@@ -880,6 +893,7 @@ struct StepView {
     Window w;
     uint32_t cur, listed, ins_local, round_done, more, done, quit;
     uint32_t tail_r, bSr;    // tail % NCH, bS % R (64-bit divisions done once, by the planner)
+    uint32_t hit;            // split step: the new window is the bucket k_spec gathered
 };
 constexpr uint32_t SEGMAX = (NBMAX + 2) * XS;  // segments, at most
 // Segment j is bucket sub-list x = j % XS of the list's k-th bucket, k = j / XS:
@@ -908,7 +922,7 @@ struct DueList {
 };
 template <int GT>
 __device__ uint32_t due_segments(const Dev& d, const StepView& sv, DueList& dl, uint32_t* s_start, uint32_t* s_lo,
-                                 uint64_t* s16, uint64_t* nfree_out) {
+                                 uint64_t* s16, uint64_t* nfree_out, bool all_written) {
     dl.bS = sv.bS;
     dl.bL = sv.bL;
     dl.pret = sv.pret;
@@ -929,7 +943,9 @@ __device__ uint32_t due_segments(const Dev& d, const StepView& sv, DueList& dl, 
         bool events;
         dl.seg(j, b, x, flags, events);
         const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
-        const uint32_t hi = d.bk[row], lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
+        // all_written (split step): k_spec wrote every reserved slot before this
+        // launch, and routed nothing, so the written count is the reserved one
+        const uint32_t hi = d.bk[row], lo = events ? (all_written ? hi : d.bw[(size_t)cur * XS * dl.R + row]) : 0u;
         const uint32_t n = ((flags ? lo : hi) + CH - 1) >> CH_SHIFT;
         s_lo[j] = lo;
         s_start[j] = n;  // the count for now
@@ -994,9 +1010,15 @@ __device__ __forceinline__ void gspec_load(const Dev& d, uint32_t w, uint32_t nw
                              (b & ((1ull << 48) - 1)) * d.W};
     }
 }
+// gmode: GM_PLAN (k_scatter: the guessed list when the plan confirms it, else
+// the list path), GM_SPEC (k_spec, before the plan: the guessed bucket as the
+// window sv describes, nothing otherwise; its ring count goes to spec_nfree),
+// GM_FALLBACK (k_post after a miss: the list path over every written slot).
+// pc: the partition counters the events are appended to.
+enum GMode { GM_PLAN = 0, GM_SPEC = 1, GM_FALLBACK = 2 };
 template <int GT>
 __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32_t nw, unsigned char* lds,
-                            const uint64_t* s_gsw, uint64_t* st) {
+                            const uint64_t* s_gsw, uint64_t* st, int gmode, uint32_t* pc) {
     constexpr int GR = 4 * (int)CH / GT;
     static_assert(GR * GT == (int)(GSPEC_N * CH), "the one-pass path holds GSPEC_N chunks");
     uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
@@ -1020,7 +1042,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
         for (uint32_t p = threadIdx.x; p < P; p += GT) {
             const uint32_t c = s_cnt[p];
             if (c) {
-                const uint32_t base = atomicAdd(&d.pcnt[p], c);
+                const uint32_t base = atomicAdd(&pc[p], c);
                 if (base + c > d.CAPP) flag(d, OV_PART);
                 s_cnt[p] = base;
             }
@@ -1090,16 +1112,20 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     const uint64_t gb = s_gsw[1] & ((1ull << 48) - 1);
     const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
     const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
-    if (XS == 1 && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb && sv.ret == UINT64_MAX && !spent &&
-        gnid <= GSPEC_N * nw) {  // uniform
+    if (gmode != GM_FALLBACK && XS == 1 && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb &&
+        sv.ret == UINT64_MAX && !spent && gnid <= GSPEC_N * nw) {  // uniform
         const uint32_t row = (uint32_t)(s_gsw[1] >> 48);
         const uint32_t hi = d.bk[row];  // in flight under the pool loads
         if (st) st[1] = __builtin_amdgcn_s_memrealtime();
         one_pass(GSPEC_N, [&]() __attribute__((always_inline)) {
             const uint32_t nd = (hi + CH - 1) >> CH_SHIFT;
             if (w == 0 && threadIdx.x == 0) {
-                d.rs->nfree2[sv.cur ^ 1] = nd;
-                atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
+                if (gmode == GM_SPEC) {  // k_post keeps it on a hit (publish_step)
+                    d.rs->spec_nfree = nd;
+                } else {
+                    d.rs->nfree2[sv.cur ^ 1] = nd;
+                    atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
+                }
             }
             if (st) {
                 st[5] = nd;
@@ -1108,14 +1134,19 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             for (uint32_t i = w + threadIdx.x * nw; i < nd; i += GT * nw) {
                 const uint32_t id = threadIdx.x < GSPEC_N && i < gnid ? s_de[threadIdx.x].id
                                                                      : d.btab[(size_t)row * d.NCH + i];
+                // as the list path's free_chunk: an id past the pool (a slot
+                // whose reservation found the pool exhausted, OV_POOL) never
+                // enters the ring
+                if (id >= d.NCH) continue;
                 const uint32_t pos = tail_r + i;  // i < NCH: one wrap at most
                 d.fring[pos >= d.NCH ? pos - d.NCH : pos] = id;
             }
         });
     } else {
+    if (gmode == GM_SPEC) return;  // uniform: no guess to gather (k_post takes the list path)
     DueList dl;
     uint64_t nfree;
-    const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree);  // barriers inside
+    const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree, gmode == GM_FALLBACK);
     if (w == 0 && threadIdx.x == 0) {
         d.rs->nfree2[sv.cur ^ 1] = nfree;
         atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GLIST * d.P], 1ull);
@@ -1628,7 +1659,8 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
 
 // mode 0: one shard, after k_proc; 1: several shards, after the all-to-all
 // (hdr: the G blocks' HDR_W header words, LDS); 2: boot (the first window is
-// listed already).  One thread, from the LDS copy of the round state
+// listed already); 3: several shards, split step (k_post: as 1, and whether
+// the new window is the bucket k_spec gathered).  One thread, from the LDS copy of the round state
 // (load_round_state), so no load of it waits for another.
 constexpr uint32_t HDR_W = HDR * RW;  // header words per exchange block
 constexpr uint32_t RSW = sizeof(RoundState) / 8;
@@ -1671,7 +1703,7 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
         m = sv.rmin0 < m ? sv.rmin0 : m;
         m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
         j = jmin0 < jm ? jmin0 : jm;
-    } else if (mode == 1) {
+    } else if (mode == 1 || mode == 3) {
         uint64_t more = 0;
         for (uint32_t p = 0; p < d.G; ++p) {
             const int64_t* blk = hdr + (size_t)p * HDR_W;
@@ -1689,6 +1721,7 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.ovf = ovf;
     sv.tail_r = (uint32_t)rs->tail_r;
     sv.bSr = (uint32_t)rs->bS_r;
+    sv.hit = 0;
     if (mode == 2 || sv.more) return;
     sv.round_done = 1;
     const Window w = next_window(d, m, j, mj0, nmj0);
@@ -1721,6 +1754,11 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
         } else {
             sv.bSr = (uint32_t)(sv.bS % d.R);
         }
+        // split step: k_spec gathered bucket spec_b as the window [spec_b * W,
+        // (spec_b + 1) * W); a hit (the plan's window is exactly that) keeps it
+        const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
+        sv.hit = mode == 3 && rs->spec_fold == sv.fold && rs->spec_b == sv.bS && sv.bL == sv.bS &&
+                 sv.ret == UINT64_MAX && !spent && sv.S == sv.bS * W;
     }
 }
 
@@ -1734,7 +1772,7 @@ __device__ __forceinline__ void load_round_state(const Dev& d, int mode, const i
     const uint64_t v = reinterpret_cast<const uint64_t*>(d.rs)[lane < RSW ? lane : 0u];
     constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
     int64_t h[HPL];
-    if (mode == 1) {  // uniform
+    if (mode == 1 || mode == 3) {  // uniform
         const uint32_t nh = d.G * HDR_W;
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q) {
@@ -1758,7 +1796,7 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     if (sv.ovf) atomicOr((unsigned long long*)&rs->overflow, (unsigned long long)sv.ovf);
     rs->fold = sv.fold + 1;
     rs->splan = 0;
-    if (mode == 1) {
+    if (mode == 1 || mode == 3) {
         rs->recv_ok = 1;  // the next k_proc stages what this launch did not route
         if (d.check) {
             // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in
@@ -1807,6 +1845,13 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     const Window& w = sv.w;
     rs->phase = 0;
     rs->jmin = sv.j;
+    if (mode == 3) {  // split step: k_spec's gather kept (its counts in pcnt), or k_post's in pcnt2
+        rs->psel = sv.hit ? 0 : 1;
+        if (sv.hit) {
+            rs->nfree2[cur ^ 1] = rs->spec_nfree;
+            atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
+        }
+    }
     if (d.wlog && sv.rounds0 < d.wlog_cap) {  // the window just executed
         d.wlog[2 * sv.rounds0] = sv.S0;
         d.wlog[2 * sv.rounds0 + 1] = sv.E0;
@@ -2135,7 +2180,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     Rec rr[EPTF];
 #pragma unroll
     for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
-    const uint32_t n_raw = d.pcnt[p];
+    // the window's count: pcnt, or pcnt2 when a split step's k_post discarded
+    // k_spec's gather (rs->psel, known once the round state arrives)
+    const uint32_t n_a = d.pcnt[p], n_b = d.pcnt2[p];
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
     const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
     uint32_t v_first = 0, v_last = 0;  // ROWS: the partition's first and last slots' vertices
@@ -2148,8 +2195,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // a use of those loads on the paths that do not need them keeps the
     // compiler from sinking them below the branches (and so behind the wait)
     auto pin = [&]() __attribute__((always_inline)) {
-        asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_raw), "v"(stash_id), "v"(stash_n), "v"(v_first),
-                     "v"(v_last));
+        asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_a), "v"(n_b), "v"(stash_id), "v"(stash_n),
+                     "v"(v_first), "v"(v_last));
     };
     if (rsf(RSF(done))) {
         pin();
@@ -2223,6 +2270,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint32_t n_raw = rsf(RSF(psel)) ? n_b : n_a;
     const uint32_t n = n_raw < d.CAPP ? n_raw : d.CAPP;
     // flat pass: a host's digest terms of its events but the last, summed in
     // LDS over s_vh / s_sb (phase A's arrays, free until phase A runs)
@@ -2399,7 +2447,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
     }
-    if (tid == 0) d.pcnt[p] = 0;  // consumed; the next k_scatter's gather refills it
+    if (tid == 0) {  // consumed; the next k_scatter's (or k_spec's / k_post's) gather refills them
+        d.pcnt[p] = 0;
+        d.pcnt2[p] = 0;
+    }
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
 #pragma unroll
@@ -3129,7 +3180,10 @@ struct Route {
 // One batch of up to SU events per thread (every thread of the workgroup
 // calls it): slot from the (partition, bucket) reservation cursor, chunk
 // from the reserving row's allocation; due events routed.  Returns nothing; carry min
-// and tombstones accumulate in smin / ntomb.
+// and tombstones accumulate in smin / ntomb.  KEEP (k_spec, the window only
+// guessed): every event is written to its slot, a due one is also copied to
+// its partition, so k_post can discard the copies and gather the slots.
+template <bool KEEP>
 __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t x, uint32_t* s_cur, uint32_t* s_pc,
                                              uint32_t* s_pk, const bool (&v)[SU], const uint64_t (&t)[SU],
                                              const uint64_t (&k)[SU], const uint32_t (&dl)[SU], uint64_t& smin,
@@ -3158,7 +3212,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         pos[q] = v[q] ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
         due[q] = v[q] && ro.listed && t[q] < ro.E;
         const bool in_ret = ro.listed && b == ro.ret;
-        write[q] = v[q] && (!due[q] || in_ret);  // fully due buckets: the slot stays empty
+        write[q] = v[q] && (KEEP || !due[q] || in_ret);  // fully due buckets: the slot stays empty
         if (v[q] && !due[q] && in_ret) smin = t[q] < smin ? t[q] : smin;
         if (due[q]) atomicAdd(&s_pc[part_of(d, dl[q])], 1u);
     }
@@ -3173,8 +3227,8 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
     for (int q = 0; q < SU; ++q) {
         // no chunk only when the pool ran out (reserve_buckets flagged it)
         if (!write[q] || (pos[q] >> CH_SHIFT) >= d.NCH || id[q] >= d.NCH) continue;
-        Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
-        ntomb += due[q];
+        Rec r{due[q] && !KEEP ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
+        ntomb += due[q] && !KEEP;
         st_rec(d.pool, (((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))) * 16, r.a, r.k);
     }
     if (!ro.listed) return;  // launch-uniform
@@ -3221,8 +3275,100 @@ __device__ __forceinline__ void insert_finish(const Dev& d, const Route& ro, uin
     }
 }
 
+// Refill role (one workgroup, every thread): bk copied into bw[nx] (every slot
+// reserved so far is written once this launch's inserts are, so the next
+// step's gather may read them all), then every reserving row's stash back to
+// ST chunk ids from the free ring, usable up to avail.
+__device__ __forceinline__ void refill_role(const Dev& d, uint32_t nx, uint64_t avail, unsigned char* lds,
+                                            uint64_t* st) {
+    RoundState* rs = d.rs;
+    const uint32_t R = d.R, tid = threadIdx.x;
+    // fold: every slot reserved so far is written by this launch, so the
+    // next step's gather may read them all
+    {
+        // (nx: the other half of bw, read by the next step)
+        constexpr uint32_t CPT = XS * RMAX / K3_T;
+        uint32_t cv[CPT];  // every load in flight at once
+#pragma unroll
+        for (uint32_t q = 0; q < CPT; ++q) {
+            const uint32_t i = tid + q * K3_T;
+            cv[q] = d.bk[i < XS * R ? i : 0u];
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < CPT; ++q)
+            if (tid + q * K3_T < XS * R) d.bw[(size_t)nx * XS * R + tid + q * K3_T] = cv[q];
+    }
+    // stash refill: every reserving row back to ST chunk ids, one ring
+    // reservation for all of them; the ring is usable up to the tail the
+    // plan set (this launch's gather frees more behind it).  The ids are
+    // copied as one flat list of (row, slot) entries, every load of a
+    // batch in flight together.
+    constexpr uint32_t RPT = (PMAX + G3MAX + K3_T - 1) / K3_T;
+    constexpr int FU = 8;
+    uint64_t* s16 = (uint64_t*)lds;
+    uint64_t* s_hh = s16 + 16;
+    uint32_t* s_have = (uint32_t*)(s_hh + 1);  // [PMAX + G3MAX]
+    uint32_t* s_roff = s_have + PMAX + G3MAX;  // [PMAX + G3MAX] first list entry of each row
+    const uint32_t rows = d.P, NCH = d.NCH;  // the reserving rows: k_proc's partitions
+    
+    uint32_t have[RPT];
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; ++q) {
+        const uint32_t r = tid + q * K3_T;
+        have[q] = r < rows ? d.stn[r] : ST;
+        mine += ST - have[q];
+    }
+    uint64_t total;
+    uint32_t off = (uint32_t)block_excl_scan(mine, s16, &total);  // barriers inside
+    if (total == 0) return;  // uniform
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; ++q) {
+        const uint32_t r = tid + q * K3_T;
+        if (r < rows) {
+            s_have[r] = have[q];
+            s_roff[r] = off;
+        }
+        off += ST - have[q];
+    }
+    if (tid == 0) *s_hh = atomicAdd((unsigned long long*)&rs->fl_head, (unsigned long long)total);
+    __syncthreads();
+    const uint64_t h = *s_hh;
+    const uint32_t hr = (uint32_t)(h % NCH);
+    if (h + total > avail && tid == 0) flag(d, OV_POOL);
+    for (uint32_t f0 = 0; f0 < rows * ST; f0 += K3_T * FU) {
+        uint32_t id[FU], dst[FU];
+        bool v[FU];
+#pragma unroll
+        for (int u = 0; u < FU; ++u) {
+            const uint32_t f = f0 + tid + u * K3_T, r = f / ST < rows ? f / ST : 0u, k = f % ST;
+            const uint32_t e = s_roff[r] + (k - s_have[r]);  // list entry (when k >= have)
+            v[u] = f < rows * ST && k >= s_have[r] && h + e < avail;
+            const uint32_t pos = hr + (v[u] ? e : 0u);  // e < total <= NCH: one wrap at most
+            id[u] = d.fring[pos >= NCH ? pos - NCH : pos];  // unconditional (clamped)
+            dst[u] = r * ST + k;
+        }
+#pragma unroll
+        for (int u = 0; u < FU; ++u)
+            if (v[u]) d.stash[dst[u]] = id[u];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; ++q) {
+        const uint32_t r = tid + q * K3_T;
+        if (r >= rows || have[q] == ST) continue;
+        const uint64_t e0 = h + s_roff[r];  // the row's first entry's ring position
+        const uint64_t got = e0 >= avail ? 0 : std::min<uint64_t>(avail - e0, ST - have[q]);
+        d.stn[r] = have[q] + (uint32_t)got;
+    }
+    if (st) st[3] = __builtin_amdgcn_s_memrealtime();
+}
+
 // mode: 0 one shard (after k_proc), 1 several shards (after the all-to-all; recv the
-// exchange blocks), 2 boot.  Every workgroup plans the step (step_view) from
+// exchange blocks), 2 boot, 3 several shards, split step (k_post: k_spec
+// inserted the staged events, refilled the stashes and gathered the guessed
+// bucket beside the all-to-all; no insert or refill workgroups are launched,
+// and the gather workgroups take the list path only when the plan misses the
+// guess).  Every workgroup plans the step (step_view) from
 // the state as the previous kernels left it, then arrives on a counter once its
 // reads of that state have returned; the last to arrive publishes the plan
 // (publish_step).  Nothing waits for anything: no workgroup depends on another
@@ -3236,12 +3382,14 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     __shared__ uint64_t s_gsw[3];                // gather: the GSpec header
     __shared__ uint32_t s_routed;
     __shared__ uint64_t s_rbase[MAXG];           // receive role: the received blocks' time bases
-    const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = gridDim.x - 2;  // gather workgroups [g0, gx)
-    // role order [insert P][receive G3][gather][refill][rmin]; SG_GFIRST
+    // role order [insert P][receive G3][gather][refill][rmin] over nv virtual
+    // workgroups; a split launch (mode 3) starts at the receive role.  SG_GFIRST
     // dispatches the gather workgroups (the launch's long pole) first
-    const uint32_t blk = SG_GFIRST ? (blockIdx.x < gx - g0 ? g0 + blockIdx.x
-                                      : blockIdx.x < gx ? blockIdx.x - (gx - g0) : blockIdx.x)
-                                   : blockIdx.x;
+    const bool split = mode == 3;
+    const uint32_t off = split ? d.P : 0u, nv = gridDim.x + off;
+    const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = nv - 2;  // gather workgroups [g0, gx)
+    const uint32_t ng = gx - g0, bi = blockIdx.x;
+    const uint32_t blk = SG_GFIRST ? (bi < ng ? g0 + bi : bi + off < gx ? off + (bi - ng) : bi + off) : bi + off;
     const uint32_t R = d.R, tid = threadIdx.x;
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
@@ -3307,11 +3455,11 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     uint64_t* st = d.stamps && tid == 0 ? d.stamps + (size_t)(d.P + 1 + blk) * SG_STAMP_W : nullptr;
     if (st) {
         st[0] = __builtin_amdgcn_s_memrealtime();
-        st[4] = blk == gridDim.x - 1 ? 3 : blk == gridDim.x - 2 ? 4 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
+        st[4] = blk == nv - 1 ? 3 : blk == nv - 2 ? 4 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
         st[1] = st[2] = st[3] = st[6] = st[0];
         st[5] = 0;
     }
-    if (blk == gridDim.x - 1) {
+    if (blk == nv - 1) {
         uint64_t* s16 = (uint64_t*)lds;
         if (d.wtime && sv.round_done) {
             // barrier wait (scheduler.c:380-389): each partition idles from its
@@ -3358,89 +3506,18 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         }
         break;
     }
-    if (blk == gridDim.x - 2) {
-        // fold: every slot reserved so far is written by this launch, so the
-        // next step's gather may read them all
-        {
-            const uint32_t nx = sv.cur ^ 1;
-            constexpr uint32_t CPT = XS * RMAX / K3_T;
-            uint32_t cv[CPT];  // every load in flight at once
-#pragma unroll
-            for (uint32_t q = 0; q < CPT; ++q) {
-                const uint32_t i = tid + q * K3_T;
-                cv[q] = d.bk[i < XS * R ? i : 0u];
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < CPT; ++q)
-                if (tid + q * K3_T < XS * R) d.bw[(size_t)nx * XS * R + tid + q * K3_T] = cv[q];
-        }
-        // stash refill: every reserving row back to ST chunk ids, one ring
-        // reservation for all of them; the ring is usable up to the tail the
-        // plan set (this launch's gather frees more behind it).  The ids are
-        // copied as one flat list of (row, slot) entries, every load of a
-        // batch in flight together.
-        constexpr uint32_t RPT = (PMAX + G3MAX + K3_T - 1) / K3_T;
-        constexpr int FU = 8;
-        uint64_t* s16 = (uint64_t*)lds;
-        uint64_t* s_hh = s16 + 16;
-        uint32_t* s_have = (uint32_t*)(s_hh + 1);  // [PMAX + G3MAX]
-        uint32_t* s_roff = s_have + PMAX + G3MAX;  // [PMAX + G3MAX] first list entry of each row
-        const uint32_t rows = d.P, NCH = d.NCH;  // the reserving rows: k_proc's partitions
-        const uint64_t avail = sv.tail;
-        uint32_t have[RPT];
-        uint32_t mine = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < RPT; ++q) {
-            const uint32_t r = tid + q * K3_T;
-            have[q] = r < rows ? d.stn[r] : ST;
-            mine += ST - have[q];
-        }
-        uint64_t total;
-        uint32_t off = (uint32_t)block_excl_scan(mine, s16, &total);  // barriers inside
-        if (total == 0) break;  // uniform
-#pragma unroll
-        for (uint32_t q = 0; q < RPT; ++q) {
-            const uint32_t r = tid + q * K3_T;
-            if (r < rows) {
-                s_have[r] = have[q];
-                s_roff[r] = off;
-            }
-            off += ST - have[q];
-        }
-        if (tid == 0) *s_hh = atomicAdd((unsigned long long*)&rs->fl_head, (unsigned long long)total);
-        __syncthreads();
-        const uint64_t h = *s_hh;
-        const uint32_t hr = (uint32_t)(h % NCH);
-        if (h + total > avail && tid == 0) flag(d, OV_POOL);
-        for (uint32_t f0 = 0; f0 < rows * ST; f0 += K3_T * FU) {
-            uint32_t id[FU], dst[FU];
-            bool v[FU];
-#pragma unroll
-            for (int u = 0; u < FU; ++u) {
-                const uint32_t f = f0 + tid + u * K3_T, r = f / ST < rows ? f / ST : 0u, k = f % ST;
-                const uint32_t e = s_roff[r] + (k - s_have[r]);  // list entry (when k >= have)
-                v[u] = f < rows * ST && k >= s_have[r] && h + e < avail;
-                const uint32_t pos = hr + (v[u] ? e : 0u);  // e < total <= NCH: one wrap at most
-                id[u] = d.fring[pos >= NCH ? pos - NCH : pos];  // unconditional (clamped)
-                dst[u] = r * ST + k;
-            }
-#pragma unroll
-            for (int u = 0; u < FU; ++u)
-                if (v[u]) d.stash[dst[u]] = id[u];
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < RPT; ++q) {
-            const uint32_t r = tid + q * K3_T;
-            if (r >= rows || have[q] == ST) continue;
-            const uint64_t e0 = h + s_roff[r];  // the row's first entry's ring position
-            const uint64_t got = e0 >= avail ? 0 : std::min<uint64_t>(avail - e0, ST - have[q]);
-            d.stn[r] = have[q] + (uint32_t)got;
-        }
-        if (st) st[3] = __builtin_amdgcn_s_memrealtime();
+    if (blk == nv - 2) {
+        // the plan's tail: this launch's gather frees more behind it.  A split
+        // launch's k_spec did this already
+        if (!split) refill_role(d, sv.cur ^ 1, sv.tail, lds, st);
         break;
     }
     if (blk >= g0) {
-        if (ro.listed) gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, s_gsw, st);
+        // split step: a hit keeps k_spec's gather; a miss gathers every written
+        // slot of the window into pcnt2 (k_spec's copies in pcnt are dropped)
+        if (ro.listed && !(split && sv.hit))
+            gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, s_gsw, st, split ? GM_FALLBACK : GM_PLAN,
+                              split ? d.pcnt2 : d.pcnt);
         if (st) st[3] = wait_stamp();
         break;
     }
@@ -3493,7 +3570,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
                     dl[q] = 0;
                 }
             }
-            insert_batch(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+            insert_batch<false>(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
         if (st) st[2] = wait_stamp();
         insert_finish(d, ro, smin, ntomb, s16);
@@ -3505,6 +3582,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // per (workgroup, partition)); the next k_proc stages the rest
     // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
+    uint32_t* pc = split && !sv.hit ? d.pcnt2 : d.pcnt;  // where this window's counts are
     if (tid == 0) s_routed = 0;
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         s_pc[p] = 0;
@@ -3523,7 +3601,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         const uint32_t c = s_pc[p];
         if (c) {
-            const uint32_t base = atomicAdd(&d.pcnt[p], c);
+            const uint32_t base = atomicAdd(&pc[p], c);
             if (base + c > d.CAPP) flag(d, OV_PART);
             s_pc[p] = base;
             atomicAdd(&s_routed, c);
@@ -3543,6 +3621,144 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
     if (tid == 0 && ticket == gridDim.x - 1) publish_step(d, mode, sv, recv);
+}
+
+// ----------------------------------------------------------------- spec ----
+// Split step (several shards), launched on a second stream
+// after k_proc, beside the all-to-all: everything of k_scatter that does not
+// need the exchange's MIN.  Roles, in launch order:
+//   [0, G1)       the bucket the next window most likely is (GSpec: the
+//                 window after the executed one, one whole bucket) gathered
+//                 into the host partitions (pcnt) as that window, its chunks
+//                 into the ring behind the tail the plan will set;
+//   [G1, G1 + P)  partition p's staged events into their reserved slots, every
+//                 one of them (KEEP), those due in the guessed window also
+//                 copied into their host partitions;
+//   last          bk into the next step's bw half, the stashes refilled (the
+//                 ring usable up to the tail as it is: the last gather's
+//                 chunks join it only when the plan moves it).
+// Nothing here writes what the plan reads.  k_post plans the window from the
+// headers and keeps this launch's partitions when the window is the guessed
+// one (rs->spec_fold / spec_b, StepView::hit); otherwise it gathers every
+// written slot of the window into pcnt2, and these copies are never read.
+__global__ __launch_bounds__(K3_T) void k_spec(Dev d) {
+    __shared__ __align__(16) unsigned char lds[SCAT_LDS];
+    __shared__ StepView sv;              // the guessed window, as a plan would put it
+    __shared__ uint64_t s_rsw[RSW];      // the round state as k_proc left it
+    __shared__ uint64_t s_gsw[3];        // the GSpec header
+    const uint32_t G1 = d.G1, P = d.P, bi = blockIdx.x, tid = threadIdx.x, R = d.R;
+    const int role = bi < G1 ? 2 : bi < G1 + P ? 0 : 4;
+    const uint32_t blk = bi < G1 ? bi : bi - G1;
+    if (tid < 64) load_round_state(d, 0, nullptr, s_rsw, nullptr);
+    if ((tid >> 6) == 1) {
+        if (role == 2) gspec_load(d, blk, G1, s_gsw, (DueEnt*)(lds + GDE_OFF));
+        else if (tid - 64 < 3) s_gsw[tid - 64] = reinterpret_cast<const uint64_t*>(d.gspec)[tid - 64];
+    }
+    Rec pre[SU];
+    uint32_t pre_n = 0;
+    if (role == 0) {  // the partition's count, first SU events per thread, reservation bases
+        pre_n = d.rcnt[blk];
+        const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
+#pragma unroll
+        for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[tid + q * K3_T]);
+        uint32_t* s_cur = (uint32_t*)lds;
+        uint32_t* s_pc = s_cur + RMAX;
+        const uint32_t* wb = d.wbase + (size_t)blk * R;
+        constexpr uint32_t WPT = RMAX / K3_T;
+        uint32_t wv[WPT];
+#pragma unroll
+        for (uint32_t q = 0; q < WPT; ++q) {
+            const uint32_t rb = tid + q * K3_T;
+            wv[q] = wb[rb < R ? rb : 0u];
+        }
+        for (uint32_t p = tid; p < P; p += K3_T) s_pc[p] = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < WPT; ++q)
+            if (tid + q * K3_T < R) s_cur[tid + q * K3_T] = wv[q];
+    }
+    lds_barrier();  // the round state, the guess's header (and ids) and the bases are in LDS
+    const RoundState* r = reinterpret_cast<const RoundState*>(s_rsw);
+    if (r->done) return;  // uniform
+    const uint64_t W = d.W, fold = r->fold, gb = s_gsw[1] & ((1ull << 48) - 1);
+    // the jump the plan takes if no shard lowers the discovery minimum (next_window)
+    uint64_t J = d.fixed_jump;
+    if (d.window_rule != SG_WINDOW_FIXED) {
+        J = r->jmin != UINT64_MAX ? r->jmin * SG_ONE_MS : r->next_min_jump;
+        J = J > 0 ? J : 10 * SG_ONE_MS;
+        if (d.runahead_min > 0 && J < d.runahead_min) J = d.runahead_min;
+    }
+    const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
+    const bool guess = XS == 1 && s_gsw[0] == fold && r->phase == 0 && J == W && gnid <= GSPEC_N * G1;
+    if (tid == 0) {
+        const uint32_t cur = (uint32_t)(fold & 1);
+        sv.S = gb * W;
+        sv.E = (gb + 1) * W;
+        sv.bS = sv.bL = gb;
+        sv.ret = sv.pret = UINT64_MAX;
+        sv.fold = fold;
+        sv.cur = cur;
+        uint32_t tr = (uint32_t)r->tail_r + (uint32_t)r->nfree2[cur];  // the plan's tail (nfree <= NCH)
+        sv.tail_r = tr >= d.NCH ? tr - d.NCH : tr;
+        if (bi == 0) {
+            d.rs->spec_fold = guess ? fold : UINT64_MAX;
+            d.rs->spec_b = gb;
+        }
+    }
+    lds_barrier();
+    if (role == 2) {
+        if (guess) gather_role<K3_T>(d, sv, blk, G1, lds, s_gsw, nullptr, GM_SPEC, d.pcnt);
+        return;
+    }
+    if (role == 4) {
+        refill_role(d, (uint32_t)(fold & 1) ^ 1u, r->fl_tail, lds, nullptr);
+        return;
+    }
+    // insert role
+    const uint32_t n = pre_n;
+    if (!r->ins_local || n == 0) return;  // uniform
+    Route ro;
+    ro.listed = guess;
+    ro.cur = sv.cur;
+    ro.S = sv.S;
+    ro.E = sv.E;
+    ro.ret = UINT64_MAX;
+    ro.bS = r->bS;  // the executed window's first bucket: every staged event is at or after it
+    ro.bSW = ro.bS * W;
+    ro.bSr = (uint32_t)r->bS_r;
+    uint32_t* s_cur = (uint32_t*)lds;
+    uint32_t* s_pc = s_cur + RMAX;
+    uint32_t* s_pk = s_pc + PMAX;
+    const Rec* src = d.loc + (size_t)blk * d.ECAP;
+    const uint64_t S0 = r->ins_S;
+    uint64_t smin = UINT64_MAX, ntomb = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
+        Rec rr[SU];
+        if (i0 == 0) {  // uniform
+#pragma unroll
+            for (int q = 0; q < SU; ++q) rr[q] = pre[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SU; ++q) {
+                const uint32_t i = i0 + tid + q * K3_T;
+                rr[q] = ld_stream(&src[i < n ? i : 0]);
+            }
+        }
+        bool v[SU];
+        uint64_t t[SU], k[SU];
+        uint32_t dl[SU];
+#pragma unroll
+        for (int q = 0; q < SU; ++q) {
+            v[q] = i0 + tid + q * K3_T < n;
+            t[q] = S0 + (rr[q].a & M40);
+            k[q] = rr[q].k;
+            dl[q] = (uint32_t)(rr[q].a >> 40);
+            if (v[q] && dl[q] >= d.L) {  // a staged record is always a local host: clamped, flagged
+                flag(d, OV_BUG);
+                dl[q] = 0;
+            }
+        }
+        insert_batch<true>(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+    }
 }
 
 // ----------------------------------------------------------------- plan ----
@@ -3592,14 +3808,29 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
         for (uint32_t x = 0; x < XS; ++x) pend += d.bk[(size_t)x * d.R + rb];
         pend -= d.btomb[rb];
     }
-    if (listed)
-        for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += d.pcnt[p];
+    if (listed) {
+        const uint32_t* pc = rs->psel ? d.pcnt2 : d.pcnt;
+        for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += pc[p];
+    }
     for (int i = 0; i < NCTR; ++i) {
         const uint64_t t = block_sum(c[i], s16);
         if (threadIdx.x == 0) d.rs->ctr[i] = t;
     }
     pend = block_sum(pend, s16);
     if (threadIdx.x == 0) *pending = pend;
+}
+
+// Test only (sg_engine_debug_inject): corrupts two of partition 0's staged
+// records between a k_proc and its k_scatter, as a corrupt calendar or a
+// staging bug would (profiles/r04/ablation/README.md: the round-4 fault): one
+// names a host past the shard, one lies beyond the calendar's horizon.  The
+// insert role must clamp both in bounds and flag OV_BUG.  One thread.
+__global__ void k_inject(Dev d) {
+    const uint32_t n = d.rcnt[0];
+    if (n < 2) return;
+    Rec* r = d.loc;
+    r[0].a = (r[0].a & M40) | ((uint64_t)(d.L + 7) << 40);         // an impossible host
+    r[1].a = (r[1].a & ~M40) | ((uint64_t)2 * d.R * d.W & M40);   // beyond R buckets of the window
 }
 
 }  // namespace
@@ -3614,6 +3845,10 @@ struct sg_engine {
     int device;
     hipStream_t stream;
     bool own_stream;
+    // split step (d.split): k_spec runs on aux beside the all-to-all, ordered
+    // by ev_proc (after k_proc) and ev_spec (before k_post)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_proc = nullptr, ev_spec = nullptr;
     bool booted;
     std::vector<void*> allocs;
     uint32_t* pcount_buf = nullptr;  // path packet counters, once enabled
@@ -3631,6 +3866,7 @@ struct sg_engine {
     // hipGraph replay of batches of rounds / steps (sg_engine_set_graph)
     uint32_t graph_batch = 0;
     uint64_t gen = 0;  // bumped whenever a kernel argument captured in a graph changes
+    bool inject = false;  // sg_engine_debug_inject: corrupt the next round's staged records
     hipGraphExec_t gexec = nullptr;
     hipEvent_t batch_ev[2] = {nullptr, nullptr};  // sg_engine_enqueue_rounds' queue bound
     const int64_t* last_recv = nullptr;  // the last step_recv's buffer (read by the next k_proc)
@@ -3690,7 +3926,7 @@ static hipEvent_t get_event(sg_engine* e) {
 // around the kernel, so the measured duration is the kernel's.  The RCCL
 // exchange records them on the stream around the collective.
 template <typename F>
-static int timed_launch(sg_engine* e, int cls, F&& launch) {
+static int timed_launch(sg_engine* e, int cls, F&& launch, hipStream_t on = nullptr) {
     hipEvent_t a = nullptr, b = nullptr;
     const bool timed = e->timing && (e->timing_mask >> cls & 1u);
     if (timed) {
@@ -3701,7 +3937,7 @@ static int timed_launch(sg_engine* e, int cls, F&& launch) {
     launch(a, b);
     HIPCHK(hipGetLastError());
     if (e->debug_sync) {
-        const hipError_t err = hipStreamSynchronize(e->stream);
+        const hipError_t err = hipStreamSynchronize(on ? on : e->stream);
         if (err != hipSuccess) {
             static const char* names[SG_KCLASSES] = {"process", "insert", "plan", "gather", "exchange"};
             sg_set_error("kernel class %s (launch %llu) failed: %s", names[cls],
@@ -3872,6 +4108,9 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         return SG_ERR_INVAL;
     }
     d.G1 = env_u32("SG_GATHER_GRID", 128);
+    // the split step for the step API (several shards, or one with exchange_cap
+    // set): SG_SPLIT=0 keeps the whole k_scatter after the all-to-all (A/B)
+    d.split = (G > 1 || p.exchange_cap) && env_u32z("SG_SPLIT", 1) != 0 ? 1u : 0u;
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
@@ -3882,8 +4121,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // eight or four shards of configs[3]) every kernel is at its latency
     // floor, and fewer workgroups cut the contention on the shared bucket and
     // partition counters: world-1 steps 44.8-45.7 -> 39.5-40.2 us at 125k,
-    // 48.9-49.1 -> 44.8-46.2 us at 250k; 500k keeps 1968 (3907 was slower)
-    // (profiles/r04/hp125k)
+    // 48.9-49.1 -> 44.8-46.2 us at 250k (profiles/r04/hp125k).  The floor
+    // applies from 64k hosts up, so 500k gets 2048 as well (245 partitions;
+    // 3907 was slower there).  It was measured on the world-1 step path; a
+    // single-shard round of 64k-500k hosts runs with it unmeasured.
     const uint32_t hp_env = env_u32("SG_HP", 0);
     uint32_t hp_auto = ((d.L + 255) / 256 + 15) / 16 * 16;
     if (d.L > 65536 && hp_auto < 2048) hp_auto = 2048;
@@ -4099,6 +4340,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.gspec, 1);
     ALLOC(D.pcnt, P);
+    ALLOC(D.pcnt2, P);
     ALLOC(D.part, P * D.CAPP);
     ALLOC(D.part2, P * D.CAPP);
     ALLOC(D.extras, P * K2_T * XCAP);
@@ -4134,6 +4376,13 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
             return SG_ERR_HIP;
         }
         e->own_stream = true;
+    }
+    if (D.split && (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&e->ev_proc, hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&e->ev_spec, hipEventDisableTiming) != hipSuccess)) {
+        sg_engine_destroy(e);
+        sg_set_error("sg_engine_create: the split step's stream / events could not be created");
+        return SG_ERR_HIP;
     }
     if (hipHostMalloc((void**)&e->h_rs, sizeof(RoundState), hipHostMallocDefault) != hipSuccess) {
         e->h_rs = nullptr;
@@ -4224,6 +4473,12 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->recv_hold) (void)hipFree(e->recv_hold);
     for (hipEvent_t ev : e->batch_ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (e->aux) {
+        (void)hipStreamSynchronize(e->aux);
+        (void)hipStreamDestroy(e->aux);
+    }
+    if (e->ev_proc) (void)hipEventDestroy(e->ev_proc);
+    if (e->ev_spec) (void)hipEventDestroy(e->ev_spec);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return SG_OK;
@@ -4300,13 +4555,35 @@ static int enqueue_process(sg_engine* e) {
 }
 
 // k_scatter: the staged events into the calendar, the next window planned and
-// gathered; several shards (recv): the received events due in it routed.
+// gathered; several shards (recv): the received events due in it routed.  The
+// split step's k_post (after k_spec on the aux stream): the plan, the receive
+// role, the gather only when the guess missed, rmin.
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
+    if (recv && d.split) {
+        HIPCHK(hipStreamWaitEvent(e->stream, e->ev_spec, 0));
+        return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
+            SG_LAUNCH(k_scatter, dim3(d.G3 + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv, 3);
+        });
+    }
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
         SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv,
                   recv ? 1 : 0);
     });
+}
+
+// Split step: k_spec on the aux stream once k_proc is done, beside the
+// all-to-all the caller enqueues next on the engine stream.
+static int enqueue_spec(sg_engine* e) {
+    const Dev& d = e->d;
+    HIPCHK(hipEventRecord(e->ev_proc, e->stream));
+    HIPCHK(hipStreamWaitEvent(e->aux, e->ev_proc, 0));
+    int rc = timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {
+        SG_LAUNCH(k_spec, dim3(d.G1 + d.P + 1), dim3(K3_T), 0, e->aux, a, b, d);
+    }, e->aux);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev_spec, e->aux));
+    return SG_OK;
 }
 
 int sg_engine_enqueue_round(sg_engine* e) {
@@ -4320,7 +4597,25 @@ int sg_engine_enqueue_round(sg_engine* e) {
     }
     int rc;
     if ((rc = enqueue_process(e))) return rc;
+    if (e->inject) {  // test only
+        e->inject = false;
+        hipLaunchKernelGGL(k_inject, dim3(1), dim3(1), 0, e->stream, e->d);
+        HIPCHK(hipGetLastError());
+    }
     return enqueue_insert_plan(e, nullptr);
+}
+
+int sg_engine_debug_inject(sg_engine* e) {
+    if (!e || !e->booted) {
+        sg_set_error("sg_engine_debug_inject: engine not booted");
+        return SG_ERR_STATE;
+    }
+    if (e->d.G != 1 || e->d.outn) {
+        sg_set_error("sg_engine_debug_inject: round-mode engines only");
+        return SG_ERR_STATE;
+    }
+    e->inject = true;
+    return SG_OK;
 }
 
 // Enqueues n iterations of body (one round or one step each) on the engine
@@ -4373,7 +4668,9 @@ int sg_engine_graph_prepare(sg_engine* e) {
         return SG_ERR_STATE;
     }
     const uint32_t n = e->graph_batch;
-    if (!n) return SG_OK;  // graphs off: nothing to capture
+    // graphs off, or a setting under which enqueue_batch launches eagerly
+    // (timing, SG_DEBUG_SYNC): nothing to capture, and nothing may run here
+    if (!n || e->timing || e->debug_sync) return SG_OK;
     const sg_engine::GraphKey key{e->gen, nullptr, nullptr, nullptr, nullptr, n};
     return enqueue_batch(e, key, n, [&] { return sg_engine_enqueue_round(e); }, false);
 }
@@ -4404,6 +4701,7 @@ int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds) {
 
 int sg_engine_sync(sg_engine* e) {
     if (!e) return SG_ERR_INVAL;
+    if (e->aux) HIPCHK(hipStreamSynchronize(e->aux));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (e->timing) harvest_timing(e);
     return SG_OK;
@@ -4617,6 +4915,7 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
     rc = enqueue_process(e);
     e->d.xsend = nullptr;
     e->d.xrecv = nullptr;
+    if (rc == SG_OK && e->d.split) rc = enqueue_spec(e);
     return rc;
 }
 

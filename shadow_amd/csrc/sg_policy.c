@@ -48,8 +48,11 @@ static int sheap_push(sheap* h, const sgp_rec* r) {
         h->a = na;
         h->cap = nc;
     }
-    uint32_t i = h->n++;
+    uint32_t i = h->n;
     h->a[i] = *r;
+    /* the owner's pop reads n without the lock (sg_policy_pop): an atomic
+     * store keeps that read well-defined whoever pushes */
+    __atomic_store_n(&h->n, i + 1, __ATOMIC_RELEASE);
     while (i) {
         uint32_t p = (i - 1) / 2;
         if (!rec_less(&h->a[i], &h->a[p])) break;
@@ -62,7 +65,9 @@ static int sheap_push(sheap* h, const sgp_rec* r) {
 }
 
 static void sheap_pop(sheap* h) {
-    h->a[0] = h->a[--h->n];
+    const uint32_t n = h->n - 1;
+    __atomic_store_n(&h->n, n, __ATOMIC_RELEASE);
+    h->a[0] = h->a[n];
     uint32_t i = 0;
     for (;;) {
         uint32_t c = 2 * i + 1;
@@ -232,6 +237,30 @@ int sg_policy_create(const sg_policy_params* prm, sg_policy** out) {
     const char* pp = getenv("SG_POLICY_PINNED");
     p->pinned = pp && *pp == '1';
     *out = p;
+    return SG_OK;
+}
+
+int sg_policy_kernel_profile(sg_policy* p, int enable, uint32_t skip_rounds) {
+    if (!p || !p->dev) return SG_ERR_INVAL;
+    return sgp_dev_kprof(p->dev, enable, skip_rounds) ? SG_ERR_HIP : SG_OK;
+}
+
+int sg_policy_kernel_stats(sg_policy* p, sg_kernel_stat* out, uint32_t cap, uint32_t* n_out) {
+    if (!p || !p->dev || (cap && !out)) return SG_ERR_INVAL;
+    enum { MAXK = 32 };
+    const char* names[MAXK];
+    uint64_t n[MAXK];
+    double ms[MAXK], by[MAXK];
+    uint32_t k = 0;
+    if (sgp_dev_kstats(p->dev, names, n, ms, by, MAXK, &k)) return SG_ERR_HIP;
+    for (uint32_t i = 0; i < k && i < cap; i++) {
+        memset(&out[i], 0, sizeof out[i]);
+        snprintf(out[i].name, sizeof out[i].name, "%s", names[i]);
+        out[i].launches = n[i];
+        out[i].ms = ms[i];
+        out[i].alg_bytes = by[i];
+    }
+    if (n_out) *n_out = k;
     return SG_OK;
 }
 
@@ -507,7 +536,7 @@ static int flush(sg_policy* p) {
         host_rt* h = &p->hosts[p->self_list[k]];
         memcpy(ex + n, h->selfq.a, h->selfq.n * sizeof(sgp_rec));
         n += h->selfq.n;
-        h->selfq.n = 0;
+        __atomic_store_n(&h->selfq.n, 0, __ATOMIC_RELEASE);
         h->in_self_list = 0;
     }
     p->n_self = 0;

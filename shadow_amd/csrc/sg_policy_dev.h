@@ -38,6 +38,11 @@ int sgp_dev_min(sgp_dev* d, uint64_t* min_out);
  * entries). */
 int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const uint32_t** off,
                     uint64_t* total);
+/* Per-kernel profile (include/shadowgpu.h sg_policy_kernel_profile). */
+int sgp_dev_kprof(sgp_dev* d, int enable, uint32_t skip_rounds);
+/* kernel classes: names[i] (static strings), launches, ms, algorithmic bytes */
+int sgp_dev_kstats(sgp_dev* d, const char** names, uint64_t* launches, double* ms, double* bytes, uint32_t cap,
+                   uint32_t* n_out);
 /* Copy out every queued record (teardown). */
 int sgp_dev_all(sgp_dev* d, sgp_rec* out, uint64_t capacity, uint64_t* n_out);
 

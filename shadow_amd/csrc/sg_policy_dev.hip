@@ -32,10 +32,12 @@
 //                      freed, the straddling bucket's and far list's minima set)
 //   MIN      k_cmin    over the RB bucket minima and the far minimum
 //                      (host_single.c:273-305)
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "sg_policy_dev.h"
 
@@ -693,9 +695,24 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 
 }  // namespace
 
+// Kernel classes of the per-kernel profile (sg_policy_kernel_profile).
+enum KCls { KC_CINS1, KC_CNEED, KC_CALLOC, KC_CINS2, KC_CMIN, KC_XPLAN, KC_HIST, KC_MSCAN, KC_PART, KC_LOCAL,
+            KC_XRANK, KC_XLONG, KC_N };
+const char* const KC_NAMES[KC_N] = {"k_cins1", "k_cneed", "k_calloc", "k_cins2", "k_cmin", "k_xplan",
+                                    "k_hist", "k_mscan", "k_part", "k_local", "k_xrank", "k_xlong"};
+
 struct sgp_dev {
     int device;
     hipStream_t s;
+    // per-kernel profile: dispatch-packet timestamps of every launch
+    // (hipExtLaunchKernelGGL), harvested at the next synchronisation
+    bool kprof = false;
+    uint32_t kskip = 0;  // extractions still to skip
+    double kms[KC_N] = {}, kbytes[KC_N] = {};
+    uint64_t kn[KC_N] = {};
+    struct KEv { hipEvent_t a, b; int cls; };
+    std::vector<KEv> kpend;
+    std::vector<hipEvent_t> kfree;
     Cal c;
     Scal* h_sc;          // pinned mirror of the device scalars
     uint64_t cur;        // lowest bucket that may hold a live event
@@ -845,9 +862,50 @@ static int grow_out(sgp_dev* d, uint64_t n) {
     return 0;
 }
 
+static hipEvent_t kev(sgp_dev* d) {
+    if (!d->kfree.empty()) {
+        hipEvent_t e = d->kfree.back();
+        d->kfree.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+static bool counting(const sgp_dev* d) { return d->kprof && d->kskip == 0; }
+// One launch of class cls on the policy's stream; profiled, it carries its
+// dispatch packet's own timestamps and adds `bytes` to the class.
+template <typename K, typename... A>
+static void klaunch(sgp_dev* d, int cls, double bytes, K kernel, dim3 g, dim3 b, A... args) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (counting(d)) {
+        e0 = kev(d);
+        e1 = kev(d);
+    }
+    if (e0 && e1) {
+        hipExtLaunchKernelGGL(kernel, g, b, 0, d->s, e0, e1, 0, args...);
+        d->kpend.push_back({e0, e1, cls});
+    } else {
+        hipLaunchKernelGGL(kernel, g, b, 0, d->s, args...);
+    }
+    if (counting(d)) {
+        d->kn[cls]++;
+        d->kbytes[cls] += bytes;
+    }
+}
+static void kharvest(sgp_dev* d) {  // after a stream synchronisation
+    for (auto& e : d->kpend) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) d->kms[e.cls] += ms;
+        d->kfree.push_back(e.a);
+        d->kfree.push_back(e.b);
+    }
+    d->kpend.clear();
+}
+
 static int read_scal(sgp_dev* d) {
     PCHK(hipMemcpyAsync(d->h_sc, d->c.sc, sizeof(Scal), hipMemcpyDeviceToHost, d->s));
     PCHK(hipStreamSynchronize(d->s));
+    kharvest(d);
     return 0;
 }
 
@@ -937,6 +995,11 @@ int sgp_dev_destroy(sgp_dev* d) {
     if (d->h_runs) (void)hipHostFree(d->h_runs);
     if (d->h_off) (void)hipHostFree(d->h_off);
     if (d->h_sc) (void)hipHostFree(d->h_sc);
+    for (auto& e : d->kpend) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    for (hipEvent_t e : d->kfree) (void)hipEventDestroy(e);
     if (d->s) (void)hipStreamDestroy(d->s);
     delete d;
     return 0;
@@ -984,13 +1047,19 @@ int sgp_dev_insert_segs(sgp_dev* d, const sgp_rec* const* segs, const uint64_t* 
     }
     const uint32_t grid = (uint32_t)((n + IPW - 1) / IPW);
     PCHK(hipMemsetAsync(&d->c.sc->need, 0, 4, d->s));
-    hipLaunchKernelGGL(k_cins1, dim3(grid), dim3(BLOCK), 0, d->s, d->c, d->cur, d->d_in, n, d->d_rslot);
-    hipLaunchKernelGGL(k_cneed, dim3(RB / BLOCK), dim3(BLOCK), 0, d->s, d->c);
+    // algorithmic bytes: k_cins1 reads each time and writes its
+    // slot (12 B); k_cneed / k_calloc read a bucket's counts (8 B) and
+    // k_calloc moves each new chunk id (8 B); k_cins2 reads the slot, the
+    // record and its chunk id and writes the record (72 B)
+    klaunch(d, KC_CINS1, 12.0 * n, k_cins1, dim3(grid), dim3(BLOCK), d->c, d->cur, (const sgp_rec*)d->d_in, n,
+            d->d_rslot);
+    klaunch(d, KC_CNEED, 8.0 * RB, k_cneed, dim3(RB / BLOCK), dim3(BLOCK), d->c);
     PCHK(hipGetLastError());
     if ((rc = read_scal(d))) return rc;
     if (h->need > h->ftop && (rc = grow_pool(d, d->nchunks + (h->need - h->ftop)))) return rc;
-    hipLaunchKernelGGL(k_calloc, dim3(RB / BLOCK), dim3(BLOCK), 0, d->s, d->c);
-    hipLaunchKernelGGL(k_cins2, dim3(grid), dim3(BLOCK), 0, d->s, d->c, d->d_in, n, d->d_rslot);
+    klaunch(d, KC_CALLOC, 8.0 * RB + 8.0 * h->need, k_calloc, dim3(RB / BLOCK), dim3(BLOCK), d->c);
+    klaunch(d, KC_CINS2, 72.0 * n, k_cins2, dim3(grid), dim3(BLOCK), d->c, (const sgp_rec*)d->d_in, n,
+            (const uint32_t*)d->d_rslot);
     PCHK(hipGetLastError());
     h->ftop -= h->need;
     d->queued += n;
@@ -999,7 +1068,7 @@ int sgp_dev_insert_segs(sgp_dev* d, const sgp_rec* const* segs, const uint64_t* 
 
 int sgp_dev_min(sgp_dev* d, uint64_t* min_out) {
     PCHK(hipSetDevice(d->device));
-    hipLaunchKernelGGL(k_cmin, dim3(RB / 1024), dim3(1024), 0, d->s, d->c);
+    klaunch(d, KC_CMIN, 8.0 * RB, k_cmin, dim3(RB / 1024), dim3(1024), d->c);  // each bucket's minimum
     PCHK(hipGetLastError());
     int rc = read_scal(d);
     if (rc) return rc;
@@ -1021,26 +1090,74 @@ int sgp_dev_extract(sgp_dev* d, uint64_t barrier, const sgp_rec** runs, const ui
         const uint64_t last = (barrier - 1) >> d->c.shift;
         if (last >= d->cur) nbk = last - d->cur + 1 < RB ? (uint32_t)(last - d->cur + 1) : RB;
     }
-    hipLaunchKernelGGL(k_xplan, dim3(1), dim3(1024), 0, d->s, d->c, d->cur, nbk, barrier, 0);
-    hipLaunchKernelGGL(k_hist, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat);
-    hipLaunchKernelGGL(k_mscan, dim3(1), dim3(1024), 0, d->s, d->d_mat, P2, d->c, d->d_pbase);
-    hipLaunchKernelGGL(k_part, dim3(XU), dim3(1024), 0, d->s, d->c, barrier, P2, d->d_mat, d->d_tmp);
-    hipLaunchKernelGGL(k_local, dim3(P2), dim3(1024), 0, d->s, d->c, d->cur, nbk, n, P2, d->d_pbase, d->d_tmp,
-                       d->d_tmp2, d->d_off);
+    // sizes known only at the end (items, extracted records): the bytes of
+    // these launches are added below
+    const bool cnt = counting(d);
+    klaunch(d, KC_XPLAN, 0, k_xplan, dim3(1), dim3(1024), d->c, d->cur, nbk, barrier, 0);
+    klaunch(d, KC_HIST, 0, k_hist, dim3(XU), dim3(1024), d->c, barrier, P2, d->d_mat);
+    klaunch(d, KC_MSCAN, 0, k_mscan, dim3(1), dim3(1024), d->d_mat, P2, (const Cal)d->c, d->d_pbase);
+    klaunch(d, KC_PART, 0, k_part, dim3(XU), dim3(1024), d->c, barrier, P2, (const uint32_t*)d->d_mat, d->d_tmp);
+    klaunch(d, KC_LOCAL, 0, k_local, dim3(P2), dim3(1024), d->c, d->cur, nbk, n, P2, (const uint32_t*)d->d_pbase,
+            (const sgp_rec*)d->d_tmp, d->d_tmp2, d->d_off);
     PCHK(hipMemsetAsync(&d->c.sc->nlong, 0, 4, d->s));
-    hipLaunchKernelGGL(k_xrank, dim3(XG), dim3(BLOCK), 0, d->s, d->d_tmp2, d->d_off, &d->c.sc->total, d->d_out,
-                       d->c.sc, d->d_long);
-    hipLaunchKernelGGL(k_xlong, dim3(XL_G), dim3(XL_T), 0, d->s, d->d_tmp2, d->d_off, d->c.sc, d->d_long, d->d_out);
+    klaunch(d, KC_XRANK, 0, k_xrank, dim3(XG), dim3(BLOCK), (const sgp_rec*)d->d_tmp2, (const uint32_t*)d->d_off,
+            (const unsigned long long*)&d->c.sc->total, d->d_out, d->c.sc, d->d_long);
+    klaunch(d, KC_XLONG, 0, k_xlong, dim3(XL_G), dim3(XL_T), (const sgp_rec*)d->d_tmp2, (const uint32_t*)d->d_off,
+            (const Scal*)d->c.sc, (const uint32_t*)d->d_long, d->d_out);
     PCHK(hipGetLastError());
     PCHK(hipMemcpyAsync(d->h_off, d->d_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, d->s));
     if ((rc = read_scal(d))) return rc;
     const uint64_t t = d->h_sc->total;
+    if (cnt) {
+        // algorithmic bytes, t extracted records of 32 B:
+        // k_xplan reads the due buckets' counts and writes a 16-B item with
+        // its chunk id per due chunk; the level-1 sort reads each due time and
+        // host (12 B) and writes / scans / reads the count matrix (4 B per
+        // entry), k_part moves each record (64 B); k_local reads each host,
+        // moves each record (68 B) and writes off[] (4 B per host); k_xrank
+        // reads each record and its run bounds and writes it (72 B); k_xlong
+        // (incast runs only) is not counted
+        const double nu = (double)((d->h_sc->nitems + UI - 1) / UI), mat = 4.0 * nu * P2;
+        d->kbytes[KC_XPLAN] += 8.0 * nbk + 20.0 * d->h_sc->nitems;
+        d->kbytes[KC_HIST] += 12.0 * t + mat;
+        d->kbytes[KC_MSCAN] += 2.0 * mat;
+        d->kbytes[KC_PART] += 64.0 * t + mat;
+        d->kbytes[KC_LOCAL] += 68.0 * t + 4.0 * n;
+        d->kbytes[KC_XRANK] += 72.0 * t;
+    }
+    if (d->kskip) --d->kskip;
     if (t) PCHK(hipMemcpy(d->h_runs, d->d_out, t * sizeof(sgp_rec), hipMemcpyDeviceToHost));
     if (barrier > 0 && (barrier >> d->c.shift) > d->cur) d->cur = barrier >> d->c.shift;
     d->queued -= t;
     *runs = d->h_runs;
     *off = d->h_off;
     *total = t;
+    return 0;
+}
+
+int sgp_dev_kprof(sgp_dev* d, int enable, uint32_t skip_rounds) {
+    PCHK(hipStreamSynchronize(d->s));
+    kharvest(d);
+    d->kprof = enable != 0;
+    d->kskip = skip_rounds;
+    for (int i = 0; i < KC_N; ++i) {
+        d->kms[i] = d->kbytes[i] = 0;
+        d->kn[i] = 0;
+    }
+    return 0;
+}
+
+int sgp_dev_kstats(sgp_dev* d, const char** names, uint64_t* launches, double* ms, double* bytes, uint32_t cap,
+                   uint32_t* n_out) {
+    PCHK(hipStreamSynchronize(d->s));
+    kharvest(d);
+    for (uint32_t i = 0; i < (uint32_t)KC_N && i < cap; ++i) {
+        names[i] = KC_NAMES[i];
+        launches[i] = d->kn[i];
+        ms[i] = d->kms[i];
+        bytes[i] = d->kbytes[i];
+    }
+    *n_out = KC_N;
     return 0;
 }
 

@@ -60,6 +60,9 @@ struct drv {
     pthread_mutex_t plock; /* the reference's path-cache lock */
     int path_err;
     char path_msg[256];    /* the failing lookup's message (sg_last_error is per thread) */
+    uint32_t msg_shift;    /* gossip: 16 (message id bits in an event id), else 0 */
+    uint32_t mw;           /* gossip: words per host in seen */
+    uint32_t* seen;        /* gossip: [N][mw] message bitsets (a host's owner writes them) */
 };
 
 static double mono_s(void) {
@@ -114,54 +117,85 @@ static void sched_push(drv* d, wctx* w, sg_hevent* e, uint32_t src, uint32_t dst
     if (src != dst && before < d->round_end) __atomic_add_fetch(&d->bumped, 1, __ATOMIC_RELAXED);
 }
 
-/* event_execute → the PHOLD task (worker.c:165-176) */
+/* One send from host h at `now` (worker_sendPacket, worker.c:243-304): the
+ * destination draw (test_phold.c:160-178), the path lookup, the reliability
+ * draw before the drop test, the delivery time.  msg: the gossip message id,
+ * kept in the low 16 bits of srcHostEventID's field (the engine's key layout,
+ * which keeps event_compare's order since (src, id) is unique); 0 for PHOLD. */
+static void send_one(drv* d, wctx* w, uint32_t h, sg_simtime now, uint32_t msg) {
+    int32_t x = sg_rand_r(&d->rng[h]);
+    uint32_t dst = choose_dst(d, x);
+    if (dst >= d->N) return;
+    w->sends++;
+    size_t pair = (size_t)d->T->host_vertex[h] * d->V + d->T->host_vertex[dst];
+    if (d->paths) {
+        /* topology_getReliability → _topology_getPathEntry: the path the
+         * reference's cache returns now (possibly the reverse entry), and
+         * the minimum latency stored so far (master.c:148-159 truncates it) */
+        uint64_t k = pair;
+        double m = 0;
+        pthread_mutex_lock(&d->plock);
+        int bad = sg_path_cache_lookup(d->paths, d->T->host_vertex[h], d->T->host_vertex[dst], &k, &m);
+        if (bad && !d->path_err) snprintf(d->path_msg, sizeof d->path_msg, "%s", sg_last_error());
+        pthread_mutex_unlock(&d->plock);
+        if (bad) {  /* no path the cache returned: send nothing, and the main
+                     * loop ends the run after this round (a worker cannot
+                     * leave mid-round: the others wait at its barriers) */
+            __atomic_store_n(&d->path_err, 1, __ATOMIC_RELAXED);
+            return;
+        }
+        pair = (size_t)k;
+        if (m > 0 && (uint64_t)m < w->jmin) w->jmin = (uint64_t)m;
+    } else {
+        uint64_t jm = d->T->jump_ms[pair];
+        if (jm < w->jmin) w->jmin = jm;
+    }
+    int32_t c = sg_rand_r(&d->rng[h]);
+    if (!(now < d->P.bootstrap_end || c <= d->T->keep_max[pair])) {
+        w->dropr++;
+        return;
+    }
+    sg_hevent* n = (sg_hevent*)malloc(sizeof *n);
+    n->time = now + d->T->delay_ns[pair];
+    n->seq = (d->evc[h]++ << d->msg_shift) | msg;
+    n->src = h;
+    n->dst = dst;
+    sched_push(d, w, n, h, dst);
+}
+
+/* event_execute → the task (worker.c:165-176): PHOLD (test_phold.c:234-239,
+ * 310-312), or configs[4]'s gossip body (orc.c execute_gossip: the origin's
+ * boot event schedules its message's self event, worker_scheduleTask
+ * worker.c:218-234; a host's first receipt forwards to `load` peers, later
+ * ones are dropped by its seen set) */
 static void execute(drv* d, wctx* w, sg_hevent* e) {
     const uint32_t h = e->dst;
     w->now = e->time;
-    d->digest[h] += digest_mix(d->pops[h]++, e->time, e->src, e->seq);
+    d->digest[h] += digest_mix(d->pops[h]++, e->time, e->src, e->seq >> d->msg_shift);
     w->pops++;
     const int boot = (e->src == h && e->seq == 0);
-    const uint32_t nsend = boot ? d->P.load : 1;
-    for (uint32_t m = 0; m < nsend; m++) {
-        int32_t x = sg_rand_r(&d->rng[h]);
-        uint32_t dst = choose_dst(d, x);
-        if (dst >= d->N) continue;
-        w->sends++;
-        size_t pair = (size_t)d->T->host_vertex[h] * d->V + d->T->host_vertex[dst];
-        if (d->paths) {
-            /* topology_getReliability → _topology_getPathEntry: the path the
-             * reference's cache returns now (possibly the reverse entry), and
-             * the minimum latency stored so far (master.c:148-159 truncates it) */
-            uint64_t k = pair;
-            double m = 0;
-            pthread_mutex_lock(&d->plock);
-            int bad = sg_path_cache_lookup(d->paths, d->T->host_vertex[h], d->T->host_vertex[dst], &k, &m);
-            if (bad && !d->path_err) snprintf(d->path_msg, sizeof d->path_msg, "%s", sg_last_error());
-            pthread_mutex_unlock(&d->plock);
-            if (bad) {  /* no path the cache returned: send nothing, and the main
-                         * loop ends the run after this round (a worker cannot
-                         * leave mid-round: the others wait at its barriers) */
-                __atomic_store_n(&d->path_err, 1, __ATOMIC_RELAXED);
-                continue;
+    if (d->P.workload == SG_WORKLOAD_GOSSIP) {
+        if (boot) {
+            const uint64_t N = d->N, M = d->P.gossip_msgs;
+            const uint64_t m = ((uint64_t)h * M + N - 1) / N; /* smallest m with m*N/M >= h */
+            if (m < M && (m * N) / M == h) {
+                sg_hevent* o = (sg_hevent*)malloc(sizeof *o);
+                o->time = d->P.gossip_start + m * d->P.gossip_interval;
+                o->seq = (d->evc[h]++ << d->msg_shift) | m;
+                o->src = o->dst = h;
+                sched_push(d, w, o, h, h);
             }
-            pair = (size_t)k;
-            if (m > 0 && (uint64_t)m < w->jmin) w->jmin = (uint64_t)m;
-        } else {
-            uint64_t jm = d->T->jump_ms[pair];
-            if (jm < w->jmin) w->jmin = jm;
+            return;
         }
-        int32_t c = sg_rand_r(&d->rng[h]);
-        if (!(e->time < d->P.bootstrap_end || c <= d->T->keep_max[pair])) {
-            w->dropr++;
-            continue;
-        }
-        sg_hevent* n = (sg_hevent*)malloc(sizeof *n);
-        n->time = e->time + d->T->delay_ns[pair];
-        n->seq = d->evc[h]++;
-        n->src = h;
-        n->dst = dst;
-        sched_push(d, w, n, h, dst);
+        const uint32_t msg = (uint32_t)(e->seq & ((1u << d->msg_shift) - 1));
+        uint32_t* sw = &d->seen[(size_t)h * d->mw + (msg >> 5)];
+        if (*sw & (1u << (msg & 31))) return; /* a duplicate: the pop still commits */
+        *sw |= 1u << (msg & 31);
+        for (uint32_t k = 0; k < d->P.load; k++) send_one(d, w, h, e->time, msg);
+        return;
     }
+    const uint32_t nsend = boot ? d->P.load : 1;
+    for (uint32_t m = 0; m < nsend; m++) send_one(d, w, h, e->time, 0);
 }
 
 /* scheduler_pop (scheduler.c:359-414) */
@@ -205,7 +239,7 @@ static void* worker_run(void* arg) {
         uint32_t h = mine[i];
         sg_hevent* e = (sg_hevent*)malloc(sizeof *e);
         e->time = 0;
-        e->seq = d->evc[h]++;
+        e->seq = d->evc[h]++ << d->msg_shift;
         e->src = h;
         e->dst = h;
         sched_push(d, w, e, h, h);
@@ -240,8 +274,10 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
                              uint64_t max_rounds, sg_sched_result* res, uint64_t* digest, uint64_t* pops,
                              uint32_t* rng, uint64_t* event_counter) {
     if (!P || !T || !ops || n_workers == 0 || P->n_hosts == 0 ||
-        (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh) || P->workload != SG_WORKLOAD_PHOLD) {
-        sg_set_error("sg_sched_run_phold: bad arguments (the CPU-worker driver runs the PHOLD body only)");
+        (P->dst_rule == SG_DST_WEIGHTS && !T->weight_thresh) || P->workload > SG_WORKLOAD_GOSSIP ||
+        (P->workload == SG_WORKLOAD_GOSSIP && (P->gossip_msgs == 0 || P->gossip_msgs > 65536 ||
+                                               P->gossip_msgs > P->n_hosts))) {
+        sg_set_error("sg_sched_run_phold: bad arguments (PHOLD, or gossip with 1 <= msgs <= min(hosts, 65536))");
         return SG_ERR_INVAL;
     }
     drv D;
@@ -259,6 +295,15 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
     d->evc = (uint64_t*)calloc(d->N, 8);
     d->pops = (uint64_t*)calloc(d->N, 8);
     d->digest = (uint64_t*)calloc(d->N, 8);
+    if (P->workload == SG_WORKLOAD_GOSSIP) {
+        d->msg_shift = 16;
+        d->mw = (P->gossip_msgs + 31) / 32;
+        d->seen = (uint32_t*)calloc((size_t)d->N * d->mw, 4);
+        if (!d->seen) {
+            sg_set_error("sg_sched_run_phold: out of memory");
+            return SG_ERR_NOMEM;
+        }
+    }
     d->w = (wctx*)calloc(n_workers, sizeof(wctx));
     uint32_t* order = (uint32_t*)malloc((size_t)d->N * 4);
     if (!d->rng || !d->evc || !d->pops || !d->digest || !d->w || !order) {
@@ -389,6 +434,7 @@ int sg_sched_run_phold_paths(const sg_phold_params* P, const sg_phold_tables* T,
     free(d->evc);
     free(d->pops);
     free(d->digest);
+    free(d->seen);
     free(d->w);
     pthread_mutex_destroy(&d->plock);
     if (d->path_err) {  /* the worker's message, on the caller's thread */
@@ -472,4 +518,8 @@ int sg_policy_ops_gpu(uint32_t n_threads, uint32_t max_hosts, int device, sg_sch
 /* First error recorded by the gpu ops adapter (0 if none). */
 int sg_policy_ops_gpu_error(const sg_sched_policy_ops* ops) {
     return ops && ops->data ? ((gpu_ops*)ops->data)->error : SG_ERR_INVAL;
+}
+
+sg_policy* sg_policy_ops_gpu_policy(const sg_sched_policy_ops* ops) {
+    return ops && ops->data && ops->free == g_free ? ((gpu_ops*)ops->data)->p : NULL;
 }

@@ -284,11 +284,13 @@ def _cuda_sync():
 
 
 def bench(args, make_shard=None):
-    """bench.py --gpus N under torch.distributed.run: the 1M-host PHOLD over N
-    GPUs (strong scaling: the host count stays 1M).  Returns the JSON dict on
+    """bench.py --gpus N under torch.distributed.run: the workload (args.cfg,
+    bench.py --workload; configs[3]'s 1M-host PHOLD by default) over N GPUs
+    (strong scaling: the host count stays fixed).  Returns the JSON dict on
     rank 0, None elsewhere.  make_shard(cfg, rank, world, device) builds the
     rank's shard: EngineShard (the product) unless a CPU test passes its own."""
     from . import phold
+    from . import workloads as WL
     from ._lib import KERNEL_CLASSES
     rank, world, local = _env_rank()
     if world != args.gpus:
@@ -304,7 +306,9 @@ def bench(args, make_shard=None):
         dist.init_process_group(args.dist_backend)
     # small collectives live where the backend wants them
     cdev = torch.device("cuda", dev) if args.dist_backend == "nccl" else torch.device("cpu")
-    cfg = phold.c4_config(n_hosts=args.hosts)
+    wname = getattr(args, "workload", "c4")
+    wl = WL.get(wname)
+    cfg = getattr(args, "cfg", None) or phold.c4_config(n_hosts=args.hosts)
     shard = make_shard(cfg, rank, world, dev)
     if args.dist_backend == "nccl" and not args.py_steps:
         try:
@@ -373,7 +377,7 @@ def bench(args, make_shard=None):
         vals = [kt[c][0] * 1e3 / kr for c in KERNEL_CLASSES]  # us per step per class
         vals += [kt["process"][1], proc_bytes(sb["pops"] - sa["pops"], a2 - a1),
                  kt["insert"][1], scatter_bytes(moves), kt["exchange"][1],
-                 float(world * shard.rows * getattr(shard, "row_words", 3) * 8)]  # exchange bytes this rank sends per step
+                 float(world * shard.rows * shard.row_words * 8)]  # exchange bytes this rank sends per step
         rows = _gather_rows(vals, cdev)
     else:
         rows = None
@@ -389,7 +393,7 @@ def bench(args, make_shard=None):
     if rank != 0:
         return None
     res = {
-        "metric": "committed events/sec (whole node), 1M-host PHOLD at 1/2/4/8 MI355X; bit-exact",
+        "metric": wl["metric"](cfg),
         "value": total / tmax,
         "unit": "events/s",
         "n_gpus": world,
@@ -401,10 +405,8 @@ def bench(args, make_shard=None):
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"PHOLD configs[3]: {args.hosts} hosts x 16, V=1024 log-normal "
-                               "latency (median 30 ms, sigma 0.9, min 1 ms), runahead 1 ms, "
-                               "weights rule, seed 1",
-                   "n_hosts": args.hosts, "events_timed": total,
+        "config": {"workload": wl["describe"](cfg), "name": wname,
+                   "n_hosts": cfg["n_hosts"], "events_timed": total,
                    "rounds_timed": rounds_sum // world, "drain_steps": (steps_sum - rounds_sum) // world,
                    "exchange_cap": cap,
                    "parallelism": f"hosts block-sharded {world} ways, one "
@@ -438,7 +440,13 @@ def dist_roofline(rows, nk, steps, classes):
         us = dict(zip(classes, r[:nk]))
         pn, pb, sn, sb, xn, xb = r[nk:nk + 6]
         kp = kernel_line(pb / max(pn, 1), us["process"] * 1e-6 * steps / max(pn, 1))
-        ks = kernel_line(sb / max(sn, 1), us["insert"] * 1e-6 * steps / max(sn, 1))
+        # the split step's k_scatter is two launches: k_spec (gather class,
+        # beside the exchange) and k_post (insert class, after it); their
+        # algorithmic bytes are priced against their summed time
+        scat_us = us["insert"] + us.get("gather", 0.0)
+        ks = kernel_line(sb / max(sn, 1), scat_us * 1e-6 * steps / max(sn, 1))
+        if us.get("gather", 0.0) > 0:
+            ks.update(k_spec_us=us["gather"] * steps / max(sn, 1), k_post_us=us["insert"] * steps / max(sn, 1))
         per_rank.append({"k_proc": kp, "k_scatter": ks,
                          "exchange": {"avg_us": us["exchange"] * steps / xn if xn else None,
                                       "bytes_per_step": xb, "timed": bool(xn)}})

@@ -118,6 +118,11 @@ class Engine:
         L.check(L.lib().sg_engine_gather_paths(self.h, *[C.byref(x) for x in v]))
         return dict(zip(("guessed", "listed"), (x.value for x in v)))
 
+    def debug_inject(self):
+        """Test only: corrupt two staged records before the next round's
+        k_scatter (sg_engine_debug_inject); the insert role must flag OV_BUG."""
+        L.check(L.lib().sg_engine_debug_inject(self.h))
+
     def host_state(self) -> dict:
         n = self.n_local
         d, p, e = (np.zeros(n, np.uint64) for _ in range(3))

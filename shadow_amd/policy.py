@@ -47,6 +47,11 @@ class SchedResult(C.Structure):
         return {n: (float if t is C.c_double else int)(getattr(self, n)) for n, t in self._fields_}
 
 
+class KernelStat(C.Structure):
+    """sg_kernel_stat (include/shadowgpu.h): one device kernel class of the policy."""
+    _fields_ = [("name", C.c_char * 16), ("launches", C.c_uint64), ("ms", C.c_double), ("alg_bytes", C.c_double)]
+
+
 def _bind():
     lib = L.lib()
     if not getattr(lib, "_policy_bound", False):
@@ -66,6 +71,11 @@ def _bind():
         lib.sg_path_cache_lookup.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_double)]
         lib.sg_path_cache_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        lib.sg_policy_ops_gpu_policy.argtypes = [C.POINTER(PolicyOps)]
+        lib.sg_policy_ops_gpu_policy.restype = C.c_void_p
+        lib.sg_policy_kernel_profile.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        lib.sg_policy_kernel_stats.argtypes = [C.c_void_p, C.POINTER(KernelStat), C.c_uint32,
+                                               C.POINTER(C.c_uint32)]
         lib._policy_bound = True
     return lib
 
@@ -112,6 +122,29 @@ def gpu_ops(n_workers: int, n_hosts: int, device: int = 0) -> PolicyOps:
     L.check(_bind().sg_policy_ops_gpu(n_workers, n_hosts, device, C.byref(ops)))
     ops._owner = "gpu"
     return ops
+
+
+def kernel_profile(ops: PolicyOps, enable: bool = True, skip_rounds: int = 0):
+    """Per-kernel device profile of a gpu vtable's policy (sg_policy_kernel_profile):
+    the first skip_rounds extractions are not counted."""
+    lib = _bind()
+    p = lib.sg_policy_ops_gpu_policy(C.byref(ops))
+    if not p:
+        raise ValueError("not a gpu policy vtable")
+    L.check(lib.sg_policy_kernel_profile(p, int(enable), skip_rounds))
+
+
+def kernel_stats(ops: PolicyOps) -> dict:
+    """{kernel: {launches, ms, alg_bytes}} of a gpu vtable's policy (before its free)."""
+    lib = _bind()
+    p = lib.sg_policy_ops_gpu_policy(C.byref(ops))
+    if not p:
+        raise ValueError("not a gpu policy vtable")
+    out = (KernelStat * 32)()
+    n = C.c_uint32()
+    L.check(lib.sg_policy_kernel_stats(p, out, 32, C.byref(n)))
+    return {out[i].name.decode(): {"launches": int(out[i].launches), "ms": float(out[i].ms),
+                                   "alg_bytes": float(out[i].alg_bytes)} for i in range(min(n.value, 32))}
 
 
 def phold_args(cfg: dict):

@@ -2,17 +2,25 @@
 interface (pre / post around one all-to-all), so the distributed step protocol
 of shadow_amd.dist — fixed-size exchange blocks with headers, drain steps when
 an outbox exceeds exchange_cap, the window from the received headers — can be
-exercised on CPU with gloo.  Mirrors sg_engine.hip's exchange-block writes
-(k_proc), received-event insertion (the next k_proc / k_scatter) and the window from the
-headers (step_view).  Never used by the product path."""
+exercised on CPU with gloo.  Its blocks have the engine's layout
+(sg_engine.hip, write_headers / k_proc's outbox copy): HDR = 4 header rows of
+RW = 2 int64 words {n, more, MIN, jmin, overflow, round, time base, 0}, then
+16-B event rows {time - the sender's window start (40 bits) | destination's
+index in the receiving shard << 40, src << 40 | srcHostEventID}, with the
+engine's bounds (a time offset below 2^40, a local destination below 2^24).
+Received-event insertion and the window from the headers follow the next
+k_proc / k_scatter (step_view).  Never used by the product path."""
 import numpy as np
 import torch
 
 from oracle import oracle as O
 from shadow_amd.dist import owner_bounds
 
-HDR = 2
+HDR = 4   # header rows (sg_engine.hip HDR)
+RW = 2    # int64 words per row (sg_engine.hip RW)
+H_N, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND, H_BASE = range(7)  # header words (enum Hdr)
 M64 = (1 << 64) - 1
+M40 = (1 << 40) - 1
 
 
 def _i64(x: int) -> int:
@@ -21,6 +29,8 @@ def _i64(x: int) -> int:
 
 
 class OracleShard:
+    row_words = RW
+
     def __init__(self, cfg, rank, world, exchange_cap=64):
         b = owner_bounds(cfg["n_hosts"], world)
         self.bounds = b
@@ -31,10 +41,11 @@ class OracleShard:
         self.msg_shift = np.uint64(16 if cfg.get("workload", 0) == 1 else 0)
         self.xcap = exchange_cap
         self.rows = HDR + exchange_cap
-        self.recv = torch.zeros((world, self.rows, 3), dtype=torch.int64)
+        self.recv = torch.zeros((world, self.rows, RW), dtype=torch.int64)
         self.phase = 0
         self.outq = [np.zeros((0, 3), np.int64) for _ in range(world)]
         self.sent = [0] * world
+        self.base = 0
         self.loc_min = (1 << 64) - 2
         self.loc_jmin = M64
         self.steps = 0
@@ -50,21 +61,28 @@ class OracleShard:
         return bool(self.sim.stats()["done"])
 
     def pre(self) -> torch.Tensor:
-        send = torch.zeros((self.world, self.rows, 3), dtype=torch.int64)
+        send = torch.zeros((self.world, self.rows, RW), dtype=torch.int64)
         if self._done():
             return send
+        st = self.sim.stats()
+        base = st["window_start"]  # H_BASE: the rows' time base (the step's window start)
         if self.phase == 0:
             self.sim.round_process()
             out = self.sim.outbox()
             owner = np.searchsorted(np.array(self.bounds[1:]), out["dst"], side="right")
             for p in range(self.world):
                 ev = out[owner == p] if p != self.rank else out[:0]
-                self.outq[p] = np.stack([ev["time"].astype(np.int64),
-                                         ((ev["src"].astype(np.uint64) << np.uint64(40)) |
-                                          (ev["seq"].astype(np.uint64) << self.msg_shift) |
-                                          ev["msg"].astype(np.uint64)).astype(np.int64),
-                                         ev["dst"].astype(np.int64)], 1) if len(ev) else \
-                    np.zeros((0, 3), np.int64)
+                if len(ev):
+                    rel = ev["time"].astype(np.uint64) - np.uint64(base)
+                    dl = ev["dst"].astype(np.uint64) - np.uint64(self.bounds[p])
+                    assert int(rel.max()) < (1 << 40), "time offset beyond 2^40 ns of the window start"
+                    assert int(dl.max()) < (1 << 24), "receiving-shard index beyond 24 bits"
+                    key = (ev["src"].astype(np.uint64) << np.uint64(40)) | \
+                          (ev["seq"].astype(np.uint64) << self.msg_shift) | ev["msg"].astype(np.uint64)
+                    self.outq[p] = np.stack([(rel | (dl << np.uint64(40))).astype(np.int64),
+                                             key.astype(np.int64)], 1)
+                else:
+                    self.outq[p] = np.zeros((0, RW), np.int64)
             self.sent = [0] * self.world
             self.peak = max([self.peak] + [len(self.outq[p]) for p in range(self.world) if p != self.rank])
             m = self.sim.local_min()
@@ -72,12 +90,14 @@ class OracleShard:
                 m = min(m, int(out["time"].min()))
             self.loc_min = m
             self.loc_jmin = self.sim.local_jmin()
+            self.base = base
         more = any(len(self.outq[q]) - self.sent[q] > self.xcap for q in range(self.world))
         rounds = self.sim.stats()["rounds"]
         for p in range(self.world):
             n = min(self.xcap, len(self.outq[p]) - self.sent[p])
-            send[p, 0] = torch.tensor([n, int(more), _i64(self.loc_min)])
-            send[p, 1] = torch.tensor([_i64(self.loc_jmin), 0, rounds])
+            h = send[p, :HDR].view(-1)
+            h[H_N], h[H_MORE], h[H_MIN] = n, int(more), _i64(self.loc_min)
+            h[H_JMIN], h[H_OVF], h[H_ROUND], h[H_BASE] = _i64(self.loc_jmin), 0, rounds, _i64(self.base)
             if n:
                 send[p, HDR:HDR + n] = torch.from_numpy(self.outq[p][self.sent[p]:self.sent[p] + n])
         return send
@@ -89,21 +109,22 @@ class OracleShard:
         m = j = M64
         more = False
         for p in range(self.world):
-            more |= bool(r[p, 0, 1])
-            m = min(m, int(r[p, 0, 2]) & M64)
-            j = min(j, int(r[p, 1, 0]) & M64)
-            assert int(r[p, 1, 2]) == self.sim.stats()["rounds"], "shards out of step"
-            n = int(r[p, 0, 0])
+            h = r[p, :HDR].reshape(-1)
+            more |= bool(h[H_MORE])
+            m = min(m, int(h[H_MIN]) & M64)
+            j = min(j, int(h[H_JMIN]) & M64)
+            assert int(h[H_ROUND]) == self.sim.stats()["rounds"], "shards out of step"
+            n = int(h[H_N])
             if p == self.rank or n == 0:
                 continue
-            tri = r[p, HDR:HDR + n].astype(np.uint64)
+            rows = r[p, HDR:HDR + n].astype(np.uint64)
             ev = np.zeros(n, O.EVENT_DTYPE)
-            ev["time"] = tri[:, 0]
-            low = tri[:, 1] & np.uint64((1 << 40) - 1)
+            ev["time"] = np.uint64(int(h[H_BASE]) & M64) + (rows[:, 0] & np.uint64(M40))
+            low = rows[:, 1] & np.uint64(M40)
             ev["seq"] = low >> self.msg_shift
             ev["msg"] = low & ((np.uint64(1) << self.msg_shift) - np.uint64(1))
-            ev["src"] = (tri[:, 1] >> np.uint64(40)).astype(np.uint32)
-            ev["dst"] = tri[:, 2].astype(np.uint32)
+            ev["src"] = (rows[:, 1] >> np.uint64(40)).astype(np.uint32)
+            ev["dst"] = ((rows[:, 0] >> np.uint64(40)) + np.uint64(self.bounds[self.rank])).astype(np.uint32)
             self.sim.ingest(ev)
         for q in range(self.world):
             self.sent[q] += min(self.xcap, len(self.outq[q]) - self.sent[q])
@@ -134,7 +155,7 @@ class OracleShard:
     def set_exchange_cap(self, cap):
         self.xcap = cap
         self.rows = HDR + cap
-        self.recv = torch.zeros((self.world, self.rows, 3), dtype=torch.int64)
+        self.recv = torch.zeros((self.world, self.rows, RW), dtype=torch.int64)
 
     def sync(self):
         pass

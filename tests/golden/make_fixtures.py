@@ -10,6 +10,9 @@ a test or the bench:
   c4_1m     configs[3]: PHOLD at 1M hosts, the state after every one of the
             first ROUNDS_C4 rounds (the bench's timed rounds are checked
             against it)
+  c2_rounds configs[1]: PHOLD 10k hosts on the 50 ms mesh, every round of the
+            whole run (bench.py --workload c2)
+  c5_rounds configs[4]: the gossip run of c5, every round (bench.py --workload c5)
 
 Per case: the oracle's counters and window, and a fingerprint of every host's
 end state (shadow_amd.trace.state_fingerprint over trace digest, pops, rand_r
@@ -41,7 +44,10 @@ CONFIGS = {
     "c3": lambda: phold.c3_config(),
     "c5": lambda: phold.c5_config(),
     "c4_1m": lambda: phold.c4_config(n_hosts=1_000_000),
+    "c2_rounds": lambda: phold.c2_config(),
+    "c5_rounds": lambda: phold.c5_config(),
 }
+PER_ROUND = {"c4_1m": ROUNDS_C4, "c2_rounds": 1 << 30, "c5_rounds": 1 << 30}
 
 
 def fingerprint(sim) -> int:
@@ -89,7 +95,7 @@ def main(names):
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}
     for name in names:
         t = time.time()
-        data[name] = per_round_case(name, ROUNDS_C4) if name == "c4_1m" else final_case(name)
+        data[name] = per_round_case(name, PER_ROUND[name]) if name in PER_ROUND else final_case(name)
         print(f"{name}: {time.time() - t:.1f} s", flush=True)
         json.dump(data, open(OUT, "w"), indent=1)
 

@@ -114,29 +114,55 @@ def test_c5_gossip_two_processes():
     assert (sum(x[3] for x in res) & ((1 << 64) - 1)) == FIX["c5"]["fingerprint"]
 
 
-def test_bench_two_ranks_self_launched():
-    """`python bench.py --gpus 2` with no launcher of its own (bench.py starts
-    torch.distributed.run), ranks on GPU 0 over gloo: one JSON line with the
-    two ranks' events and parity.match true."""
+def _self_launched_bench(n, extra, timeout):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
-                        "--warmup", "10", "--same-device", "--dist-backend", "gloo"],
-                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--same-device",
+                        "--dist-backend", "gloo"] + extra,
+                       capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["n_gpus"] == n and res["value"] > 0
     assert res["parity"]["match"] is True, res["parity"]
     assert res["metric"].endswith("; bit-exact")
     # the N > 1 line's roofline: every rank's k_proc / k_scatter fraction and
     # the exchange's bytes per step (north_star: a fraction per kernel at N > 1)
     rf = res["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["kernel"] == "k_proc"
-    assert len(rf["per_rank"]) == 2
+    assert len(rf["per_rank"]) == n
     for pr in rf["per_rank"]:
         for k in ("k_proc", "k_scatter"):
             assert pr[k]["avg_us"] > 0 and pr[k]["alg_bytes_per_launch"] > 0 and 0 < pr[k]["frac"] < 1, (k, pr)
         assert pr["exchange"]["bytes_per_step"] > 0
     assert set(rf["per_kernel"]) == {"k_proc", "k_scatter"}
+    return res
+
+
+def test_bench_two_ranks_self_launched():
+    """`python bench.py --gpus 2` with no launcher of its own (bench.py starts
+    torch.distributed.run), ranks on GPU 0 over gloo: one JSON line with the
+    two ranks' events and parity.match true."""
+    _self_launched_bench(2, ["--steps", "20", "--warmup", "10"], 300)
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_self_launched():
+    """The driver's N = 8 command, rehearsed: `bench.py --gpus 8` starting its
+    own torch.distributed.run, 8 ranks of 125k hosts of configs[3] (all on GPU
+    0, gloo in place of RCCL, which refuses two ranks on one device): the
+    parity point matches the oracle's per-round fixture and the line carries
+    8 per-rank roofline rows."""
+    res = _self_launched_bench(8, ["--steps", "20", "--warmup", "5", "--kernel-rounds", "10"], 600)
+    assert res["config"]["n_hosts"] == 1_000_000 and res["config"]["name"] == "c4"
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_gossip_workload():
+    """`bench.py --gpus 2 --workload c5`: configs[4]'s lossy gossip sharded over
+    two ranks (its 2/4/8-GPU scaling config is one flag away), checked against
+    the per-round fixture of the gossip run."""
+    res = _self_launched_bench(2, ["--workload", "c5", "--steps", "30", "--warmup", "100",
+                                   "--kernel-rounds", "10"], 600)
+    assert res["config"]["name"] == "c5" and res["config"]["n_hosts"] == 100_000

@@ -58,3 +58,32 @@ def test_c4_64bit_bucket_arithmetic_matches_the_oracle(monkeypatch):
     assert (st["pops"], st["window_start"], st["window_end"]) == (ROWS[60][1], ROWS[60][3], ROWS[60][4])
     hs = eng.host_state()
     assert state_fingerprint(eng.first_host, hs["digest"], hs["pops"], hs["rng"], hs["ev"]) == ROWS[60][2]
+
+
+def test_ov_bug_guard_clamps_corrupt_staged_records():
+    """The bounds guard of k_scatter's insert role (the round-4 fault,
+    profiles/r04/ablation/README.md): two staged records are corrupted between
+    a k_proc and its k_scatter (sg_engine_debug_inject: a host past the shard,
+    a time beyond the calendar's horizon).  The launch must clamp both in
+    bounds and flag OV_BUG (128) without faulting the GPU, the run must stop
+    on it, and a new engine in the same process must run configs[3] to its
+    fixture."""
+    from shadow_amd._lib import SgError
+    eng = Engine(phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2))
+    eng.boot()
+    eng.run(4)
+    assert eng.stats()["overflow"] == 0
+    eng.debug_inject()
+    with pytest.raises(SgError):
+        eng.run(4)  # stops at the next plan, which sees the flag
+    st = eng.stats()
+    assert st["overflow"] & 128, hex(st["overflow"])
+    assert st["overflow"] & ~(128 | 32) == 0, hex(st["overflow"])  # nothing else ran out
+    eng.close()
+    eng = Engine(phold.c4_config(n_hosts=1_000_000))
+    eng.boot()
+    eng.run(25)
+    st = eng.stats()
+    assert st["rounds"] == 25 and st["overflow"] == 0
+    hs = eng.host_state()
+    assert state_fingerprint(eng.first_host, hs["digest"], hs["pops"], hs["rng"], hs["ev"]) == ROWS[25][2]

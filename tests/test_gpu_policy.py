@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("kind,workers", [("tiny_lossy", 1), ("tiny_lossy", 4),
                                           ("probe10_bumps", 3), ("c2_small", 8),
-                                          ("self_heavy", 2), ("runahead", 5)])
+                                          ("self_heavy", 2), ("runahead", 5),
+                                          ("gossip_small", 1), ("gossip_small", 6)])
 def test_gpu_policy_matches_oracle(kind, workers):
     cfg = {
         "tiny_lossy": lambda: phold.tiny_config(n_hosts=200, V=6, load=4, end_time_s=0.4, loss=0.1),
@@ -21,6 +22,8 @@ def test_gpu_policy_matches_oracle(kind, workers):
         # 4 hosts: a quarter of all sends are self events, many inside the window
         "self_heavy": lambda: phold.probe_config(n_hosts=4, jump_ms=20, end_time_s=0.5),
         "runahead": lambda: phold.tiny_config(n_hosts=120, runahead_ms=6, end_time_s=0.3),
+        # configs[4]'s gossip body: lossy links, origin self events, seen sets
+        "gossip_small": lambda: phold.c5_config(n_hosts=3000, V=16, msgs=24, end_time_s=0.6),
     }[kind]()
     ref = O.Sim(cfg)
     ref.boot()
@@ -126,3 +129,29 @@ def test_gpu_policy_incast(n, w0):
     assert np.array_equal(r["ev"], rs["ev"])
     for k in ("rounds", "pops", "sends", "bumped"):
         assert r[k] == st[k], k
+
+
+def test_gpu_policy_kernel_profile():
+    """The device half's per-kernel profile (sg_policy_kernel_profile): every
+    insert / MIN / extraction kernel class is timed and carries algorithmic
+    bytes over the rounds after the skipped ones, and profiling changes nothing
+    in the run (per-host state still equals the oracle's)."""
+    cfg = phold.c2_config(n_hosts=2000, end_time_s=0.6)
+    ref = O.Sim(cfg)
+    ref.boot()
+    ref.run()
+    rs = ref.host_state()
+    ops = policy.gpu_ops(3, cfg["n_hosts"])
+    try:
+        policy.kernel_profile(ops, True, 2)
+        r = policy.run_phold(cfg, 3, ops, free_ops=False)
+        ks = policy.kernel_stats(ops)
+    finally:
+        ops.free(ops.data)
+    assert np.array_equal(r["digest"], rs["digest"])
+    assert list(ks)[:6] == ["k_cins1", "k_cneed", "k_calloc", "k_cins2", "k_cmin", "k_xplan"]
+    for k in ("k_cins1", "k_cins2", "k_cmin", "k_xplan", "k_hist", "k_part", "k_local", "k_xrank"):
+        assert ks[k]["launches"] > 0 and ks[k]["ms"] > 0 and ks[k]["alg_bytes"] > 0, (k, ks[k])
+    # the extraction classes ran once per counted round
+    assert ks["k_hist"]["launches"] == ks["k_part"]["launches"] == ks["k_xrank"]["launches"]
+    assert ks["k_hist"]["launches"] <= r["rounds"] - 2 + 1

@@ -78,6 +78,26 @@ def test_inprocess_shards_match_oracle(world, kind, xcap):
         assert st[0]["exchange_steps"] > want["rounds"]
 
 
+@pytest.mark.parametrize("split,gspec", [("1", "1"), ("1", "0"), ("1", "2"), ("0", "1")])
+def test_split_step_modes_match_oracle(split, gspec, monkeypatch):
+    """The split step (k_spec inserts, refills and gathers the
+    guessed bucket on a second stream beside the exchange; k_post plans from
+    the headers and keeps that gather on a hit) against the oracle: with the
+    guess on (hits in steady rounds), off (SG_GSPEC=0: k_post's list path every
+    round), deliberately wrong (SG_GSPEC=2: k_spec gathers the bucket after the
+    right one, k_post must discard it), and the unsplit step (SG_SPLIT=0)."""
+    monkeypatch.setenv("SG_SPLIT", split)  # read when the engines are created
+    monkeypatch.setenv("SG_GSPEC", gspec)
+    cfg = phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)
+    shards, _ = _run_shards(cfg, 4, None)
+    _check(cfg, shards)
+    g = [s.eng.gather_paths() for s in shards]
+    if gspec == "1":
+        assert all(x["guessed"] > 0 for x in g), g
+    else:
+        assert all(x["guessed"] == 0 and x["listed"] > 0 for x in g), g
+
+
 def test_sharded_windows_and_trace_match_oracle():
     cfg = phold.probe_config(n_hosts=300, jump_ms=10, end_time_s=0.3)
     shards, _ = _run_shards(cfg, 3, 16, trace=1 << 20)
@@ -139,6 +159,26 @@ def test_graph_rounds_match_oracle(graph, prepare):
     for k in ("digest", "pops", "rng", "ev"):
         assert np.array_equal(g[k], o[k]), k
     assert eng.stats()["rounds"] == ref.stats()["rounds"]
+
+
+def test_graph_prepare_runs_nothing_when_eager():
+    """sg_engine_graph_prepare under a setting that makes enqueue_batch launch
+    eagerly (kernel timing on): it must neither capture nor run rounds, so the
+    round count and the host state stay where they were."""
+    from shadow_amd.engine import Engine
+    cfg = phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)
+    eng = Engine(cfg, device=0)
+    eng.boot()
+    eng.run(3, batch=3)
+    eng.set_graph(8)
+    eng.set_timing(True)
+    r0 = eng.stats()["rounds"]
+    d0 = eng.host_state()["digest"].copy()
+    eng.prepare_graph()
+    assert eng.stats()["rounds"] == r0
+    assert np.array_equal(eng.host_state()["digest"], d0)
+    eng.set_timing(False)
+    eng.set_graph(0)
 
 
 POISON = -0x0123456789ABCDF  # not a valid event row or header
