@@ -95,6 +95,9 @@ def parse():
                          "instead of sg_engine_run_steps")
     ap.add_argument("--kernel-rounds", type=int, default=50,
                     help="rounds after the timed region that are re-run with per-kernel HIP events")
+    ap.add_argument("--kernel-timing", choices=("after", "inline"), default=None,
+                    help="per-kernel durations from rounds after the timed region (c4's default) or "
+                         "from the timed rounds themselves (c2 / c5: their rounds change along the run)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N > 1: nccl (RCCL, the measured path) or gloo (rehearsal only)")
     ap.add_argument("--dist", action="store_true",
@@ -108,9 +111,15 @@ def parse():
         ap.error("--hosts applies to --workload c4 only")
     a.warmup = w["warmup"] if a.warmup is None else a.warmup
     a.steps = w["steps"] if a.steps is None else a.steps
-    a.cfg = w["build"](a.hosts)
-    a.hosts = a.cfg["n_hosts"]
+    a.kernel_timing = a.kernel_timing or w["kernel_timing"]
     return a
+
+
+def build_config(a):
+    """The workload's config (a.cfg, a.hosts), built in the process that runs
+    it (a self-launching parent never loads the native library)."""
+    a.cfg = WL.get(a.workload)["build"](a.hosts)
+    a.hosts = a.cfg["n_hosts"]
 
 
 def _cpu_model() -> str:
@@ -223,7 +232,12 @@ def run_single(args):
     eng.set_graph(args.graph)
     eng.run(args.warmup, batch=args.graph or args.batch)
     eng.prepare_graph()  # graphs on: the first timed batch replays, it does not capture
+    inline = args.kernel_timing == "inline"
     s0 = eng.stats()
+    if inline:  # the timed rounds' own kernel durations (dispatch-packet timestamps, no extra packets)
+        a1, _ = eng.active_hosts()
+        mv1 = eng.event_moves()
+        eng.set_timing(True)
     eng.sync()
     # timed region: K rounds, nothing but the rounds on the stream (at most two
     # batches queued, no read-back)
@@ -231,6 +245,9 @@ def run_single(args):
     eng.enqueue_rounds(args.steps)
     eng.sync()
     dt = time.perf_counter() - t0
+    if inline:
+        kt = eng.kernel_times()
+        eng.set_timing(False)
     s1 = eng.stats()
     if s1["overflow"]:
         raise SystemExit(f"device queue overflow during bench: {s1['overflow']:#x}")
@@ -242,28 +259,32 @@ def run_single(args):
     hs = eng.host_state()  # the state at the end of the timed region, for the parity check
     fp = state_fingerprint(0, hs["digest"], hs["pops"], hs["rng"], hs["ev"])
     del hs
-    # kernel durations: the next rounds of the same run, every launch carrying
-    # HIP events as its dispatch packet's start / stop timestamps
-    # (hipExtLaunchKernelGGL) on the engine stream — kept out of the headline
-    # region all the same
-    a1, _ = eng.active_hosts()
-    mv1 = eng.event_moves()
-    kr = max(1, min(args.steps, args.kernel_rounds))
-    eng.set_timing(True)
-    eng.run(kr, batch=args.batch)
-    kt = eng.kernel_times()
-    eng.set_timing(False)
+    if inline:
+        kr, s2, kpops = rounds, s1, pops
+    else:
+        # kernel durations: the next rounds of the same run, every launch carrying
+        # HIP events as its dispatch packet's start / stop timestamps
+        # (hipExtLaunchKernelGGL) on the engine stream — kept out of the headline
+        # region all the same
+        a1, _ = eng.active_hosts()
+        mv1 = eng.event_moves()
+        kr = max(1, min(args.steps, args.kernel_rounds))
+        eng.set_timing(True)
+        eng.run(kr, batch=args.batch)
+        kt = eng.kernel_times()
+        eng.set_timing(False)
+        s2 = eng.stats()
+        kpops = s2["pops"] - s1["pops"]
+        kr = s2["rounds"] - s1["rounds"]
     proc_ms, proc_n = kt["process"]
-    s2 = eng.stats()
     a2, _ = eng.active_hosts()
     mv2 = eng.event_moves()
-    kpops = s2["pops"] - s1["pops"]
     alg_bytes = proc_bytes(kpops, a2 - a1)
     per_launch_bytes = alg_bytes / max(proc_n, 1)
     avg_launch_s = proc_ms / 1e3 / max(proc_n, 1)
     achieved = per_launch_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic, traffic_lower, traffic_src = pmc_traffic(args.workload, args.hosts)
-    kus = {k: v[0] * 1e3 / kr for k, v in kt.items() if v[1]}
+    kus = {k: v[0] * 1e3 / v[1] for k, v in kt.items() if v[1]}  # us per launch (one per round each)
     ins_ms, ins_n = kt["insert"]
     moves = {k: mv2[k] - mv1[k] for k in mv2}
     per_kernel = {
@@ -301,8 +322,10 @@ def run_single(args):
                      "per_kernel": per_kernel,
                      "gaps_us_per_round": dt * 1e6 / args.steps - sum(kus.values()),
                      "timing_method": "HIP events as each launch's dispatch-packet timestamps "
-                                      "(hipExtLaunchKernelGGL), rounds after the timed region; "
-                                      "the rest of ms_per_step is launch gaps"},
+                                      "(hipExtLaunchKernelGGL), " +
+                                      ("over the timed rounds themselves" if inline else
+                                       "rounds after the timed region") +
+                                      "; the rest of ms_per_step is launch gaps"},
         "_end_round": s1["rounds"], "_fingerprint": fp,
     }
     cw = wl["cpu_warmup"]
@@ -371,9 +394,12 @@ def main():
         sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1 or args.dist:
+        # dist.bench builds the config itself (args.cfg), after torch has set up
+        # the device: a rank that loaded the native library first saw no device
         from shadow_amd import dist
         res = dist.bench(args)
     else:
+        build_config(args)
         res = run_single(args)
     if res is None:
         return

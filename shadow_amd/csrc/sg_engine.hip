@@ -141,6 +141,22 @@ struct Slot {
 #ifndef SG_NT
 #define SG_NT 0
 #endif
+// SG_ABL (timing experiments only; results are wrong with any bit set): 1 no
+// digest atomics, 2 no host-state stores, 4 no destination loads, 8 no staging
+// stores, 16 no bucket bins, 32 no digest hash, 64 no bucket-minimum atomics in
+// the reservations, 128 no returning reservation atomics (bases read, not added)
+#ifndef SG_ABL
+#define SG_ABL 0
+#endif
+// SG_PMIN: each reserving row keeps its own minimum time offset per bucket
+// (pmin, a plain load / min / store of its own row) instead of a 64-bit
+// device-scope atomicMin on the bucket's minimum (bmin); the rmin role takes
+// the first non-empty bucket beyond the window and the minimum of its column.
+// In isolation (tools/resv_bench.hip, profiles/r05/resv) the atomicMin adds
+// 3.4 us to 256 x 300 reservations, the row update 0.6 us.
+#ifndef SG_PMIN
+#define SG_PMIN 1
+#endif
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ Rec ld_stream(const Rec* p) {
 #if SG_NT & 1
@@ -318,6 +334,7 @@ struct Dev {
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
+    uint32_t grec;                // gossip: hosts record their forwards for phases B / C (SG_GREC, default 1)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
@@ -342,7 +359,9 @@ struct Dev {
     uint32_t* bw;             // [2][XS][R] slots written before the step: k_scatter reads
                               // bw[fold & 1] and copies bk into the other half for the next step
     uint32_t* btomb;          // [R] tombstones
-    uint64_t* bmin;           // [R] min live time
+    uint64_t* bmin;           // [R] min live time (SG_PMIN=0)
+    uint32_t* pmin;           // [P][R] SG_PMIN: each reserving row's min time offset in each bucket
+                              // (UINT32_MAX: none); a bucket's minimum is its column's
     uint32_t* fring;          // [NCH] free chunk ring (head: rs->fl_head, taken atomically)
     uint32_t* stash;          // [P + G3][ST] chunk ids each reserving row keeps at hand
     uint32_t* stn;            // [P + G3] ids in the row's stash
@@ -753,6 +772,7 @@ __global__ void k_boot(Dev d) {
         d.btomb[i] = 0;
         d.bmin[i] = i == 0 ? 0 : UINT64_MAX;
     }
+    for (size_t j = i; j < (size_t)d.P * d.R; j += (size_t)gridDim.x * blockDim.x) d.pmin[j] = UINT32_MAX;
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
     if (i < d.P) {
         d.pcnt[i] = 0;
@@ -1529,7 +1549,15 @@ __device__ __forceinline__ SegScan seg_scan(const Rec* seg, uint32_t cnt, uint64
 // event.c:38 after worker.c:268-273); no self event can land inside the window
 // (host_single.c:237-267 would pop it this round).  Every lane of the host
 // computes the same answer; the others run phase A.
-constexpr uint32_t FLAT_CMAX = 16;
+// Events of one host the flat pass takes at most (each lane scans its host's
+// events in LDS and replays the draws of those before it, so a lane's work
+// grows with it).  configs[1] (10k hosts, 16 events each, 50 ms windows) has
+// Poisson(16) events per host per round: at 16, 43 % of its hosts fell back to
+// phase A, one lane per host (k_proc 85 us per round; profiles/r05/stamps).
+#ifndef SG_FLAT_CMAX
+#define SG_FLAT_CMAX 64
+#endif
+constexpr uint32_t FLAT_CMAX = SG_FLAT_CMAX;
 __device__ __forceinline__ bool flat_ok(const Dev& d, uint32_t cnt, const SegScan& s, bool self_possible, uint64_t S,
                                         uint64_t E, uint32_t vh) {
     if (s.boot || cnt > FLAT_CMAX || (cnt > 1 && d.pair_fmt != PAIR_DELAY)) return false;
@@ -1573,10 +1601,18 @@ __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint
         first[q] = 0;
         const uint32_t c = rb < R ? s_bc[rb] : 0u;
         if (!c) continue;
-        const uint32_t base = atomicAdd(&bkx[rb], c);
+#if SG_PMIN
+        uint32_t* pm = d.pmin + (size_t)row * R + rb;  // this row's own entry: no other row writes it
+        const uint32_t pold = *pm;
+#endif
+        const uint32_t base = (SG_ABL & 128) ? bkx[rb] : atomicAdd(&bkx[rb], c);
         wb[rb] = base;
+#if SG_PMIN
+        *pm = s_bm[rb] < pold ? s_bm[rb] : pold;
+#else
         const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
-        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
+        if (!(SG_ABL & 64)) atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
+#endif
         const uint32_t f = (base + CH - 1) >> CH_SHIFT, l = (base + c - 1) >> CH_SHIFT;
         first[q] = f;
         nn[q] = l + 1 > f ? l + 1 - f : 0u;
@@ -1897,6 +1933,15 @@ __device__ __forceinline__ void reset_consumed(const Dev& d) {
             atomicExch((unsigned long long*)&d.bmin[rb], (unsigned long long)UINT64_MAX);
         }
     }
+#if SG_PMIN
+    // the consumed buckets' columns of every row's minima (the rows reserve in
+    // buckets at or after the current window only, so none writes these now)
+    for (uint32_t i = threadIdx.x; i < nb * d.P; i += blockDim.x) {
+        const uint64_t b = pbS + i / d.P;
+        if (b == pret && pret >= bS) continue;
+        d.pmin[(size_t)(i % d.P) * R + (uint32_t)(b % R)] = UINT32_MAX;
+    }
+#endif
 }
 
 // One workgroup per partition of HP hosts.
@@ -2106,12 +2151,6 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
     return mn;
 }
 
-// SG_ABL (timing experiments only; results are wrong with any bit set): 1 no
-// digest atomics, 2 no host-state stores, 4 no destination loads, 8 no staging
-// stores, 16 no bucket bins, 32 no digest hash
-#ifndef SG_ABL
-#define SG_ABL 0
-#endif
 // The next gather's guessed due list (GSpec): when this window ends on a
 // bucket boundary, the next one most likely is that bucket, whole.  Its slots
 // written before the step are bw[fold & 1] (the last k_scatter's copy) and
@@ -2152,6 +2191,14 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #endif
 #ifndef SG_INS_PRE
 #define SG_INS_PRE 1
+#endif
+// SG_LATE_TICKET: k_scatter's workgroups arrive on the plan counter at their
+// end (1) or right after planning (0).  Arriving early, the 386 arrivals land
+// together on one counter (fan-in ~11 ns each), and wave 0 of every role then
+// waits for its arrival at its first load-use (vmcnt counts in order): the
+// stamps showed 7 us from entry to role start (profiles/r05/stamps).
+#ifndef SG_LATE_TICKET
+#define SG_LATE_TICKET 1
 #endif
 // SG_FLAT_LDSB: the barrier after the flat pass orders LDS only (default;
 // profiles/r04/flatb: 52.2 against 52.5-53.3 us/round, interleaved).
@@ -2514,6 +2561,24 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if (!bin_time(d, t, bS, bSW, bSr, s_bc, s_bm)) horizon = true;
     };
     uint32_t nacta = nact;  // the hosts phase A takes: s_act[0, nacta)
+    // gossip (configs[4]): hosts take the record path (phases B / C resolve
+    // their sends one lane each) while the message ids fit the record's 12 bits
+    // and the host's seen set GMW registers
+    constexpr uint32_t GMW = 4;
+    // (the flat pass is PHOLD's: its instantiations carry none of this)
+    const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
+                            d.mw <= GMW && d.grec;
+    uint32_t gsw[GMW];
+    auto gword = [](const uint32_t (&w)[GMW], uint32_t i) __attribute__((always_inline)) {
+        uint32_t v = w[0];
+#pragma unroll
+        for (uint32_t k = 1; k < GMW; ++k) v = i == k ? w[k] : v;
+        return v;
+    };
+    auto gset = [](uint32_t (&w)[GMW], uint32_t i, uint32_t v) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t k = 0; k < GMW; ++k) w[k] = i == k ? v : w[k];
+    };
     auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
         Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
 #pragma unroll 1
@@ -2551,7 +2616,33 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     if (st0) stamp[8] = wait_stamp();
                     sort_segment(seg, cnt);  // pop order
                     if (st0) stamp[9] = wait_stamp();
-                    if (d.workload != SG_WORKLOAD_PHOLD ||
+                    // gossip hosts record their forwards for phases B / C (their
+                    // loads one lane per send) unless a boot event or a same-round
+                    // self event needs the sequential body
+                    bool gos = gossip_rec && !(self_possible && S + (seg[0].a & M52) + self_delay < E);
+                    for (uint32_t i = 0; gos && i < cnt; ++i) {
+                        const uint64_t bk = seg[i].k;
+                        gos = !(((uint32_t)(bk >> SRC_SHIFT) == c.h) & ((bk & SEQ_MASK) == 0));
+                    }
+                    if (gos) {
+                        // forwards, at most: a message's first receipt (in the
+                        // host's seen set as the round leaves it so far) sends to
+                        // `load` peers; the record path pads the draws that select
+                        // no host.  The seen words stay in registers until the
+                        // host's records are written.
+#pragma unroll
+                        for (uint32_t w = 0; w < GMW; ++w) gsw[w] = w < d.mw ? d.seen[(size_t)lh * d.mw + w] : 0u;
+                        uint32_t tmp[GMW];
+#pragma unroll
+                        for (uint32_t w = 0; w < GMW; ++w) tmp[w] = gsw[w];
+                        for (uint32_t i = 0; i < cnt; ++i) {
+                            const uint32_t msg = (uint32_t)(seg[i].k & 0xFFFFu), bit = 1u << (msg & 31);
+                            const uint32_t wv = gword(tmp, msg >> 5);
+                            ns += wv & bit ? 0u : d.load;
+                            gset(tmp, msg >> 5, wv | bit);
+                        }
+                        go = true;
+                    } else if (d.workload != SG_WORKLOAD_PHOLD ||
                                (self_possible && S + (seg[0].a & M52) + self_delay < E)) {
                         // sequential body: a self event may land inside this window
                         uint32_t nx = 0;
@@ -2665,9 +2756,57 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             s_vh[j] = c.vh | (ns << 16);
             sput(base, Rec{c.s.evc, HDR_REC | ((uint64_t)j << 32) | c.h});
             uint32_t k = base + 1;
-            pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
-                sput(k++, Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
-            });
+            if (gossip_rec) {  // (a lane on this path with gossip took the gossip record path)
+                // the gossip body's draws (orc.c execute_gossip): trace digest,
+                // then per first receipt `load` sends, each a destination draw and,
+                // when it selects a host, the reliability draw (worker.c:268-269);
+                // the message id rides in the record (bits 40-51)
+                for (uint32_t i = 0; i < cnt; ++i) {
+                    const Rec ev = seg[i];
+                    const uint64_t trel = ev.a & M52, bt = S + trel;
+                    const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
+                    const uint64_t bseq = (ev.k & SEQ_MASK) >> d.msg_shift;
+                    const uint32_t msg = (uint32_t)(ev.k & 0xFFFFu), bit = 1u << (msg & 31);
+                    c.s.digest += digest_mix(c.s.pops, bt, bsrc, bseq);
+                    if (d.trace) {
+                        const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
+                        if (ts < d.trace_cap) {
+                            sg_trace_rec tr;
+                            tr.time = bt;
+                            tr.seq = bseq;
+                            tr.host = c.h;
+                            tr.src = bsrc;
+                            tr.pos = c.s.pops;
+                            d.trace[ts] = tr;
+                        } else {
+                            a.overflow = true;
+                        }
+                    }
+                    ++c.s.pops;
+                    ++a.ctr[C_POPS];
+                    const uint32_t wv = gword(gsw, msg >> 5);
+                    if (wv & bit) continue;  // a duplicate: the pop still commits
+                    gset(gsw, msg >> 5, wv | bit);
+                    for (uint32_t m = 0; m < d.load; ++m) {
+                        const int32_t x = dev_rand_r(c.s.rng);
+                        if (x > last) {  // no host selected (test_phold.c:176-177)
+                            ++a.ctr[C_NULL];
+                            continue;
+                        }
+                        const int32_t ch = dev_rand_r(c.s.rng);  // worker.c:268-269
+                        ++a.ctr[C_SENDS];
+                        sput(k++, Rec{((uint64_t)j << 52) | ((uint64_t)msg << 40) | trel,
+                                      (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
+                    }
+                }
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w)
+                    if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = gsw[w];
+            } else {
+                pop_segment(d, rs, S, c, a, seg, cnt, last, [&](int32_t x, int32_t ch, uint64_t trel) {
+                    sput(k++, Rec{((uint64_t)j << 52) | trel, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
+                });
+            }
             const uint32_t nreal = k - base - 1;  // sends with a destination
             for (; k <= base + ns; ++k) sput(k, Rec{0, HDR_REC | PAD_REC});  // draws that selected no host
             // {rng, pops, digest} now; evc now too when every send is kept, else
@@ -2914,7 +3053,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             a.jmin = pr.jump < a.jmin ? pr.jump : a.jmin;  // topology.c:1374-1385
             if (d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j] & 0xFFFFu) * d.V + vd], 1u);  // worker.c:279
             const uint64_t sq = hd.a + (i - sb - 1);   // event.c:38: the host's real sends precede its pads
-            uint64_t tn = S + (r.a & M52) + pr.delay;  // worker.c:275-277
+            // gossip records carry the message id in bits 40-51 (the key's low bits)
+            const uint64_t msg = gossip_rec ? (r.a >> 40) & 0xFFFu : 0u;
+            uint64_t tn = S + (r.a & (gossip_rec ? M40 : M52)) + pr.delay;  // worker.c:275-277
             if (tn >= d.end_time) {                    // scheduler.c:343-346
                 ++a.ctr[C_DROPEND];
                 continue;
@@ -2926,7 +3067,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 ++a.ctr[C_BUMPED];
             }
             const uint32_t h = (uint32_t)hd.k;
-            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
+            if (sq >> (SRC_SHIFT - d.msg_shift)) a.overflow = true;
+            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | (sq << d.msg_shift) | msg))
+                count_local(tn);
         }
     } else {
         for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
@@ -2951,25 +3094,30 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
             const PairRec pr0 = pair_of(s_vh[j0] & 0xFFFFu, vd0, want_jump);
             const PairRec pr1 = pair_of(s_vh[j1] & 0xFFFFu, vd1, want_jump);
+            // gossip records carry the message id in bits 40-51; it moves to
+            // the resolved record's high word beside the destination
+            const uint64_t tmask = gossip_rec ? M40 : M52;
             if (!(r0.k & HDR_REC)) {
-                const uint64_t bt = S + (r0.a & M52);
+                const uint64_t bt = S + (r0.a & tmask);
                 const int32_t ch = (int32_t)(uint32_t)(r0.k >> 32);
                 a.jmin = pr0.jump < a.jmin ? pr0.jump : a.jmin;            // topology.c:1374-1385
                 const bool keep = bt < d.bootstrap_end || ch <= pr0.keep;  // worker.c:268-273
                 if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j0] & 0xFFFFu) * d.V + vd0], 1u);
                 const uint64_t rel = bt + pr0.delay - S;  // worker.c:275-277
                 if (rel >> 40) a.overflow = true;
-                sput(i0, Rec{((uint64_t)keep << 63) | ((uint64_t)j0 << 40) | rel, dst0});
+                const uint64_t msg = gossip_rec ? (r0.a >> 40) & 0xFFFu : 0u;
+                sput(i0, Rec{((uint64_t)keep << 63) | ((uint64_t)j0 << 40) | rel, dst0 | (msg << 32)});
             }
             if (v1 && !(r1.k & HDR_REC)) {
-                const uint64_t bt = S + (r1.a & M52);
+                const uint64_t bt = S + (r1.a & tmask);
                 const int32_t ch = (int32_t)(uint32_t)(r1.k >> 32);
                 a.jmin = pr1.jump < a.jmin ? pr1.jump : a.jmin;
                 const bool keep = bt < d.bootstrap_end || ch <= pr1.keep;
                 if (keep && d.pcount) atomicAdd(&d.pcount[(size_t)(s_vh[j1] & 0xFFFFu) * d.V + vd1], 1u);
                 const uint64_t rel = bt + pr1.delay - S;
                 if (rel >> 40) a.overflow = true;
-                sput(i1, Rec{((uint64_t)keep << 63) | ((uint64_t)j1 << 40) | rel, dst1});
+                const uint64_t msg = gossip_rec ? (r1.a >> 40) & 0xFFFu : 0u;
+                sput(i1, Rec{((uint64_t)keep << 63) | ((uint64_t)j1 << 40) | rel, dst1 | (msg << 32)});
             }
         }
         __syncthreads();
@@ -3007,6 +3155,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 continue;
             }
             const uint32_t dst = (uint32_t)r.k;
+            const uint64_t msg = r.k >> 32;  // gossip: the message id (0 for PHOLD)
             const uint32_t sg = d.lo + sbase + s_act[j];
             if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
             if (dst != sg && tn < E) {              // host_single.c:180-184
@@ -3014,7 +3163,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 ++a.ctr[C_BUMPED];
             }
             const uint32_t h = (uint32_t)hd.k;
-            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | sq)) count_local(tn);
+            if (sq >> (SRC_SHIFT - d.msg_shift)) a.overflow = true;
+            if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)h << SRC_SHIFT) | (sq << d.msg_shift) | msg))
+                count_local(tn);
         }
     }
     if (stage_recv) {  // uniform; a barrier inside
@@ -3374,6 +3525,7 @@ __device__ __forceinline__ void refill_role(const Dev& d, uint32_t nx, uint64_t 
 // (publish_step).  Nothing waits for anything: no workgroup depends on another
 // being resident, whatever the order the hardware dispatches them in.
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, int mode) {
+    const uint64_t t_in = d.stamps ? __builtin_amdgcn_s_memrealtime() : 0;  // SG_STAMPS: the workgroup's entry
     RoundState* rs = d.rs;
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     __shared__ StepView sv;
@@ -3403,8 +3555,10 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         // address is made opaque (divergent to the compiler): for a uniform one
         // the atomic optimizer reads the result back at once, which would wait
         // for the arrival's round trip here.
+#if !SG_LATE_TICKET
         const uint32_t z = opaque(tid) - tid;  // 0
         if (!sv.quit) ticket = atomicAdd((unsigned long long*)&rs->splan + z, 1ull);
+#endif
     }
     // gather workgroups, wave 1: the guessed due list (GSpec) beside the round state
     if (blk >= g0 && blk < gx && (tid >> 6) == 1) gspec_load(d, blk - g0, gx - g0, s_gsw, (DueEnt*)(lds + GDE_OFF));
@@ -3458,6 +3612,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         st[4] = blk == nv - 1 ? 3 : blk == nv - 2 ? 4 : blk >= g0 ? 2 : blk >= d.P ? 1 : 0;
         st[1] = st[2] = st[3] = st[6] = st[0];
         st[5] = 0;
+        st[16] = t_in;
     }
     if (blk == nv - 1) {
         uint64_t* s16 = (uint64_t*)lds;
@@ -3484,6 +3639,40 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         const uint64_t bS = sv.bS, bL = sv.bL, pbS = sv.pbS, pbL = sv.pbL;
         const uint32_t span = (uint32_t)(bL - bS), bLr = (uint32_t)(bL % R);
         constexpr uint32_t OPT = RMAX / K3_T;
+#if SG_PMIN
+        // the first bucket beyond the window holding events (reserved slots),
+        // then the minimum of its column of the rows' minima
+        uint32_t kv[OPT];  // every count in flight at once (clamped slots)
+#pragma unroll
+        for (uint32_t q = 0; q < OPT; ++q) {
+            const uint32_t o = tid + 1 + q * K3_T;
+            const uint32_t rb = o + span < R ? (bLr + o >= R ? bLr + o - R : bLr + o) : 0u;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < XS; ++x) c += d.bk[(size_t)x * R + rb];
+            kv[q] = c;
+        }
+        uint64_t fo = UINT64_MAX;
+#pragma unroll
+        for (uint32_t q = 0; q < OPT; ++q) {
+            const uint32_t o = tid + 1 + q * K3_T;
+            const uint64_t b = bL + o - R;  // the ring slot's consumed bucket, if any
+            const bool live = o + span < R && !(pbS != UINT64_MAX && b >= pbS && b <= pbL);
+            fo = live && kv[q] && o < fo ? o : fo;
+        }
+        fo = block_min(fo, s16);  // barriers inside
+        uint64_t mn = UINT64_MAX;
+        if (fo != UINT64_MAX) {  // uniform
+            const uint32_t rb = bLr + (uint32_t)fo >= R ? bLr + (uint32_t)fo - R : bLr + (uint32_t)fo;
+            uint32_t m = UINT32_MAX;
+            for (uint32_t p = tid; p < d.P; p += K3_T) {
+                const uint32_t v = d.pmin[(size_t)p * R + rb];
+                m = v < m ? v : m;
+            }
+            const uint64_t bm = block_min((uint64_t)m, s16);
+            mn = bm != UINT32_MAX ? (bL + fo) * d.W + bm : UINT64_MAX;
+        }
+#else
         uint64_t bv[OPT];  // every minimum in flight at once (clamped slots)
 #pragma unroll
         for (uint32_t q = 0; q < OPT; ++q) {
@@ -3500,6 +3689,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
             mn = live && bv[q] < mn ? bv[q] : mn;
         }
         mn = block_min(mn, s16);  // barriers inside
+#endif
         if (tid == 0) {
             rs->rmin2[sv.cur ^ 1] = mn < SIMTIME_MAX ? mn : SIMTIME_MAX;
             if (st) st[3] = __builtin_amdgcn_s_memrealtime();
@@ -3620,6 +3810,12 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     }
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
+#if SG_LATE_TICKET
+    if (tid == 0) {
+        const uint32_t z = opaque(tid) - tid;  // 0
+        ticket = atomicAdd((unsigned long long*)&rs->splan + z, 1ull);
+    }
+#endif
     if (tid == 0 && ticket == gridDim.x - 1) publish_step(d, mode, sv, recv);
 }
 
@@ -3849,6 +4045,7 @@ struct sg_engine {
     // by ev_proc (after k_proc) and ev_spec (before k_post)
     hipStream_t aux = nullptr;
     hipEvent_t ev_proc = nullptr, ev_spec = nullptr;
+    bool split_same = false;  // SG_SPLIT=2 (measurement): k_spec on the engine stream, no fork / join
     bool booted;
     std::vector<void*> allocs;
     uint32_t* pcount_buf = nullptr;  // path packet counters, once enabled
@@ -4109,8 +4306,13 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     d.G1 = env_u32("SG_GATHER_GRID", 128);
     // the split step for the step API (several shards, or one with exchange_cap
-    // set): SG_SPLIT=0 keeps the whole k_scatter after the all-to-all (A/B)
-    d.split = (G > 1 || p.exchange_cap) && env_u32z("SG_SPLIT", 1) != 0 ? 1u : 0u;
+    // set), SG_SPLIT=1: k_spec on a second stream beside the all-to-all.  Off by
+    // default: the fork and join between the streams cost more than the overlap
+    // saves (world-1 RCCL steps at 125k hosts 56-57 against 37.5 us, at 1M 81
+    // against 63.5 us; profiles/r05/split/).  SG_SPLIT=2 runs k_spec in stream
+    // order (measurement of the fork / join's cost)
+    const uint32_t split_env = env_u32z("SG_SPLIT", 0);
+    d.split = (G > 1 || p.exchange_cap) && split_env != 0 ? 1u : 0u;
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
@@ -4288,6 +4490,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.light_max = std::min<uint32_t>(env_u32z("SG_LIGHT_MAX", 2), 2);
     D.rec_all = env_u32z("SG_REC_ALL", 2 * K2_T);
     D.flat = env_u32z("SG_FLAT", 1) != 0 && D.workload == SG_WORKLOAD_PHOLD;
+    D.grec = env_u32z("SG_GREC", 1) != 0 ? 1u : 0u;
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
@@ -4334,6 +4537,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.bw, (size_t)2 * XS * D.R);
     ALLOC(D.btomb, D.R);
     ALLOC(D.bmin, D.R);
+    ALLOC(D.pmin, (size_t)D.P * D.R);
     ALLOC(D.fring, D.NCH);
     ALLOC(D.stash, (size_t)(D.P + D.G3) * ST);
     ALLOC(D.stn, D.P + D.G3);
@@ -4377,7 +4581,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         }
         e->own_stream = true;
     }
-    if (D.split && (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
+    e->split_same = D.split && split_env == 2;
+    if (D.split && !e->split_same && (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
                     hipEventCreateWithFlags(&e->ev_proc, hipEventDisableTiming) != hipSuccess ||
                     hipEventCreateWithFlags(&e->ev_spec, hipEventDisableTiming) != hipSuccess)) {
         sg_engine_destroy(e);
@@ -4561,7 +4766,7 @@ static int enqueue_process(sg_engine* e) {
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
     if (recv && d.split) {
-        HIPCHK(hipStreamWaitEvent(e->stream, e->ev_spec, 0));
+        if (!e->split_same) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_spec, 0));
         return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
             SG_LAUNCH(k_scatter, dim3(d.G3 + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv, 3);
         });
@@ -4576,6 +4781,10 @@ static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
 // all-to-all the caller enqueues next on the engine stream.
 static int enqueue_spec(sg_engine* e) {
     const Dev& d = e->d;
+    if (e->split_same)  // measurement: the same kernels in stream order, nothing beside the exchange
+        return timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {
+            SG_LAUNCH(k_spec, dim3(d.G1 + d.P + 1), dim3(K3_T), 0, e->stream, a, b, d);
+        });
     HIPCHK(hipEventRecord(e->ev_proc, e->stream));
     HIPCHK(hipStreamWaitEvent(e->aux, e->ev_proc, 0));
     int rc = timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {

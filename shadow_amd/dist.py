@@ -308,7 +308,13 @@ def bench(args, make_shard=None):
     cdev = torch.device("cuda", dev) if args.dist_backend == "nccl" else torch.device("cpu")
     wname = getattr(args, "workload", "c4")
     wl = WL.get(wname)
-    cfg = getattr(args, "cfg", None) or phold.c4_config(n_hosts=args.hosts)
+    # the config is built here, once torch has set up the device: ranks that
+    # loaded the native library before it saw no HIP device
+    cfg = getattr(args, "cfg", None)
+    if cfg is None:
+        cfg = wl["build"](args.hosts) if hasattr(args, "workload") else phold.c4_config(n_hosts=args.hosts)
+        args.cfg = cfg
+    args.hosts = cfg["n_hosts"]
     shard = make_shard(cfg, rank, world, dev)
     if args.dist_backend == "nccl" and not args.py_steps:
         try:

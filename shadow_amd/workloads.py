@@ -11,8 +11,10 @@
 
 Each entry: the config builder, a description for the bench line's
 config.workload, the default warmup / timed rounds (a window of the run where
-the rounds are busy: gossip floods peak around rounds 100-240), and the key of
-its per-round oracle fixture in tests/golden/oracle_fixtures.json.
+the rounds are busy: gossip floods peak around rounds 100-240), where the
+per-kernel durations come from (rounds after the timed region, or the timed
+rounds themselves where the rounds change along the run), and the key of its
+per-round oracle fixture in tests/golden/oracle_fixtures.json.
 """
 from __future__ import annotations
 
@@ -31,14 +33,14 @@ WORKLOADS = {
         describe=lambda cfg: (f"PHOLD configs[3]: {cfg['n_hosts']} hosts x 16, V=1024 log-normal latency "
                               "(median 30 ms, sigma 0.9, min 1 ms), runahead 1 ms, weights rule, seed 1"),
         metric=lambda cfg: METRIC_C4,
-        warmup=20, steps=200, cpu_warmup=12,
+        warmup=20, steps=200, cpu_warmup=12, kernel_timing="after",
         fixture=lambda cfg: "c4_1m" if cfg["n_hosts"] == 1_000_000 else None),
     "c2": dict(
         build=lambda hosts: phold.c2_config(),
         describe=lambda cfg: (f"PHOLD configs[1]: {cfg['n_hosts']} hosts x 16, uniform 50 ms full mesh "
                               "(one vertex), weights rule, seed 1 (50 ms windows: every event due each round)"),
         metric=lambda cfg: "committed events/sec (whole node), configs[1] 10k-host PHOLD on MI355X; bit-exact",
-        warmup=10, steps=150, cpu_warmup=12,
+        warmup=10, steps=150, cpu_warmup=12, kernel_timing="inline",
         fixture=lambda cfg: "c2_rounds"),
     "c5": dict(
         build=lambda hosts: phold.c5_config(),
@@ -46,7 +48,7 @@ WORKLOADS = {
                               "V=256 log-normal latency (median 40 ms, min 2 ms), edge loss 0.5-5 %, seed 1"),
         metric=lambda cfg: ("committed events/sec (whole node), configs[4] 100k-host lossy gossip on "
                             "MI355X; bit-exact"),
-        warmup=100, steps=120, cpu_warmup=100,
+        warmup=100, steps=120, cpu_warmup=100, kernel_timing="inline",
         fixture=lambda cfg: "c5_rounds"),
 }
 

@@ -120,7 +120,9 @@ def _self_launched_bench(n, extra, timeout):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--same-device",
                         "--dist-backend", "gloo"] + extra,
                        capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    # rank 0's traceback, not the launcher's summary around it
+    tb = "\n".join(x for x in r.stderr.splitlines() if x.startswith("[rank0]"))
+    assert r.returncode == 0, (tb or r.stderr[-3000:]) + r.stdout[-2000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])

@@ -282,3 +282,23 @@ def test_lds_path_rows_switch(no_rows, monkeypatch):
                 phold.c4_config(n_hosts=50_000, V=256, end_time_s=0.2)):
         eng, orc = _run_both(cfg, max_rounds=60)
         _assert_same(eng, orc)
+
+
+@pytest.mark.parametrize("kind,grec", [("lossy", "1"), ("lossless", "1"), ("many_msgs", "1"), ("lossy", "0")])
+def test_gossip_record_path(kind, grec, monkeypatch):
+    """configs[4]'s gossip body on the record path (phase A records each first
+    receipt's forwards, phases B / C resolve them one lane per send, the
+    message id riding in the records): lossy links (phase B / C), lossless
+    links (the fused pass), more messages than the record path's seen-set
+    registers hold (the sequential body instead) and the record path off
+    (SG_GREC=0), each against the oracle with the pop traces diffed."""
+    monkeypatch.setenv("SG_GREC", grec)
+    loss = (0.0, 0.0) if kind == "lossless" else (0.005, 0.05)
+    msgs = 200 if kind == "many_msgs" else 40
+    cfg = phold.c5_config(n_hosts=4000, V=16, msgs=msgs, interval_ms=1.0, end_time_s=0.5, loss=loss)
+    eng, orc = _run_both(cfg, trace=1 << 20)
+    _assert_same(eng, orc)
+    key = ["host", "pos"]
+    assert np.array_equal(np.sort(eng.trace(), order=key), np.sort(orc.trace(), order=key))
+    if kind != "lossless":
+        assert orc.stats()["drop_reliability"] > 0

@@ -78,17 +78,20 @@ def test_inprocess_shards_match_oracle(world, kind, xcap):
         assert st[0]["exchange_steps"] > want["rounds"]
 
 
-@pytest.mark.parametrize("split,gspec", [("1", "1"), ("1", "0"), ("1", "2"), ("0", "1")])
+@pytest.mark.parametrize("split,gspec", [("1", "1"), ("1", "0"), ("1", "2"), ("2", "1"), ("0", "1")])
 def test_split_step_modes_match_oracle(split, gspec, monkeypatch):
     """The split step (k_spec inserts, refills and gathers the
     guessed bucket on a second stream beside the exchange; k_post plans from
     the headers and keeps that gather on a hit) against the oracle: with the
     guess on (hits in steady rounds), off (SG_GSPEC=0: k_post's list path every
     round), deliberately wrong (SG_GSPEC=2: k_spec gathers the bucket after the
-    right one, k_post must discard it), and the unsplit step (SG_SPLIT=0)."""
+    right one, k_post must discard it), k_spec in stream order (SG_SPLIT=2) and
+    the unsplit step (SG_SPLIT=0, the default)."""
     monkeypatch.setenv("SG_SPLIT", split)  # read when the engines are created
     monkeypatch.setenv("SG_GSPEC", gspec)
-    cfg = phold.c4_config(n_hosts=40_000, V=64, end_time_s=0.2)
+    # V = 1024 as in configs[3]: the discovered minimum is 1 ms, so steady
+    # windows are one whole bucket (V = 64 leaves 2-3 ms windows: no guess)
+    cfg = phold.c4_config(n_hosts=60_000, end_time_s=0.15)
     shards, _ = _run_shards(cfg, 4, None)
     _check(cfg, shards)
     g = [s.eng.gather_paths() for s in shards]

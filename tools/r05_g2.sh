@@ -8,7 +8,7 @@ export PYTHONUNBUFFERED=1
 O=gpurun_out/g2
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_sharded.py tests/test_gpu_gspec.py "tests/test_gpu_policy.py" tests/test_gpu_dist.py \
+  ${TESTS:-tests/test_gpu_sharded.py tests/test_gpu_gspec.py tests/test_gpu_policy.py tests/test_gpu_dist.py} \
   > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 port=29581

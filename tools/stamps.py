@@ -10,10 +10,16 @@ sys.path.insert(0, ".")
 from shadow_amd import phold  # noqa: E402
 from shadow_amd.engine import Engine  # noqa: E402
 
-cfg = phold.c4_config(n_hosts=int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000)
+# STAMPS_WL=c2 / c5: that workload (shadow_amd/workloads.py) after STAMPS_AT rounds
+wl = os.environ.get("STAMPS_WL", "c4")
+if wl == "c4":
+    cfg = phold.c4_config(n_hosts=int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000)
+else:
+    from shadow_amd import workloads
+    cfg = workloads.get(wl)["build"](None)
 eng = Engine(cfg)
 eng.boot()
-eng.run(40)
+eng.run(int(os.environ.get("STAMPS_AT", "40")))
 for r in range(3):
     eng.run(1)
     st_all = eng.stamps().astype(np.int64)
@@ -55,6 +61,16 @@ for r in range(3):
     sc = sc[sc[:, 0] > 0]
     s0 = sc[:, 0].min()
     print(f"   k_scatter: span {(sc[:, 3].max() - s0) / 100:.1f} us, WG start spread {(sc[:, 0].max() - s0) / 100:.1f} us")
+    if (sc[:, 16] > 0).all():  # entry stamps: dispatch spread, prologue (round state + plan), launch gap
+        e0 = sc[:, 16].min()
+        print(f"   k_scatter entry: spread {(sc[:, 16].max() - e0) / 100:.1f} us, prologue (entry -> start) median "
+              f"{np.median(sc[:, 0] - sc[:, 16]) / 100:.2f} max {(sc[:, 0] - sc[:, 16]).max() / 100:.2f} us; "
+              f"first entry {(e0 - st[:, 4].max()) / 100:.2f} us after k_proc's last workgroup ended")
+        for role, nm in enumerate(["insert", "received", "gather", "rmin", "refill"]):
+            x = sc[sc[:, 4] == role]
+            if len(x):
+                print(f"     {nm:<9} prologue median {np.median(x[:, 0] - x[:, 16]) / 100:5.2f} us, "
+                      f"entry median {np.median(x[:, 16] - e0) / 100:5.2f} us")
     for role, nm in enumerate(["insert", "received", "gather", "rmin", "refill"]):
         x = sc[sc[:, 4] == role]
         if not len(x):
