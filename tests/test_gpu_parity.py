@@ -295,8 +295,9 @@ def test_gossip_record_path(kind, grec, monkeypatch):
     monkeypatch.setenv("SG_GREC", grec)
     loss = (0.0, 0.0) if kind == "lossless" else (0.005, 0.05)
     msgs = 200 if kind == "many_msgs" else 40
-    cfg = phold.c5_config(n_hosts=4000, V=16, msgs=msgs, interval_ms=1.0, end_time_s=0.5, loss=loss)
-    eng, orc = _run_both(cfg, trace=1 << 20)
+    # about 2000 hosts x 8 receipts of each message pop: the trace holds them all
+    cfg = phold.c5_config(n_hosts=2000, V=16, msgs=msgs, end_time_s=0.6, loss=loss)
+    eng, orc = _run_both(cfg, trace=1 << 22)
     _assert_same(eng, orc)
     key = ["host", "pos"]
     assert np.array_equal(np.sort(eng.trace(), order=key), np.sort(orc.trace(), order=key))

@@ -93,6 +93,13 @@ for r in range(3):
           % (np.median(dur), np.percentile(dur, 90), dur.max(), np.median(st[:, 4] - t0) / 100, (st[:, 4].max() - t0) / 100))
     for nm, col in (("due", 5), ("active", 6), ("sends", 7)):
         print(f"     corr(duration, {nm}) = {np.corrcoef(dur, st[:, col])[0, 1]:.2f}")
+    # workgroup p runs on XCD p % 8 (round-robin dispatch): a slow XCD shows here
+    xcd = np.arange(len(st)) % 8
+    print("     per XCD: dur med", [round(float(np.median(dur[xcd == k])), 2) for k in range(8)],
+          " start med", [round(float(np.median(st[xcd == k, 0] - t0)) / 100, 2) for k in range(8)],
+          " due med", [int(np.median(st[xcd == k, 5])) for k in range(8)])
+    for k in range(8):
+        print(f"       XCD {k} phases med", np.round(np.median(ph[xcd == k], axis=0), 2))
     top = np.argsort(-(st[:, 4] - t0))[:6]
     for w in top:
         print("     slow WG %3d end %.2f start %.2f dur %.2f  phases %s  due/active/sends %s" % (
