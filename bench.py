@@ -103,6 +103,10 @@ def parse():
     ap.add_argument("--dist", action="store_true",
                     help="take the multi-rank step path even at N=1 (a world-1 RCCL job: "
                          "rehearses the collective path on a one-GPU box)")
+    ap.add_argument("--exchange", choices=("auto", "xgmi", "rccl"), default="auto",
+                    help="N > 1 (or --dist): the step's block exchange as xGMI peer stores into "
+                         "the peers' receive regions (sg_xlink, after a self-test on every rank) or "
+                         "the RCCL all-to-all; auto takes xgmi when its self-test passes")
     ap.add_argument("--same-device", action="store_true",
                     help="N > 1 rehearsal: every rank on GPU 0 (needs --dist-backend gloo)")
     a = ap.parse_args()

@@ -448,6 +448,38 @@ int sg_comm_destroy(sg_comm* c);
 int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, uint64_t n_steps);
 int sg_engine_set_graph(sg_engine* e, uint32_t batch);
 
+/* Native step loop over xGMI peer stores instead of a collective (the same
+ * step, the same blocks): every shard exports one region of uncached device
+ * memory (arrival counters + double-buffered receive blocks), the caller
+ * all-gathers the 128-byte handles in rank order, and each step's k_xpush
+ * copies block q of this shard's send buffer straight into shard q's region
+ * (release at system scope, then one arrival count), k_xwait waits for every
+ * sender's arrivals (bounded: 5 s, then it flags a time-out and the kernel
+ * ends) and step_recv reads the region.  Replaces the ncclAllToAll of
+ * sg_engine_run_steps (k_scatter's prologue does the wait when every shard
+ * has a device of its own; shards sharing a device wait in a one-workgroup
+ * kernel, so spinning workgroups never hold the CUs a peer needs to arrive);
+ * the MIN all-reduce of scheduler.c:386-408 /
+ * master.c:450-480 still rides in the block headers.
+ *   create   after exchange_cap is final (a later change is refused);
+ *   handle   this shard's region and device, to all-gather;
+ *   attach   the G handles in rank order (this shard's own is skipped);
+ *   selftest n_steps exchanges of a known pattern, checked on the device:
+ *            *bad = mismatched words (+ 2^63 if a wait timed out); every shard
+ *            must call it with the same n_steps;
+ *   status   synchronises the engine stream; *timed_out != 0 if a wait gave up;
+ *   destroy  after every shard stopped stepping (the caller's barrier): the
+ *            last received blocks are copied back into the engine first. */
+#define SG_XLINK_HANDLE_BYTES 128 /* the region's IPC handle + the device's PCI bus id */
+typedef struct sg_xlink sg_xlink;
+int sg_xlink_create(sg_engine* e, sg_xlink** out);
+int sg_xlink_handle(sg_xlink* x, uint8_t out[SG_XLINK_HANDLE_BYTES]);
+int sg_xlink_attach(sg_xlink* x, const uint8_t* handles);
+int sg_xlink_selftest(sg_xlink* x, uint32_t n_steps, uint64_t* bad);
+int sg_xlink_status(sg_xlink* x, uint32_t* timed_out);
+int sg_xlink_destroy(sg_xlink* x);
+int sg_engine_run_steps_xlink(sg_engine* e, sg_xlink* x, uint64_t n_steps);
+
 /* Kernel timing since sg_engine_set_timing(e, 1) (HIP events on the engine
  * stream): total ms and launches per kernel class, arrays of SG_KCLASSES. */
 enum sg_kernel_class {

@@ -107,7 +107,8 @@ EXPORTS = [
     "sg_policy_remaining", "sg_policy_ops_gpu", "sg_policy_ops_gpu_error", "sg_policy_ops_gpu_policy",
     "sg_policy_kernel_profile", "sg_policy_kernel_stats", "sg_sched_run_phold",
     "sg_sched_run_phold_paths", "sg_path_cache_create", "sg_path_cache_destroy", "sg_path_cache_lookup",
-    "sg_path_cache_stats",
+    "sg_path_cache_stats", "sg_xlink_create", "sg_xlink_handle", "sg_xlink_attach", "sg_xlink_selftest",
+    "sg_xlink_status", "sg_xlink_destroy", "sg_engine_run_steps_xlink",
 ]
 
 
@@ -178,6 +179,13 @@ def lib():
     L.sg_engine_run_steps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
     L.sg_engine_set_graph.argtypes = [C.c_void_p, C.c_uint32]
     L.sg_engine_graph_prepare.argtypes = [C.c_void_p]
+    L.sg_xlink_create.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.sg_xlink_handle.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_xlink_attach.argtypes = [C.c_void_p, C.c_void_p]
+    L.sg_xlink_selftest.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
+    L.sg_xlink_status.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
+    L.sg_xlink_destroy.argtypes = [C.c_void_p]
+    L.sg_engine_run_steps_xlink.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     _lib = L
     return L
 

@@ -22,8 +22,19 @@ ARCH = "gfx950"
 
 C_FLAGS = ["-O2", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
            "-Wextra", "-Wno-unused-parameter", "-I" + INC]
+# The kernels take their ~1 KB Dev struct by value.  clang copies a by-value
+# kernel argument into a private alloca that InstCombine folds back into
+# kernarg loads only while the copy has at most
+# instcombine-max-copied-from-constant-users users (default 300); past that the
+# whole struct lives in scratch and k_proc slows 3x (65 against 19 us per
+# 125k-host step, profiles/r05/xlink/).  The limit is raised, and the build
+# fails if a hot kernel still needs more scratch than its own spills.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
-             "-fno-fast-math", "-Wall", "-I" + INC, "-I" + CSRC]
+             "-fno-fast-math", "-Wall", "-I" + INC, "-I" + CSRC,
+             "-mllvm", "-instcombine-max-copied-from-constant-users=8000",
+             "-Rpass-analysis=kernel-resource-usage"]
+SCRATCH_MAX = 256  # bytes per lane a hot kernel may spill (k_proc: 40-72)
+HOT_KERNELS = ("k_proc", "k_scatter", "k_spec")
 
 C_SOURCES = ["sg_host.c", "sg_policy.c", "sg_sched.c", "sg_topology.c"]
 HIP_SOURCES = ["sg_engine.hip", "sg_policy_dev.hip"]
@@ -37,6 +48,20 @@ def _run(cmd, verbose):
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("build step failed: " + " ".join(cmd))
     return r
+
+
+def _scratch_check(remarks: str) -> dict:
+    """The hot kernels whose scratch per lane exceeds SCRATCH_MAX, from the
+    kernel-resource-usage remarks of one compile."""
+    bad, name = {}, None
+    for line in remarks.splitlines():
+        if "Function Name:" in line:
+            name = line.split("Function Name:")[1].split()[0]
+        elif "ScratchSize [bytes/lane]:" in line and name:
+            n = int(line.split("ScratchSize [bytes/lane]:")[1].split()[0])
+            if n > SCRATCH_MAX and any(k in name for k in HOT_KERNELS):
+                bad[name] = n
+    return bad
 
 
 def _stale(out, srcs):
@@ -71,7 +96,12 @@ def build(verbose: bool = False, force: bool = False, variant: str = "", defines
             continue
         obj = os.path.join(BUILD, src + ".o")
         if force or _stale(obj, [path] + hdrs):
-            _run([HIPCC] + HIP_FLAGS + list(defines) + ["-c", path, "-o", obj], verbose)
+            r = _run([HIPCC] + HIP_FLAGS + list(defines) + ["-c", path, "-o", obj], verbose)
+            bad = _scratch_check(r.stderr)
+            if bad:
+                os.remove(obj)
+                raise RuntimeError(f"{src}: hot kernels need scratch beyond {SCRATCH_MAX} B/lane "
+                                   f"(a by-value Dev copied to scratch?): {bad}")
         objs.append(obj)
     if force or _stale(LIB, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-lpthread"],

@@ -401,6 +401,15 @@ struct Dev {
     uint64_t* wlog;           // [wlog_cap][2] executed windows {start, end}
     uint64_t wlog_cap;
     RoundState* rs;
+    // sg_xlink: k_scatter's wave 0 waits for every sender's arrivals before it
+    // reads the received headers (null: the blocks were in place at launch)
+    const uint64_t* xwait;    // [G] arrival counters in this shard's exchange region
+    uint64_t xwait_target;
+    uint32_t* xwait_err;      // a wait that gave up (5 s) sets it, and OV_XCHG
+    // sg_xlink, fused push: k_proc stores block q straight into shard q's
+    // region (null: into xsend, for a copy or a collective after the kernel)
+    int64_t* const* xpeer;    // [G] each shard's region in this process
+    uint64_t xoff;            // int64 offset of this shard's block of this step in every region
 };
 
 // The path record of vertex pair (sv, dv).  want_jump: the discovery minimum
@@ -1976,12 +1985,27 @@ __device__ __forceinline__ uint64_t atomic_read(uint64_t* a) {
 }
 // outn / overflow are read atomically: the last k_proc workgroup reads what
 // the others' device-scope atomics performed (their L2 lines may be stale here).
+// Peer q's exchange block of this step: in xsend, or (fused xGMI push) in
+// shard q's own region.
+__device__ __forceinline__ int64_t* xblock(const Dev& d, uint32_t q) {
+    return d.xpeer ? d.xpeer[q] + d.xoff : d.xsend + (size_t)q * d.xrows * RW;
+}
+// Fused push: the blocks are complete at every peer (the caller's workgroup is
+// the last to arrive, and every workgroup waited for its stores before it
+// arrived); release at system scope, then one arrival per peer.
+__device__ __forceinline__ void xlink_signal(const Dev& d) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x < d.G)
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(d.xpeer[threadIdx.x]) + d.g, 1ull,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
     RoundState* rs = d.rs;
     if (threadIdx.x < d.G) {
         const uint32_t p = threadIdx.x;
         const uint64_t left = atomic_read(&d.outn[p]) - d.sent[p];
-        int64_t* blk = d.xsend + (size_t)p * d.xrows * RW;
+        int64_t* blk = xblock(d, p);
         blk[H_N] = (int64_t)(left < d.xcap ? left : d.xcap);
         blk[H_BASE] = (int64_t)rs->S;  // the rows' time base: the step's window start
         blk[H_MIN] = (int64_t)m;
@@ -1996,7 +2020,7 @@ __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t
             more |= (on - d.sent[q] > d.xcap) ? 1u : 0u;
             peak = q != d.g && on > peak ? on : peak;
         }
-        for (uint32_t q = 0; q < d.G; ++q) d.xsend[(size_t)q * d.xrows * RW + H_MORE] = (int64_t)more;
+        for (uint32_t q = 0; q < d.G; ++q) xblock(d, q)[H_MORE] = (int64_t)more;
         rs->peak_peer = peak;
     }
 }
@@ -2006,7 +2030,7 @@ __device__ __forceinline__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t
     for (uint32_t p = 0; p < d.G; ++p) {
         const uint64_t left = d.outn[p] - d.sent[p];
         const uint64_t n = left < d.xcap ? left : d.xcap;
-        int64_t* dst = d.xsend + ((size_t)p * d.xrows + HDR) * RW;
+        int64_t* dst = xblock(d, p) + HDR * RW;
         const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * RW;
         for (uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x; i < n * RW; i += (uint64_t)nblk * blockDim.x)
             dst[i] = src[i];
@@ -2015,6 +2039,17 @@ __device__ __forceinline__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t
         uint64_t m, j;
         reduce_local(d, s16, m, j);  // barriers inside
         write_headers(d, m, j);
+    }
+    if (d.xpeer) {  // fused push: the last workgroup to finish its copies signals the peers
+        __shared__ bool s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores performed
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd((unsigned long long*)&d.rs->ticket, 1ULL) == nblk - 1;
+        __syncthreads();
+        if (s_last) {
+            if (threadIdx.x == 0) d.rs->ticket = 0;
+            xlink_signal(d);
+        }
     }
 }
 
@@ -2247,6 +2282,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     };
     if (rsf(RSF(done))) {
         pin();
+        if (d.xpeer && p == 0) xlink_signal(d);  // the peers' k_scatter still waits for this step
         return;
     }
     const uint64_t rs_fold = rsf(RSF(fold)), rs_bS = rsf(RSF(bS));
@@ -3193,8 +3229,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t q = owner_of(d, dst);
             const uint64_t r = s_obase[q] + atomicAdd(&s_oslot[q], 1u);
             const Slot ev = d.rem[so];
-            int64_t* o = r < d.xcap ? d.xsend + ((uint64_t)q * d.xrows + HDR + r) * RW
-                                    : d.outq + ((uint64_t)q * d.oreg + r) * RW;
+            int64_t* o = r < d.xcap ? xblock(d, q) + (HDR + r) * RW : d.outq + ((uint64_t)q * d.oreg + r) * RW;
             const uint64_t rel = ev.t - S;  // new events are at or after the window's end
             if (rel >> 40) a.overflow = true;  // beyond 2^40 ns (18 min) of the window start
             o[0] = (int64_t)((rel & M40) | ((uint64_t)(dst - d.bounds[q]) << 40));
@@ -3255,7 +3290,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         // waits for another.
         __shared__ bool s_lastwg;
         __shared__ uint64_t s_mj[2];
-        if (wid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // fused push: every wave's rows are performed at the peers before the
+        // workgroup arrives (the last one signals them)
+        if (wid == 0 || d.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0)
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
@@ -3276,6 +3313,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             __syncthreads();
             write_headers(d, s_mj[0], s_mj[1]);
+            if (d.xpeer) xlink_signal(d);
         }
     }
     if (stamp && tid == 0) {
@@ -3524,9 +3562,34 @@ __device__ __forceinline__ void refill_role(const Dev& d, uint32_t nx, uint64_t 
 // reads of that state have returned; the last to arrive publishes the plan
 // (publish_step).  Nothing waits for anything: no workgroup depends on another
 // being resident, whatever the order the hardware dispatches them in.
+constexpr uint64_t XWAIT_TICKS = 500000000;  // 5 s of the 100 MHz clock: a peer that never arrives
+
+// sg_xlink: one lane per sender waits until its arrival counter reaches the
+// step's target (the peer's rows were performed before its counter moved), or
+// gives up after XWAIT_TICKS and flags the exchange.  The blocks live in
+// uncached memory, so the loads issued after the loop read what the peers
+// stored; the compiler barrier keeps them after it.
+__device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, uint64_t target, uint32_t* err,
+                                           uint64_t* ovf) {
+    const uint32_t q = threadIdx.x;
+    if (q < G) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+                atomicOr(err, 1u << (q & 31));
+                if (ovf) atomicOr((unsigned long long*)ovf, (unsigned long long)OV_XCHG);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, int mode) {
     const uint64_t t_in = d.stamps ? __builtin_amdgcn_s_memrealtime() : 0;  // SG_STAMPS: the workgroup's entry
     RoundState* rs = d.rs;
+    if (d.xwait && threadIdx.x < 64) xlink_wait(d.xwait, d.G, d.xwait_target, d.xwait_err, &rs->overflow);
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     __shared__ StepView sv;
     __shared__ uint64_t s_rsw[RSW];              // the round state as the previous kernels left it
@@ -5068,6 +5131,25 @@ static int need_sharded(sg_engine* e, const char* fn) {
     return SG_OK;
 }
 
+// Copies the last received blocks (which the next k_proc stages from) into
+// engine-owned memory, before their buffer is reallocated or unmapped.
+static int hold_last_recv(sg_engine* e) {
+    if (e->last_recv && e->last_recv != e->recv_hold) {
+        const size_t bytes = (size_t)e->d.G * e->last_rows * RW * sizeof(int64_t);
+        if (bytes > e->recv_hold_bytes) {
+            if (e->recv_hold) HIPCHK(hipFree(e->recv_hold));
+            e->recv_hold = nullptr;
+            e->recv_hold_bytes = 0;
+            HIPCHK(hipMalloc(&e->recv_hold, bytes));
+            e->recv_hold_bytes = bytes;
+        }
+        HIPCHK(hipMemcpyAsync(e->recv_hold, e->last_recv, bytes, hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->last_recv = e->recv_hold;
+    }
+    return SG_OK;
+}
+
 int sg_engine_exchange_rows(sg_engine* e, uint64_t* rows) {
     if (!e || !rows) return SG_ERR_INVAL;
     *rows = e->d.xrows;
@@ -5082,19 +5164,7 @@ int sg_engine_set_exchange_cap(sg_engine* e, uint64_t exchange_cap) {
     // the last step's received blocks are still to be staged by the next
     // k_proc, and the caller reallocates its buffers for the new cap: keep a
     // copy (in the old layout, which the next k_proc decodes)
-    if (e->last_recv && e->last_recv != e->recv_hold) {
-        const size_t bytes = (size_t)e->d.G * e->last_rows * RW * sizeof(int64_t);
-        if (bytes > e->recv_hold_bytes) {
-            if (e->recv_hold) HIPCHK(hipFree(e->recv_hold));
-            e->recv_hold = nullptr;
-            e->recv_hold_bytes = 0;
-            HIPCHK(hipMalloc(&e->recv_hold, bytes));
-            e->recv_hold_bytes = bytes;
-        }
-        HIPCHK(hipMemcpyAsync(e->recv_hold, e->last_recv, bytes, hipMemcpyDeviceToDevice, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        e->last_recv = e->recv_hold;
-    }
+    if (int rc = hold_last_recv(e)) return rc;
     e->d.xcap = exchange_cap;
     e->d.xrows = HDR + exchange_cap;
     e->gen++;
@@ -5306,6 +5376,111 @@ struct sg_comm {
     int rank, world, device;
 };
 
+// ------------------------------------------------ xGMI peer exchange ----
+// sg_xlink: the step's all-to-all as direct stores into the peers' receive
+// blocks over xGMI (hipIpc-mapped memory), with no collective.  Each rank owns
+// one region of uncached device memory, so a peer's stores and this GPU's
+// loads meet in HBM, never in a stale L2 line:
+//   [XFLAG_BYTES]         arrival counters, one u64 per sender;
+//   [2][G][xrows][RW]     receive blocks, double-buffered by step parity.
+// Step k's blocks are read by its k_scatter and by step k + 1's k_proc (the
+// events it did not route); a sender writes parity k & 1 again only in step
+// k + 2, after its k_xwait(k + 1) saw this rank's push(k + 1), which this rank
+// issues after its k_proc(k + 1).  Per step: step_send (k_proc writes the
+// blocks into the local send buffer), k_xpush (XNW workgroups per peer copy
+// the header and n rows into the peer's parity buffer, release at system
+// scope, one arrival each), k_xwait (one lane per sender waits, bounded),
+// step_recv on the parity buffer.  The MIN all-reduce of scheduler.c:386-408
+// still rides in the block headers.
+constexpr size_t XFLAG_BYTES = 4096;  // the counters' page
+
+// workgroups per destination block: 256 in all (64 at most per peer), so one
+// shard's whole block (world 1) is copied as fast as eight peers' slices
+static uint32_t xlink_nw(uint32_t G) { return std::max<uint32_t>(4, std::min<uint32_t>(64, 256 / G)); }
+
+struct XArgs {
+    int64_t* peer[MAXG];  // each shard's region in this process (this shard's own for q == g)
+    const int64_t* send;  // [G][xrows][RW]
+    uint64_t xrows;
+    uint64_t buf_off;     // int64 offset of this step's parity buffer (after the counters)
+    uint32_t G, g, nw;
+};
+
+__global__ __launch_bounds__(256) void k_xpush(XArgs a) {
+    static_assert(RW == 2, "one exchange row is 16 bytes");
+    const uint32_t XNW = a.nw, q = blockIdx.x / XNW, w = blockIdx.x % XNW;
+    const int64_t* src = a.send + (size_t)q * a.xrows * RW;
+    const uint64_t n = (uint64_t)src[H_N], cap = a.xrows - HDR;  // n <= xcap (write_headers)
+    const uint64_t rows = HDR + (n < cap ? n : cap);
+    int64_t* dst = a.peer[q] + a.buf_off + (size_t)a.g * a.xrows * RW;
+    const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
+    longlong2* d2 = reinterpret_cast<longlong2*>(dst);
+    for (uint64_t i = (uint64_t)w * blockDim.x + threadIdx.x; i < rows; i += (uint64_t)XNW * blockDim.x) d2[i] = s2[i];
+    __threadfence_system();  // the rows are performed at the peer before its counter moves
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.peer[q]) + a.g, 1ull, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The self-test's wait as a kernel of its own (k_scatter waits in its
+// prologue on real steps): the kernel always ends.
+__global__ __launch_bounds__(64) void k_xwait(const uint64_t* flags, uint32_t G, uint64_t target, uint32_t* err) {
+    xlink_wait(flags, G, target, err, nullptr);
+}
+
+// Self-test pattern: block q of sender g, row r, word c = a value only (g, q,
+// r, c, step) gives; k_xcheck counts the received words that differ.
+__device__ __forceinline__ int64_t xpattern(uint32_t g, uint32_t q, uint64_t r, uint32_t c, uint64_t step) {
+    return (int64_t)(((uint64_t)g << 56) ^ ((uint64_t)q << 48) ^ (r << 8) ^ ((uint64_t)c << 4) ^ (step * 0x9E3779B97F4A7C15ull));
+}
+__global__ void k_xfill(int64_t* send, uint64_t xrows, uint32_t G, uint32_t g, uint64_t n, uint64_t step) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)G * xrows * RW;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)(i / (xrows * RW));
+        const uint64_t r = (i / RW) % xrows;
+        const uint32_t c = (uint32_t)(i % RW);
+        send[i] = r == 0 && c == 0 ? (int64_t)n : xpattern(g, q, r, c, step);
+    }
+}
+__global__ void k_xcheck(const int64_t* recv, uint64_t xrows, uint32_t G, uint32_t g, uint64_t n, uint64_t step,
+                         unsigned long long* bad) {
+    uint32_t nb = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)G * xrows * RW;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(i / (xrows * RW));
+        const uint64_t r = (i / RW) % xrows;
+        const uint32_t c = (uint32_t)(i % RW);
+        if (r >= HDR + n) continue;
+        const int64_t want = r == 0 && c == 0 ? (int64_t)n : xpattern(s, g, r, c, step);
+        nb += recv[i] != want;
+    }
+    if (nb) atomicAdd(bad, (unsigned long long)nb);
+}
+
+struct sg_xlink {
+    sg_engine* e = nullptr;
+    uint32_t G = 0, g = 0;
+    uint64_t xrows = 0;
+    int64_t* region = nullptr;  // this shard's (uncached)
+    size_t region_bytes = 0;
+    int64_t* send = nullptr;    // [G][xrows][RW], ordinary device memory
+    int64_t* peer[MAXG] = {};
+    bool opened[MAXG] = {};
+    uint32_t* err = nullptr;    // k_xwait's timeout flags (device)
+    uint64_t steps = 0;         // steps pushed since attach
+    bool attached = false;
+    // another shard runs on this device: the arrivals are awaited by k_xwait
+    // (one workgroup), not in k_scatter's prologue, whose spinning workgroups
+    // would hold the CUs the peer's kernels need to arrive at all
+    bool shared = false;
+    // fused push (SG_XFUSE, default 1): k_proc stores the blocks into the peers'
+    // regions and its last workgroup signals them; 0: k_xpush copies x->send
+    bool fuse = true;
+    int64_t** d_peer = nullptr;  // device copy of peer[] (k_proc's xblock)
+    uint64_t expect = 0;         // arrivals every sender's counter holds once the last step is in
+};
+
 extern "C" {
 
 int sg_comm_available(void) { return rccl_open(); }
@@ -5391,6 +5566,225 @@ int sg_engine_run_steps(sg_engine* e, sg_comm* c, int64_t* send, int64_t* recv, 
         n_steps -= n;
     }
     return SG_OK;
+}
+
+static int xlink_fail(sg_xlink* x, const char* what, hipError_t err) {
+    sg_set_error("%s failed: %s", what, hipGetErrorString(err));
+    (void)sg_xlink_destroy(x);
+    return SG_ERR_HIP;
+}
+
+int sg_xlink_create(sg_engine* e, sg_xlink** out) {
+    if (!out) return SG_ERR_INVAL;
+    *out = nullptr;
+    int rc = need_sharded(e, "sg_xlink_create");
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(e->device));
+    sg_xlink* x = new sg_xlink();
+    x->e = e;
+    x->G = e->d.G;
+    x->g = e->d.g;
+    x->xrows = e->d.xrows;
+    const size_t blk = (size_t)x->G * x->xrows * RW * sizeof(int64_t);
+    x->region_bytes = XFLAG_BYTES + 2 * blk;
+    // uncached by default; SG_XLINK_MEM=1 takes fine-grained memory instead
+    const unsigned flags = env_u32z("SG_XLINK_MEM", 0) == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+    hipError_t err = hipExtMallocWithFlags((void**)&x->region, x->region_bytes, flags);
+    if (err != hipSuccess) return xlink_fail(x, "hipExtMallocWithFlags (exchange region)", err);
+    if ((err = hipMemset(x->region, 0, x->region_bytes)) != hipSuccess) return xlink_fail(x, "hipMemset", err);
+    if ((err = hipMalloc(&x->send, blk)) != hipSuccess) return xlink_fail(x, "hipMalloc (send blocks)", err);
+    if ((err = hipMalloc(&x->err, sizeof(uint32_t))) != hipSuccess) return xlink_fail(x, "hipMalloc", err);
+    if ((err = hipMemset(x->err, 0, sizeof(uint32_t))) != hipSuccess) return xlink_fail(x, "hipMemset", err);
+    if ((err = hipDeviceSynchronize()) != hipSuccess) return xlink_fail(x, "hipDeviceSynchronize", err);
+    if ((err = hipMalloc(&x->d_peer, MAXG * sizeof(int64_t*))) != hipSuccess) return xlink_fail(x, "hipMalloc", err);
+    x->peer[x->g] = x->region;
+    x->fuse = env_u32z("SG_XFUSE", 1) != 0;
+    *out = x;
+    return SG_OK;
+}
+
+// handle = the region's IPC handle, then the device's PCI bus id (ranks that
+// share a device are told apart at attach)
+constexpr size_t XBUS = SG_XLINK_HANDLE_BYTES - sizeof(hipIpcMemHandle_t);
+static_assert(XBUS >= 16, "room for a PCI bus id");
+
+int sg_xlink_handle(sg_xlink* x, uint8_t out[SG_XLINK_HANDLE_BYTES]) {
+    if (!x || !out) return SG_ERR_INVAL;
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, x->region));
+    memset(out, 0, SG_XLINK_HANDLE_BYTES);
+    memcpy(out, &h, sizeof h);
+    HIPCHK(hipDeviceGetPCIBusId((char*)out + sizeof h, (int)XBUS - 1, x->e->device));
+    return SG_OK;
+}
+
+int sg_xlink_attach(sg_xlink* x, const uint8_t* handles) {
+    if (!x || !handles) return SG_ERR_INVAL;
+    if (x->attached) {
+        sg_set_error("sg_xlink_attach: already attached");
+        return SG_ERR_STATE;
+    }
+    HIPCHK(hipSetDevice(x->e->device));
+    const uint8_t* own = handles + (size_t)x->g * SG_XLINK_HANDLE_BYTES + sizeof(hipIpcMemHandle_t);
+    for (uint32_t q = 0; q < x->G; ++q) {
+        if (q == x->g) continue;
+        const uint8_t* hq = handles + (size_t)q * SG_XLINK_HANDLE_BYTES;
+        if (memcmp(hq + sizeof(hipIpcMemHandle_t), own, XBUS) == 0) x->shared = true;
+        hipIpcMemHandle_t h;
+        memcpy(&h, hq, sizeof h);
+        void* p = nullptr;
+        const hipError_t err = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (err != hipSuccess) {
+            sg_set_error("sg_xlink_attach: hipIpcOpenMemHandle (shard %u) failed: %s", q, hipGetErrorString(err));
+            return SG_ERR_HIP;
+        }
+        x->peer[q] = (int64_t*)p;
+        x->opened[q] = true;
+    }
+    HIPCHK(hipMemcpy(x->d_peer, x->peer, MAXG * sizeof(int64_t*), hipMemcpyHostToDevice));
+    x->attached = true;
+    return SG_OK;
+}
+
+// Enqueues one push of the blocks in x->send into the peers' regions; returns
+// the receive buffer of this step's parity and the arrival count every
+// sender's counter reaches (the caller's k_scatter, or k_xwait, waits for it).
+static int xlink_push(sg_engine* e, sg_xlink* x, const int64_t** recv, uint64_t* target) {
+    XArgs a;
+    for (uint32_t q = 0; q < MAXG; ++q) a.peer[q] = q < x->G ? x->peer[q] : nullptr;
+    a.send = x->send;
+    a.xrows = x->xrows;
+    a.G = x->G;
+    a.g = x->g;
+    a.nw = xlink_nw(x->G);
+    const uint64_t k = x->steps + 1;  // this exchange's number since attach
+    a.buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
+    int rc = timed_launch(e, SG_K_EXCHANGE, [&](hipEvent_t ea, hipEvent_t eb) {
+        SG_LAUNCH(k_xpush, dim3(x->G * a.nw), dim3(256), 0, e->stream, ea, eb, a);
+    });
+    if (rc) return rc;
+    x->steps = k;
+    x->expect += a.nw;
+    *recv = x->region + a.buf_off;
+    *target = x->expect;
+    return SG_OK;
+}
+
+static int xlink_ready(sg_engine* e, sg_xlink* x, const char* fn) {
+    if (!x || !x->attached || x->e != e) {
+        sg_set_error("%s: exchange link not attached to this engine", fn);
+        return SG_ERR_STATE;
+    }
+    if (e->d.xrows != x->xrows) {
+        sg_set_error("%s: exchange_cap changed since sg_xlink_create (rows %llu, link %llu)", fn,
+                     (unsigned long long)e->d.xrows, (unsigned long long)x->xrows);
+        return SG_ERR_STATE;
+    }
+    return SG_OK;
+}
+
+int sg_engine_run_steps_xlink(sg_engine* e, sg_xlink* x, uint64_t n_steps) {
+    int rc = need_sharded(e, "sg_engine_run_steps_xlink");
+    if (rc || (rc = xlink_ready(e, x, "sg_engine_run_steps_xlink"))) return rc;
+    for (uint64_t i = 0; i < n_steps; ++i) {
+        const int64_t* recv = nullptr;
+        uint64_t target = 0;
+        if (x->fuse) {
+            // k_proc stores the blocks into the peers' regions, its last
+            // workgroup signals each peer once
+            const uint64_t k = x->steps + 1;
+            const uint64_t buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
+            e->d.xpeer = x->d_peer;
+            e->d.xoff = buf_off + (uint64_t)x->g * x->xrows * RW;
+            rc = sg_engine_step_send(e, x->send);
+            e->d.xpeer = nullptr;
+            if (rc) return rc;
+            x->steps = k;
+            x->expect += 1;
+            recv = x->region + buf_off;
+            target = x->expect;
+        } else {
+            if ((rc = sg_engine_step_send(e, x->send))) return rc;
+            if ((rc = xlink_push(e, x, &recv, &target))) return rc;
+        }
+        if (x->shared) {
+            hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, e->stream, (const uint64_t*)x->region, x->G, target,
+                               x->err);
+            HIPCHK(hipGetLastError());
+            if ((rc = sg_engine_step_recv(e, recv))) return rc;
+            continue;
+        }
+        // k_scatter's wave 0 waits for the arrivals before it reads the headers
+        e->d.xwait = (const uint64_t*)x->region;
+        e->d.xwait_target = target;
+        e->d.xwait_err = x->err;
+        rc = sg_engine_step_recv(e, recv);
+        e->d.xwait = nullptr;
+        if (rc) return rc;
+    }
+    return SG_OK;
+}
+
+int sg_xlink_selftest(sg_xlink* x, uint32_t n_steps, uint64_t* bad) {
+    if (!bad) return SG_ERR_INVAL;
+    *bad = 0;
+    int rc = xlink_ready(x ? x->e : nullptr, x, "sg_xlink_selftest");
+    if (rc) return rc;
+    sg_engine* e = x->e;
+    unsigned long long* d_bad = nullptr;
+    HIPCHK(hipMalloc(&d_bad, sizeof *d_bad));
+    HIPCHK(hipMemsetAsync(d_bad, 0, sizeof *d_bad, e->stream));
+    const uint64_t cap = x->xrows - HDR;
+    for (uint32_t i = 0; i < n_steps && rc == SG_OK; ++i) {
+        const uint64_t k = x->steps + 1;
+        const uint64_t n = (k * 2654435761ull) % (cap + 1);  // rows this step, the same on every shard
+        hipLaunchKernelGGL(k_xfill, dim3(64), dim3(256), 0, e->stream, x->send, x->xrows, x->G, x->g, n, k);
+        const int64_t* recv = nullptr;
+        uint64_t target = 0;
+        rc = xlink_push(e, x, &recv, &target);
+        if (rc == SG_OK) {
+            hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, e->stream, (const uint64_t*)x->region, x->G, target,
+                               x->err);
+            hipLaunchKernelGGL(k_xcheck, dim3(64), dim3(256), 0, e->stream, recv, x->xrows, x->G, x->g, n, k, d_bad);
+        }
+    }
+    unsigned long long h_bad = 0;
+    uint32_t h_err = 0;
+    hipError_t err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess) err = hipMemcpy(&h_bad, d_bad, sizeof h_bad, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(&h_err, x->err, sizeof h_err, hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (rc) return rc;
+    HIPCHK(err);
+    *bad = h_bad + (h_err ? (1ull << 63) : 0ull);
+    return SG_OK;
+}
+
+int sg_xlink_status(sg_xlink* x, uint32_t* timed_out) {
+    if (!x || !timed_out) return SG_ERR_INVAL;
+    HIPCHK(hipStreamSynchronize(x->e->stream));
+    HIPCHK(hipMemcpy(timed_out, x->err, sizeof *timed_out, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_xlink_destroy(sg_xlink* x) {
+    if (!x) return SG_OK;
+    int rc = SG_OK;
+    if (x->e) {
+        (void)hipStreamSynchronize(x->e->stream);
+        // the next k_proc stages from the last received blocks: keep them
+        const char* lr = (const char*)x->e->last_recv;
+        if (x->region && lr >= (const char*)x->region && lr < (const char*)x->region + x->region_bytes)
+            rc = hold_last_recv(x->e);
+    }
+    for (uint32_t q = 0; q < MAXG; ++q)
+        if (x->opened[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
+    if (x->region) (void)hipFree(x->region);
+    if (x->send) (void)hipFree(x->send);
+    if (x->err) (void)hipFree(x->err);
+    if (x->d_peer) (void)hipFree(x->d_peer);
+    delete x;
+    return rc;
 }
 
 }  // extern "C"

@@ -61,6 +61,7 @@ class EngineShard:
         self.world = world
         self.rank = rank
         self.comm = None  # the native step loop's communicator (enable_native)
+        self.xl = None    # the xGMI peer exchange (enable_xlink), preferred to comm once set
         self.eng = Engine(cfg, device=device, shard_index=rank, shard_count=world,
                           queue_cap=queue_cap, exchange_cap=exchange_cap,
                           trace_capacity=trace_capacity, stream=self.stream.cuda_stream)
@@ -129,17 +130,72 @@ class EngineShard:
         self.comm = comm
         self.eng.set_graph(graph_batch)
 
+    def enable_xlink(self, selftest_steps: int = 16):
+        """Exchange blocks by xGMI peer stores (sg_xlink) from now on: each rank
+        exports its receive region, the 128-byte handles are all-gathered,
+        every rank maps its peers', and `selftest_steps` pattern exchanges are
+        checked on every rank before the first real step.  Collective like
+        enable_native: all ranks take the link or none (RuntimeError on every
+        rank otherwise).  Call it once exchange_cap is final."""
+        from .engine import XLink
+        xl, err, h = None, None, bytes(XLink.HANDLE_BYTES)
+        try:
+            xl = XLink(self.eng)
+            h = xl.handle()
+        except Exception as exc:  # noqa: BLE001 — every rank learns it below
+            err = exc
+        if not self._all_ok(xl is not None and err is None):
+            self._drop_link(xl)
+            raise RuntimeError(f"xGMI exchange region unavailable on some rank ({err})")
+        t = torch.frombuffer(bytearray(h), dtype=torch.uint8)
+        if _backend() == "nccl":
+            t = t.to(self.dev)
+        parts = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t)
+        handles = b"".join(bytes(p.cpu().tolist()) for p in parts)
+        try:
+            xl.attach(handles)
+        except Exception as exc:  # noqa: BLE001
+            err = exc
+        if not self._all_ok(err is None):
+            self._drop_link(xl)
+            raise RuntimeError(f"mapping the peers' exchange regions failed on some rank ({err})")
+        bad = xl.selftest(selftest_steps)
+        if not self._all_ok(bad == 0):
+            self._drop_link(xl)
+            raise RuntimeError(f"xGMI exchange self-test failed on some rank (this rank: {bad:#x})")
+        self.xl = xl
+
+    def _drop_link(self, xl):
+        dist.barrier()  # no peer still stores into this rank's region
+        if xl is not None:
+            xl.close()
+
     def close_native(self):
-        """Drop the captured graphs, then the communicator (RCCL frees captured
+        """Drop the exchange link (after every rank stopped stepping), the
+        captured graphs, then the communicator (RCCL frees captured
         collectives' resources with their graph)."""
+        if getattr(self, "xl", None) is not None:
+            timed_out = self.xl.timed_out()
+            self._drop_link(self.xl)
+            self.xl = None
+            if timed_out:
+                raise RuntimeError("an xGMI exchange wait timed out (a peer never arrived)")
         if getattr(self, "comm", None) is not None:
             self.eng.set_graph(0)
             self.sync()
             self.comm.close()
             self.comm = None
 
+    @property
+    def native(self) -> bool:
+        return self.xl is not None or self.comm is not None
+
     def run_native(self, n: int):
-        self.eng.run_steps(self.comm, self.send.data_ptr(), self.recv.data_ptr(), n)
+        if self.xl is not None:
+            self.eng.run_steps_xlink(self.xl, n)
+        else:
+            self.eng.run_steps(self.comm, self.send.data_ptr(), self.recv.data_ptr(), n)
 
     def stream_ctx(self):
         return torch.cuda.stream(self.stream)
@@ -211,7 +267,7 @@ def run_step(shard, world: int):
 def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16) -> int:
     """Run steps until the simulation is done (checked every check_every steps)
     or max_steps; returns the steps run."""
-    if getattr(shard, "comm", None) is not None:
+    if getattr(shard, "native", False):
         n = 0
         while n < max_steps:
             k = min(check_every - n % check_every, max_steps - n)
@@ -335,6 +391,17 @@ def bench(args, make_shard=None):
     dist.all_reduce(peak, op=dist.ReduceOp.MAX)
     cap = -(-(int(peak.item()) * 5 // 4 + 256) // 256) * 256
     shard.set_exchange_cap(cap)
+    exch = "RCCL all-to-all" if native else f"{args.dist_backend} all-to-all"
+    want = getattr(args, "exchange", "rccl")
+    if want in ("auto", "xgmi") and hasattr(shard, "enable_xlink"):
+        try:
+            shard.enable_xlink()
+            exch = "xGMI peer stores (sg_xlink)"
+        except Exception as exc:  # the same on every rank (enable_xlink decides collectively)
+            if want == "xgmi":
+                raise
+            import sys
+            print(f"xGMI exchange unavailable ({exc}); keeping the {exch}", file=sys.stderr, flush=True)
     run(shard, world, 8, check_every=1 << 30)
     shard.sync()
     s0 = shard.stats()
@@ -415,10 +482,10 @@ def bench(args, make_shard=None):
                    "n_hosts": cfg["n_hosts"], "events_timed": total,
                    "rounds_timed": rounds_sum // world, "drain_steps": (steps_sum - rounds_sum) // world,
                    "exchange_cap": cap,
-                   "parallelism": f"hosts block-sharded {world} ways, one "
-                                  f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
-                                  "all-to-all per step",
-                   "step_loop": f"native (sg_engine_run_steps, hipGraph batch {args.graph})" if native
+                   "parallelism": f"hosts block-sharded {world} ways, one exchange per step: {exch}",
+                   "exchange": exch,
+                   "step_loop": "native (sg_engine_run_steps_xlink)" if exch.startswith("xGMI") else
+                                f"native (sg_engine_run_steps, hipGraph batch {args.graph})" if native
                                 else "python"},
         # bench.py checks these against the oracle fixture and drops them
         "_end_round": end_round, "_fingerprint": fp,
@@ -428,9 +495,10 @@ def bench(args, make_shard=None):
         res["per_rank_us_per_step"] = {
             "classes": list(KERNEL_CLASSES), "steps": kr, "rows": [r[:nk] for r in rows],
             "note": "HIP events around every launch on each rank's engine stream (they inflate "
-                    "each kernel by a few us); 'exchange' is the RCCL all-to-all: wait for the "
-                    "slowest rank + transfer (barrier idle, scheduler.c:380-389); the Python "
-                    "step loop (--py-steps, gloo) leaves it untimed"}
+                    "each kernel by a few us); 'exchange' is the step's block exchange (xGMI push "
+                    "+ arrival wait, or the RCCL all-to-all): wait for the slowest rank + transfer "
+                    "(barrier idle, scheduler.c:380-389); the Python step loop (--py-steps, gloo) "
+                    "leaves it untimed"}
         res["roofline"] = dist_roofline(rows, nk, kr, KERNEL_CLASSES)
     return res
 

@@ -244,6 +244,52 @@ class Engine:
         """n whole steps (step_send, RCCL all-to-all, step_recv) issued from C."""
         L.check(L.lib().sg_engine_run_steps(self.h, comm.h, send_ptr, recv_ptr, n))
 
+    def run_steps_xlink(self, xl: "XLink", n: int):
+        """n whole steps with the exchange as xGMI peer stores (sg_engine_run_steps_xlink)."""
+        L.check(L.lib().sg_engine_run_steps_xlink(self.h, xl.h, n))
+
+
+class XLink:
+    """The xGMI peer exchange of one shard (sg_xlink_*): this shard's region of
+    uncached device memory, exported as a 128-byte handle (IPC + device); attach() maps the
+    peers' regions (all handles in rank order, all-gathered by the caller).
+    Steps then run through Engine.run_steps_xlink: each block is stored
+    straight into its peer's region, with no collective."""
+
+    HANDLE_BYTES = 128  # IPC handle + PCI bus id (include/shadowgpu.h)
+
+    def __init__(self, eng: "Engine"):
+        h = C.c_void_p()
+        L.check(L.lib().sg_xlink_create(eng.h, C.byref(h)))
+        self.h = h
+        self.eng = eng
+
+    def handle(self) -> bytes:
+        buf = (C.c_uint8 * self.HANDLE_BYTES)()
+        L.check(L.lib().sg_xlink_handle(self.h, buf))
+        return bytes(buf)
+
+    def attach(self, handles: bytes):
+        buf = (C.c_uint8 * len(handles)).from_buffer_copy(handles)
+        L.check(L.lib().sg_xlink_attach(self.h, buf))
+
+    def selftest(self, n_steps: int) -> int:
+        """Mismatched words over n_steps pattern exchanges (+2^63 if a wait
+        timed out); every shard calls it with the same n_steps."""
+        bad = C.c_uint64()
+        L.check(L.lib().sg_xlink_selftest(self.h, n_steps, C.byref(bad)))
+        return bad.value
+
+    def timed_out(self) -> bool:
+        t = C.c_uint32()
+        L.check(L.lib().sg_xlink_status(self.h, C.byref(t)))
+        return t.value != 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            h, self.h = self.h, None
+            L.check(L.lib().sg_xlink_destroy(h))
+
 
 class Comm:
     """An RCCL communicator owned by libshadowgpu (sg_comm_create): rank 0 makes

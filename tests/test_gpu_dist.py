@@ -9,6 +9,8 @@ scheduler.c:386-398 and master.c:450-480 with the header-carried window.
   configs[3] at 1M hosts, 2 x 500k, against the oracle's per-round fixture
   configs[4] gossip, 100k hosts, the whole run, against its whole-run fixture
   bench.py --gpus 2 --same-device --dist-backend gloo: parity.match true
+The first two also run with the blocks stored straight into the peer's
+exchange region (sg_xlink), the exchange the N > 1 bench takes by default.
 """
 import json
 import os
@@ -32,7 +34,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, xcap, stop_round, q):
+def _worker(rank, world, port, kind, xcap, stop_round, q, xlink=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     sys.path.insert(0, ROOT)
@@ -45,6 +47,8 @@ def _worker(rank, world, port, kind, xcap, stop_round, q):
         cfg = phold.c4_config(n_hosts=1_000_000) if kind == "c4" else phold.c5_config()
         sh = D.EngineShard(cfg, rank, world, 0, exchange_cap=xcap)
         sh.boot()
+        if xlink:  # every step from here through the xGMI exchange regions (sg_xlink)
+            sh.enable_xlink()
         if stop_round:
             D.run_until_round(sh, world, stop_round, check_every=4)
             st = D.finish_round(sh, world)
@@ -52,6 +56,7 @@ def _worker(rank, world, port, kind, xcap, stop_round, q):
             D.run(sh, world, check_every=8)
             st = sh.stats()
         fp = sh.fingerprint()
+        sh.close_native()  # collective: raises if an exchange wait timed out
         q.put((rank, None, st, fp))
         dist.barrier()
         dist.destroy_process_group()
@@ -61,11 +66,11 @@ def _worker(rank, world, port, kind, xcap, stop_round, q):
         raise
 
 
-def _run(kind, world, xcap, stop_round=0, timeout=240):
+def _run(kind, world, xcap, stop_round=0, timeout=240, xlink=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, xcap, stop_round, q))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, xcap, stop_round, q, xlink))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -84,11 +89,14 @@ def _run(kind, world, xcap, stop_round=0, timeout=240):
 
 
 @pytest.mark.parametrize("xcap", [None, 8192])
-def test_c4_1m_two_processes(xcap):
+@pytest.mark.parametrize("xlink", [False, True], ids=["gloo", "xgmi"])
+def test_c4_1m_two_processes(xcap, xlink):
     """configs[3]: 1M hosts as 2 ranks of 500k; default blocks and 8192-row
-    blocks (drain steps); the state at the round boundary after round 24
-    against the oracle's fixture for that round."""
-    res = _run("c4", 2, xcap, stop_round=24)
+    blocks (drain steps); the blocks exchanged over gloo or stored straight
+    into the peer's exchange region (sg_xlink: IPC-mapped uncached memory,
+    arrival counters, parity buffers); the state at the round boundary after
+    round 24 against the oracle's fixture for that round."""
+    res = _run("c4", 2, xcap, stop_round=24, xlink=xlink)
     st = [r[2] for r in res]
     r = st[0]["rounds"]
     assert r >= 24 and all(x["rounds"] == r and x["phase"] == 0 for x in st)
@@ -102,8 +110,9 @@ def test_c4_1m_two_processes(xcap):
         assert st[0]["exchange_steps"] > r  # drain steps happened
 
 
-def test_c5_gossip_two_processes():
-    res = _run("c5", 2, 8192)
+@pytest.mark.parametrize("xlink", [False, True], ids=["gloo", "xgmi"])
+def test_c5_gossip_two_processes(xlink):
+    res = _run("c5", 2, 8192, xlink=xlink)
     st = [r[2] for r in res]
     fx = FIX["c5"]["stats"]
     assert all(x["overflow"] == 0 for x in st)
@@ -142,11 +151,16 @@ def _self_launched_bench(n, extra, timeout):
     return res
 
 
-def test_bench_two_ranks_self_launched():
+@pytest.mark.parametrize("exchange", ["xgmi", "rccl"])
+def test_bench_two_ranks_self_launched(exchange):
     """`python bench.py --gpus 2` with no launcher of its own (bench.py starts
-    torch.distributed.run), ranks on GPU 0 over gloo: one JSON line with the
-    two ranks' events and parity.match true."""
-    _self_launched_bench(2, ["--steps", "20", "--warmup", "10"], 300)
+    torch.distributed.run), ranks on GPU 0: one JSON line with the two ranks'
+    events and parity.match true, the timed steps exchanging blocks by xGMI
+    peer stores (sg_xlink) or, with --exchange rccl on a gloo group, by
+    gloo's all-to-all."""
+    res = _self_launched_bench(2, ["--steps", "20", "--warmup", "10", "--exchange", exchange], 300)
+    want = "xGMI" if exchange == "xgmi" else "gloo"
+    assert res["config"]["exchange"].startswith(want), res["config"]
 
 
 @pytest.mark.timeout(600)
@@ -158,6 +172,8 @@ def test_bench_eight_ranks_self_launched():
     8 per-rank roofline rows."""
     res = _self_launched_bench(8, ["--steps", "20", "--warmup", "5", "--kernel-rounds", "10"], 600)
     assert res["config"]["n_hosts"] == 1_000_000 and res["config"]["name"] == "c4"
+    # the default exchange (auto) took the xGMI link after its self-test
+    assert res["config"]["exchange"].startswith("xGMI"), res["config"]
 
 
 @pytest.mark.timeout(600)

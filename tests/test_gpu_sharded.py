@@ -116,6 +116,45 @@ def test_sharded_windows_and_trace_match_oracle():
     assert np.array_equal(np.sort(tr, order=key), np.sort(rt, order=key))
 
 
+@pytest.mark.parametrize("xcap", [4096, 7])
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_xlink_steps_world1_match_oracle(xcap, fuse, monkeypatch):
+    """sg_engine_run_steps_xlink at world 1: every block goes through k_xpush
+    into this shard's own exchange region (uncached memory, parity buffers,
+    arrival counters) and k_xwait, after a pattern self-test; a 7-row cap
+    forces drain steps.  SG_XFUSE=1 (the default): k_proc stores the blocks
+    into the region itself and its last workgroup signals; 0: k_xpush copies
+    them after it.  Half way the link is closed (the last received blocks are
+    copied back into the engine) and the run finishes on in-process block
+    copies."""
+    from shadow_amd.dist import EngineShard
+    monkeypatch.setenv("SG_XFUSE", fuse)  # read by sg_xlink_create
+    from shadow_amd.engine import XLink
+    cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
+    sh = EngineShard(cfg, 0, 1, 0, exchange_cap=xcap)
+    sh.boot()
+    xl = XLink(sh.eng)
+    xl.attach(xl.handle())  # world 1: only this shard's own region, no IPC mapping
+    assert xl.selftest(6) == 0
+    sh.xl = xl
+    n = 0
+    while not sh.done() and n < 24:
+        sh.run_native(8)
+        n += 8
+    assert not xl.timed_out()
+    xl.close()
+    sh.xl = None
+    with torch.cuda.stream(sh.stream):
+        while not sh.done():
+            send = sh.pre()
+            sh.recv.copy_(send)
+            sh.post()
+            n += 1
+            assert n < 100_000
+    sh.sync()
+    _check(cfg, [sh])
+
+
 @pytest.mark.parametrize("graph", [0, 4])
 def test_native_rccl_steps_world1_match_oracle(graph):
     """sg_engine_run_steps: step_send, RCCL all-to-all (a world-1 communicator of
