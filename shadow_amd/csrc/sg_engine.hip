@@ -410,6 +410,7 @@ struct Dev {
     // region (null: into xsend, for a copy or a collective after the kernel)
     int64_t* const* xpeer;    // [G] each shard's region in this process
     uint64_t xoff;            // int64 offset of this shard's block of this step in every region
+    uint32_t xfence;          // SG_XFENCE: a system-scope fence before each arrival
 };
 
 // The path record of vertex pair (sv, dv).  want_jump: the discovery minimum
@@ -1811,6 +1812,30 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
 // the G blocks' header words, copied into LDS with one load per lane (a chain
 // of dependent scalar loads of the round state cost about a microsecond per
 // link).  Every lane of wave 0.
+constexpr uint64_t XWAIT_TICKS = 500000000;  // 5 s of the 100 MHz clock: a peer that never arrives
+
+// sg_xlink: one lane per sender waits until its arrival counter reaches the
+// step's target (the peer's rows were performed before its counter moved), or
+// gives up after XWAIT_TICKS and flags the exchange.  The blocks live in
+// uncached memory, so the loads issued after the loop read what the peers
+// stored; the compiler barrier keeps them after it.
+__device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, uint64_t target, uint32_t* err,
+                                           uint64_t* ovf) {
+    const uint32_t q = threadIdx.x;
+    if (q < G) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+                atomicOr(err, 1u << (q & 31));
+                if (ovf) atomicOr((unsigned long long*)ovf, (unsigned long long)OV_XCHG);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void load_round_state(const Dev& d, int mode, const int64_t* recv, uint64_t* s_rsw,
                                                  int64_t* s_hdr) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1818,6 +1843,9 @@ __device__ __forceinline__ void load_round_state(const Dev& d, int mode, const i
     constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
     int64_t h[HPL];
     if (mode == 1 || mode == 3) {  // uniform
+        // sg_xlink: the peers' arrivals before their headers are read (the
+        // round-state load above is in flight meanwhile)
+        if (d.xwait) xlink_wait(d.xwait, d.G, d.xwait_target, d.xwait_err, &d.rs->overflow);
         const uint32_t nh = d.G * HDR_W;
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q) {
@@ -1994,11 +2022,16 @@ __device__ __forceinline__ int64_t* xblock(const Dev& d, uint32_t q) {
 // the last to arrive, and every workgroup waited for its stores before it
 // arrived); release at system scope, then one arrival per peer.
 __device__ __forceinline__ void xlink_signal(const Dev& d) {
-    __threadfence_system();
+    // the blocks are in uncached memory: a store is acknowledged once it is
+    // performed there, so the wave's store count reaching zero orders them
+    // before the arrival; SG_XFENCE=1 adds the full system-scope release
+    // (an L2 write-back of this XCD's dirty lines, which the blocks are not)
+    if (d.xfence) __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < d.G)
         __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(d.xpeer[threadIdx.x]) + d.g, 1ull,
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
     RoundState* rs = d.rs;
@@ -3562,34 +3595,9 @@ __device__ __forceinline__ void refill_role(const Dev& d, uint32_t nx, uint64_t 
 // reads of that state have returned; the last to arrive publishes the plan
 // (publish_step).  Nothing waits for anything: no workgroup depends on another
 // being resident, whatever the order the hardware dispatches them in.
-constexpr uint64_t XWAIT_TICKS = 500000000;  // 5 s of the 100 MHz clock: a peer that never arrives
-
-// sg_xlink: one lane per sender waits until its arrival counter reaches the
-// step's target (the peer's rows were performed before its counter moved), or
-// gives up after XWAIT_TICKS and flags the exchange.  The blocks live in
-// uncached memory, so the loads issued after the loop read what the peers
-// stored; the compiler barrier keeps them after it.
-__device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, uint64_t target, uint32_t* err,
-                                           uint64_t* ovf) {
-    const uint32_t q = threadIdx.x;
-    if (q < G) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
-                atomicOr(err, 1u << (q & 31));
-                if (ovf) atomicOr((unsigned long long*)ovf, (unsigned long long)OV_XCHG);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    asm volatile("" ::: "memory");
-}
-
 __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, int mode) {
     const uint64_t t_in = d.stamps ? __builtin_amdgcn_s_memrealtime() : 0;  // SG_STAMPS: the workgroup's entry
     RoundState* rs = d.rs;
-    if (d.xwait && threadIdx.x < 64) xlink_wait(d.xwait, d.G, d.xwait_target, d.xwait_err, &rs->overflow);
     __shared__ __align__(16) unsigned char lds[SCAT_LDS];
     __shared__ StepView sv;
     __shared__ uint64_t s_rsw[RSW];              // the round state as the previous kernels left it
@@ -4377,6 +4385,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     const uint32_t split_env = env_u32z("SG_SPLIT", 0);
     d.split = (G > 1 || p.exchange_cap) && split_env != 0 ? 1u : 0u;
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
+    d.xfence = env_u32z("SG_XFENCE", 0);
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
     // host partitions: HP hosts per k_proc workgroup, about one partition per
@@ -4389,10 +4398,12 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // 48.9-49.1 -> 44.8-46.2 us at 250k (profiles/r04/hp125k).  The floor
     // applies from 64k hosts up, so 500k gets 2048 as well (245 partitions;
     // 3907 was slower there).  It was measured on the world-1 step path; a
-    // single-shard round of 64k-500k hosts runs with it unmeasured.
+    // single-shard round of 64k-500k hosts runs with it unmeasured.  PHOLD
+    // only: configs[4]'s gossip hosts carry ~3 due events each, and 49
+    // partitions of 2048 left 200 CUs idle (k_proc 136 us per round).
     const uint32_t hp_env = env_u32("SG_HP", 0);
     uint32_t hp_auto = ((d.L + 255) / 256 + 15) / 16 * 16;
-    if (d.L > 65536 && hp_auto < 2048) hp_auto = 2048;
+    if (d.L > 65536 && hp_auto < 2048 && p.workload == SG_WORKLOAD_PHOLD) hp_auto = 2048;
     d.HP = std::min<uint32_t>(HPMAX, std::max<uint32_t>(64, hp_env ? hp_env : hp_auto));
     d.hpdiv = make_div32(d.HP);
     d.P = (d.L + d.HP - 1) / d.HP;
@@ -5403,7 +5414,7 @@ struct XArgs {
     const int64_t* send;  // [G][xrows][RW]
     uint64_t xrows;
     uint64_t buf_off;     // int64 offset of this step's parity buffer (after the counters)
-    uint32_t G, g, nw;
+    uint32_t G, g, nw, fence;
 };
 
 __global__ __launch_bounds__(256) void k_xpush(XArgs a) {
@@ -5416,10 +5427,12 @@ __global__ __launch_bounds__(256) void k_xpush(XArgs a) {
     const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
     longlong2* d2 = reinterpret_cast<longlong2*>(dst);
     for (uint64_t i = (uint64_t)w * blockDim.x + threadIdx.x; i < rows; i += (uint64_t)XNW * blockDim.x) d2[i] = s2[i];
-    __threadfence_system();  // the rows are performed at the peer before its counter moves
+    // the rows are performed at the peer (uncached memory) before its counter moves
+    if (a.fence) __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.peer[q]) + a.g, 1ull, __ATOMIC_RELEASE,
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.peer[q]) + a.g, 1ull, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -5657,6 +5670,7 @@ static int xlink_push(sg_engine* e, sg_xlink* x, const int64_t** recv, uint64_t*
     a.G = x->G;
     a.g = x->g;
     a.nw = xlink_nw(x->G);
+    a.fence = e->d.xfence;
     const uint64_t k = x->steps + 1;  // this exchange's number since attach
     a.buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
     int rc = timed_launch(e, SG_K_EXCHANGE, [&](hipEvent_t ea, hipEvent_t eb) {

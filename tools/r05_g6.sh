@@ -33,3 +33,5 @@ timeout -k 10 300 python bench.py --gpus 2 --same-device --dist-backend gloo --s
 python -c "import json;d=json.loads(open('$O/two_xgmi.log').read().strip().splitlines()[-1]);print('2 ranks same device', '%.4g'%d['value'], round(d['ms_per_step']*1e3,1), 'us/step', d['config']['exchange'], d['parity']['match'])"
 timeout -k 10 200 python tools/stamps.py > $O/stamps.txt 2>&1 || { tail $O/stamps.txt; exit 4; }
 grep -A9 "per XCD" $O/stamps.txt | head -24
+STAMPS_WL=c5 STAMPS_AT=150 timeout -k 10 200 python tools/stamps.py > $O/stamps_c5.txt 2>&1 || { tail $O/stamps_c5.txt; exit 5; }
+head -30 $O/stamps_c5.txt
