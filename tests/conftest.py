@@ -23,3 +23,15 @@ def _built():
         b.build()
     if not os.path.exists(os.path.join(ROOT, "oracle", "liborc.so")):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_device_first(request):
+    # GPU runs: torch's HIP runtime must see the device before libshadowgpu.so
+    # (ROCm 7.2's runtime) is loaded, or torch reports no device for the rest of
+    # the process (a test file that uses torch.cuda after one that only drives
+    # the library through ctypes would fail by test order alone).
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
