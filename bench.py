@@ -95,9 +95,11 @@ def parse():
                          "instead of sg_engine_run_steps")
     ap.add_argument("--kernel-rounds", type=int, default=50,
                     help="rounds after the timed region that are re-run with per-kernel HIP events")
-    ap.add_argument("--kernel-timing", choices=("after", "inline"), default=None,
-                    help="per-kernel durations from rounds after the timed region (c4's default) or "
-                         "from the timed rounds themselves (c2 / c5: their rounds change along the run)")
+    ap.add_argument("--kernel-timing", choices=("after", "replay", "inline"), default=None,
+                    help="per-kernel durations from rounds after the timed region (c4's default), from "
+                         "a second engine replaying the timed rounds (c2 / c5: their rounds change "
+                         "along the run, and the run is deterministic) or from the timed rounds "
+                         "themselves (their events then slow the timed region)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="N > 1: nccl (RCCL, the measured path) or gloo (rehearsal only)")
     ap.add_argument("--dist", action="store_true",
@@ -265,6 +267,25 @@ def run_single(args):
     del hs
     if inline:
         kr, s2, kpops = rounds, s1, pops
+    elif args.kernel_timing == "replay":
+        # the same rounds again on a second engine (the run is deterministic),
+        # every launch carrying HIP events: the timed region stays event-free
+        eng.close()
+        eng = Engine(cfg, device=0)
+        eng.boot()
+        eng.run(args.warmup, batch=args.batch)
+        r0 = eng.stats()
+        a1, _ = eng.active_hosts()
+        mv1 = eng.event_moves()
+        eng.set_timing(True)
+        eng.run(args.steps, batch=args.batch)
+        kt = eng.kernel_times()
+        eng.set_timing(False)
+        s2 = eng.stats()
+        kpops = s2["pops"] - r0["pops"]
+        kr = s2["rounds"] - r0["rounds"]
+        if kpops != pops or kr != rounds:
+            raise SystemExit(f"replay diverged: {kpops} pops in {kr} rounds against {pops} in {rounds}")
     else:
         # kernel durations: the next rounds of the same run, every launch carrying
         # HIP events as its dispatch packet's start / stop timestamps
@@ -328,6 +349,9 @@ def run_single(args):
                      "timing_method": "HIP events as each launch's dispatch-packet timestamps "
                                       "(hipExtLaunchKernelGGL), " +
                                       ("over the timed rounds themselves" if inline else
+                                       "over the timed rounds replayed on a second engine (the run is "
+                                       "deterministic; the timed region carries no events)"
+                                       if args.kernel_timing == "replay" else
                                        "rounds after the timed region") +
                                       "; the rest of ms_per_step is launch gaps"},
         "_end_round": s1["rounds"], "_fingerprint": fp,

@@ -13,8 +13,10 @@ Each entry: the config builder, a description for the bench line's
 config.workload, the default warmup / timed rounds (a window of the run where
 the rounds are busy: gossip floods peak around rounds 100-240), where the
 per-kernel durations come from (rounds after the timed region, or the timed
-rounds themselves where the rounds change along the run), and the key of its
-per-round oracle fixture in tests/golden/oracle_fixtures.json.
+rounds replayed where the rounds change along the run), and the key of its
+per-round oracle fixture in tests/golden/oracle_fixtures.json.  "replay": a
+second engine replays the timed rounds with HIP events on every launch (events
+inside the timed region itself added ~10 us of gaps per round).
 """
 from __future__ import annotations
 
@@ -40,7 +42,7 @@ WORKLOADS = {
         describe=lambda cfg: (f"PHOLD configs[1]: {cfg['n_hosts']} hosts x 16, uniform 50 ms full mesh "
                               "(one vertex), weights rule, seed 1 (50 ms windows: every event due each round)"),
         metric=lambda cfg: "committed events/sec (whole node), configs[1] 10k-host PHOLD on MI355X; bit-exact",
-        warmup=10, steps=150, cpu_warmup=12, kernel_timing="inline",
+        warmup=10, steps=150, cpu_warmup=12, kernel_timing="replay",
         fixture=lambda cfg: "c2_rounds"),
     "c5": dict(
         build=lambda hosts: phold.c5_config(),
@@ -48,7 +50,7 @@ WORKLOADS = {
                               "V=256 log-normal latency (median 40 ms, min 2 ms), edge loss 0.5-5 %, seed 1"),
         metric=lambda cfg: ("committed events/sec (whole node), configs[4] 100k-host lossy gossip on "
                             "MI355X; bit-exact"),
-        warmup=100, steps=120, cpu_warmup=100, kernel_timing="inline",
+        warmup=100, steps=120, cpu_warmup=100, kernel_timing="replay",
         fixture=lambda cfg: "c5_rounds"),
 }
 
