@@ -157,6 +157,11 @@ struct Slot {
 #ifndef SG_PMIN
 #define SG_PMIN 1
 #endif
+// SG_RS_LANES: k_scatter's planning thread reads the round state from wave
+// 0's registers (one readlane per word) instead of from its LDS copy.
+#ifndef SG_RS_LANES
+#define SG_RS_LANES 1
+#endif
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ Rec ld_stream(const Rec* p) {
 #if SG_NT & 1
@@ -1711,7 +1716,8 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
 constexpr uint32_t HDR_W = HDR * RW;  // header words per exchange block
 constexpr uint32_t RSW = sizeof(RoundState) / 8;
 static_assert(sizeof(RoundState) % 8 == 0 && RSW <= 64, "one word per lane of a wave");
-__device__ void step_view(const Dev& d, int mode, const RoundState* rs, const int64_t* hdr, StepView& sv) {
+__device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundState* rs, const int64_t* hdr,
+                                          StepView& sv) {
     const uint64_t W = d.W;
     sv.quit = rs->done != 0;
     sv.fold = rs->fold;
@@ -1721,9 +1727,10 @@ __device__ void step_view(const Dev& d, int mode, const RoundState* rs, const in
     sv.rounds0 = rs->rounds;
     const uint64_t nmj0 = rs->next_min_jump, mj0 = rs->min_jump, jmin0 = rs->jmin;
     const uint64_t tail0 = rs->fl_tail;
-    sv.nfree0 = rs->nfree2[sv.cur];
-    sv.carry0 = rs->xcarry2[sv.cur];
-    sv.rmin0 = rs->rmin2[sv.cur];
+    // (selects, not indices: a register copy of the state stays in registers)
+    sv.nfree0 = sv.cur ? rs->nfree2[1] : rs->nfree2[0];
+    sv.carry0 = sv.cur ? rs->xcarry2[1] : rs->xcarry2[0];
+    sv.rmin0 = sv.cur ? rs->rmin2[1] : rs->rmin2[0];
     sv.ins_S = rs->ins_S;
     sv.ins_local = (uint32_t)rs->ins_local;
     // the current window (kept on a drain step and at boot)
@@ -1836,8 +1843,8 @@ __device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, ui
     asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ void load_round_state(const Dev& d, int mode, const int64_t* recv, uint64_t* s_rsw,
-                                                 int64_t* s_hdr) {
+__device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, const int64_t* recv, uint64_t* s_rsw,
+                                                     int64_t* s_hdr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t v = reinterpret_cast<const uint64_t*>(d.rs)[lane < RSW ? lane : 0u];
     constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
@@ -1857,6 +1864,7 @@ __device__ __forceinline__ void load_round_state(const Dev& d, int mode, const i
             if (lane + q * 64 < nh) s_hdr[lane + q * 64] = h[q];
     }
     if (lane < RSW) s_rsw[lane] = v;
+    return v;  // the lane's word: thread 0 reads the state by readlane (SG_RS_LANES)
 }
 
 // The last workgroup to read the round state writes the plan (one thread).
@@ -3617,11 +3625,21 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
     // waited for until the workgroup's end: the last to arrive publishes then.
-    uint64_t ticket = 0;
-    if (tid < 64) load_round_state(d, mode, recv, s_rsw, s_hdr);
+    uint64_t ticket = 0, rsv = 0;
+    if (tid < 64) rsv = load_round_state(d, mode, recv, s_rsw, s_hdr);
     asm volatile("" ::: "memory");  // the copy's stores before thread 0's reads of it
     if (tid == 0) {
+#if SG_RS_LANES
+        // the round state from wave 0's registers (one readlane per word), not
+        // through a chain of LDS reads
+        RoundState rl;
+        uint64_t* rw = reinterpret_cast<uint64_t*>(&rl);
+#pragma unroll
+        for (uint32_t i = 0; i < RSW; ++i) rw[i] = readlane64(rsv, i);
+        step_view(d, mode, &rl, s_hdr, sv);
+#else
         step_view(d, mode, reinterpret_cast<const RoundState*>(s_rsw), s_hdr, sv);
+#endif
         // every read of the round state has returned (they are in LDS).  The
         // address is made opaque (divergent to the compiler): for a uniform one
         // the atomic optimizer reads the result back at once, which would wait
