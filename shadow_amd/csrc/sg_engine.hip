@@ -1717,7 +1717,7 @@ constexpr uint32_t HDR_W = HDR * RW;  // header words per exchange block
 constexpr uint32_t RSW = sizeof(RoundState) / 8;
 static_assert(sizeof(RoundState) % 8 == 0 && RSW <= 64, "one word per lane of a wave");
 __device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundState* rs, const int64_t* hdr,
-                                          StepView& sv) {
+                                          StepView& sv, uint64_t h0 = 0, bool h_lanes = false) {
     const uint64_t W = d.W;
     sv.quit = rs->done != 0;
     sv.fold = rs->fold;
@@ -1758,14 +1758,18 @@ __device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundSta
         j = jmin0 < jm ? jmin0 : jm;
     } else if (mode == 1 || mode == 3) {
         uint64_t more = 0;
+        // the header words from wave 0's registers when the G blocks' words fit
+        // one per lane (h_lanes: G <= 8), else from their LDS copy
+        auto hw = [&](uint32_t p, uint32_t f) __attribute__((always_inline)) {
+            return h_lanes ? readlane64(h0, p * HDR_W + f) : (uint64_t)hdr[(size_t)p * HDR_W + f];
+        };
         for (uint32_t p = 0; p < d.G; ++p) {
-            const int64_t* blk = hdr + (size_t)p * HDR_W;
-            more |= (uint64_t)blk[H_MORE];
-            const uint64_t bm = (uint64_t)blk[H_MIN], bj = (uint64_t)blk[H_JMIN];
+            more |= hw(p, H_MORE);
+            const uint64_t bm = hw(p, H_MIN), bj = hw(p, H_JMIN);
             m = bm < m ? bm : m;
             j = bj < j ? bj : j;
-            ovf |= (uint64_t)blk[H_OVF];
-            if ((uint64_t)blk[H_ROUND] != sv.rounds0) ovf |= OV_STEP;  // shards out of step
+            ovf |= hw(p, H_OVF);
+            if (hw(p, H_ROUND) != sv.rounds0) ovf |= OV_STEP;  // shards out of step
         }
         sv.more = more != 0;
     }
@@ -1844,7 +1848,7 @@ __device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, ui
 }
 
 __device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, const int64_t* recv, uint64_t* s_rsw,
-                                                     int64_t* s_hdr) {
+                                                     int64_t* s_hdr, uint64_t* h0 = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t v = reinterpret_cast<const uint64_t*>(d.rs)[lane < RSW ? lane : 0u];
     constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
@@ -1862,6 +1866,7 @@ __device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, con
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q)
             if (lane + q * 64 < nh) s_hdr[lane + q * 64] = h[q];
+        if (h0) *h0 = (uint64_t)h[0];
     }
     if (lane < RSW) s_rsw[lane] = v;
     return v;  // the lane's word: thread 0 reads the state by readlane (SG_RS_LANES)
@@ -3625,8 +3630,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
     // waited for until the workgroup's end: the last to arrive publishes then.
-    uint64_t ticket = 0, rsv = 0;
-    if (tid < 64) rsv = load_round_state(d, mode, recv, s_rsw, s_hdr);
+    uint64_t ticket = 0, rsv = 0, h0 = 0;
+    if (tid < 64) rsv = load_round_state(d, mode, recv, s_rsw, s_hdr, &h0);
     asm volatile("" ::: "memory");  // the copy's stores before thread 0's reads of it
     if (tid == 0) {
 #if SG_RS_LANES
@@ -3636,7 +3641,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         uint64_t* rw = reinterpret_cast<uint64_t*>(&rl);
 #pragma unroll
         for (uint32_t i = 0; i < RSW; ++i) rw[i] = readlane64(rsv, i);
-        step_view(d, mode, &rl, s_hdr, sv);
+        step_view(d, mode, &rl, s_hdr, sv, h0, d.G * HDR_W <= 64);
 #else
         step_view(d, mode, reinterpret_cast<const RoundState*>(s_rsw), s_hdr, sv);
 #endif
