@@ -2843,6 +2843,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 // then per first receipt `load` sends, each a destination draw and,
                 // when it selects a host, the reliability draw (worker.c:268-269);
                 // the message id rides in the record (bits 40-51)
+                if (st0) stamp[16] = __builtin_amdgcn_s_memrealtime();  // (the light path's slots: unused here)
                 for (uint32_t i = 0; i < cnt; ++i) {
                     const Rec ev = seg[i];
                     const uint64_t trel = ev.a & M52, bt = S + trel;
@@ -2881,6 +2882,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                                       (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
                     }
                 }
+                if (st0) stamp[17] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
                 for (uint32_t w = 0; w < GMW; ++w)
                     if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = gsw[w];
@@ -2900,6 +2902,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             } else {
                 hp->digest = c.s.digest;
             }
+            if (st0 && gossip_rec) stamp[18] = __builtin_amdgcn_s_memrealtime();
             if (st0) stamp[12] = wait_stamp();
             if (stamp && tid == 0 && q == 1) stamp[24] = wait_stamp();
         }

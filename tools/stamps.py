@@ -110,6 +110,12 @@ for r in range(3):
         print("   phase A second host (lane 0, median us): start %.2f after phase A start, reserve done +%.2f, record+store +%.2f"
               % (np.median(x[:, 23] - x[:, 1]) / 100, np.median(x[:, 25] - x[:, 23]) / 100,
                  np.median(x[:, 24] - x[:, 25]) / 100))
+    if wl == "c5":  # the gossip record path, lane 0's first host (no store waits in 16-18)
+        g = st[(st[:, 16] >= st[:, 11]) & (st[:, 17] >= st[:, 16]) & (st[:, 18] >= st[:, 17]) & (st[:, 12] >= st[:, 18])]
+        if len(g):
+            print("   gossip record path, lane 0 (median us): reserve->loop %.2f  receipts loop %.2f  seen+pads+state %.2f  "
+                  "store drain %.2f  (%d WGs)" % (np.median(g[:, 16] - g[:, 11]) / 100, np.median(g[:, 17] - g[:, 16]) / 100,
+                                                 np.median(g[:, 18] - g[:, 17]) / 100, np.median(g[:, 12] - g[:, 18]) / 100, len(g)))
     wend = (st[:, 26:30] - st[:, [1]]) / 100
     print("   phase A end per wave 0/4/8/12 (median us after phase A start):", np.round(np.median(wend, axis=0), 2),
           " barrier at %.2f" % np.median((st[:, 2] - st[:, 1]) / 100))
