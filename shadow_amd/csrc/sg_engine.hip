@@ -413,6 +413,10 @@ struct Dev {
     uint32_t* xwait_err;      // a wait that gave up (5 s) sets it, and OV_XCHG
     // sg_xlink, fused push: k_proc stores block q straight into shard q's
     // region (null: into xsend, for a copy or a collective after the kernel)
+    // flat pass: an event's earlier events in its host consumed two draws
+    // each unless one selected no host (rare; detected, that host replayed in
+    // phase A), so the LCG is skipped ahead instead of replayed
+    const uint2* skip;        // [FLAT_CMAX] {A, C}: the state after 2k draws is A * s + C (null: replay)
     int64_t* const* xpeer;    // [G] each shard's region in this process
     uint64_t xoff;            // int64 offset of this shard's block of this step in every region
     uint32_t xfence;          // SG_XFENCE: a system-scope fence before each arrival
@@ -1573,6 +1577,7 @@ __device__ __forceinline__ SegScan seg_scan(const Rec* seg, uint32_t cnt, uint64
 #define SG_FLAT_CMAX 64
 #endif
 constexpr uint32_t FLAT_CMAX = SG_FLAT_CMAX;
+constexpr uint32_t NULL_DRAW = 1u << 31;  // s_n mark: a flat-pass host whose skip-ahead miscounted
 __device__ __forceinline__ bool flat_ok(const Dev& d, uint32_t cnt, const SegScan& s, bool self_possible, uint64_t S,
                                         uint64_t E, uint32_t vh) {
     if (s.boot || cnt > FLAT_CMAX || (cnt > 1 && d.pair_fmt != PAIR_DELAY)) return false;
@@ -2650,6 +2655,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // (the flat pass is PHOLD's: its instantiations carry none of this)
     const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
                             d.mw <= GMW && d.grec;
+
     uint32_t gsw[GMW];
     auto gword = [](const uint32_t (&w)[GMW], uint32_t i) __attribute__((always_inline)) {
         uint32_t v = w[0];
@@ -2676,7 +2682,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (j < nacta) {
                 s_sb[j] = UINT32_MAX;
                 const uint32_t hl = s_act[j];
-                cnt = s_n[hl];
+                cnt = s_n[hl] & ~NULL_DRAW;
                 seg = segs + (s_c[hl] - cnt);
                 lh = sbase + hl;  // local slot
                 c.sg = d.lo + lh;
@@ -2922,10 +2928,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     __shared__ uint32_t s_nser;
     bool ser = !flat;
     if (flat) {
+        // skip-ahead pays where hosts carry several due events (configs[1]:
+        // 16 each); with about one per host (configs[3]) the barrier the
+        // null-draw check needs costs more than the few replays it saves
+        const bool use_skip = d.skip && n >= 2 * nact;  // uniform
         if (tid == 0) s_nser = 0;
         __syncthreads();
         // what stage 3 needs of an event, kept small (two are live at once)
-        enum : uint32_t { F_OK = 1, F_SND = 2, F_LAST = 4, F_MULTI = 8 };
+        enum : uint32_t { F_OK = 1, F_SND = 2, F_LAST = 4, F_MULTI = 8, F_FIRST = 16 };
         struct FlatEv {
             uint32_t hl, h, vh, rng, g, flags;
             int32_t x, ch;
@@ -2944,7 +2954,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.g = 0;
             f.vh = 0;
             if (!valid || f.hl >= HP) return f;  // past the count / flagged by the histogram
-            const uint32_t cnt = s_n[f.hl];
+            const uint32_t cnt = s_n[f.hl] & ~NULL_DRAW;  // (the skip path's mark: below)
             const uint64_t et = ev.a & M52;
             const SegScan sc = seg_scan(s_ev + (s_c[f.hl] - cnt), cnt, et, ev.k);
             f.h = (uint32_t)(w01.x >> 32);
@@ -2953,15 +2963,22 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 if (sc.rank == 0) s_act[atomicAdd(&s_nser, 1u)] = (uint16_t)f.hl;  // phase A takes it
                 return f;
             }
-            f.flags = F_OK | (sc.rank + 1 == cnt ? F_LAST : 0u) | (cnt > 1 ? F_MULTI : 0u);
+            f.flags = F_OK | (sc.rank + 1 == cnt ? F_LAST : 0u) | (cnt > 1 ? F_MULTI : 0u) |
+                      (sc.rank == 0 ? F_FIRST : 0u);
             uint32_t rng = (uint32_t)w01.x;
             const uint64_t pops0 = w01.y & M48;
             f.pops_end = pops0 + cnt;
             uint32_t before = 0;  // sends of the host's earlier events (all kept: flat_ok)
-            for (uint32_t k = 0; k < sc.rank; ++k) {
-                if (dev_rand_r(rng) <= last) {
-                    (void)dev_rand_r(rng);
-                    ++before;
+            if (use_skip) {  // two draws per earlier event, skipped in one step
+                const uint2 sk = d.skip[sc.rank];
+                rng = sk.x * rng + sk.y;
+                before = sc.rank;
+            } else {
+                for (uint32_t k = 0; k < sc.rank; ++k) {
+                    if (dev_rand_r(rng) <= last) {
+                        (void)dev_rand_r(rng);
+                        ++before;
+                    }
                 }
             }
             f.sq = w23.y + before;  // event.c:38: the counter plus the kept sends before
@@ -2989,6 +3006,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.x = dev_rand_r(rng);
             const bool snd = f.x <= last;  // test_phold.c:176-177
             f.flags |= snd ? F_SND : 0u;
+            // skip path: a draw selecting no host shifts every later event's
+            // draws by one; the host is marked (and replayed in phase A)
+            if (use_skip && !snd && sc.rank + 1 < cnt) atomicOr(&s_n[f.hl], NULL_DRAW);
             f.ch = 0;
             if (snd) f.ch = dev_rand_r(rng);  // worker.c:268-269
             f.rng = rng;
@@ -3044,8 +3064,24 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         };
         const bool stf = stamp && tid == 0;
         if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
-        const FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
-        const FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
+        FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
+        FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
+        if (use_skip) {
+            // a host whose draws the skip-ahead miscounted goes to phase A
+            // (its rank-0 lane lists it), its events here are dropped
+            lds_barrier();  // every mark is in
+            auto unflat = [&](FlatEv& f) __attribute__((always_inline)) {
+                if (!(f.flags & F_OK) || !(s_n[f.hl] & NULL_DRAW)) return;
+                --a.ctr[C_POPS];
+                if (f.flags & F_FIRST) {
+                    --a.ctr[C_ACTIVE];
+                    s_act[atomicAdd(&s_nser, 1u)] = (uint16_t)f.hl;
+                }
+                f.flags = 0;
+            };
+            unflat(f0);
+            unflat(f1);
+        }
         if (stf) stamp[17] = wait_stamp();
         // stage 2: both events' destination records in flight together
         // (unconditional loads; an unused one reads record 0's line), resolved
@@ -4653,6 +4689,33 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.sends, P * D.ECAP);
     ALLOC(D.p2min, 2 * P);
     ALLOC(D.pcum, NCTR * P);
+    {
+        // rand_r skip-ahead for the flat pass (its ranks stay below FLAT_CMAX):
+        // glibc's LCG s -> 1103515245 s + 12345 runs three steps per draw, so an
+        // event's two draws are six steps; {A, C} composes 6k of them.  An
+        // earlier event whose destination draw selects no host (x above the
+        // last weight threshold, e.g. x = RAND_MAX when the cumulative weight
+        // rounds below 1) consumed one draw, not two: k_proc detects it and
+        // sends that host to phase A's replay.  Off with a trace (the flat
+        // pass writes an event's trace record before the check).
+        D.skip = nullptr;
+        if (env_u32z("SG_SKIP", 1) && !p.trace_capacity) {
+            const uint32_t n = FLAT_CMAX;
+            std::vector<uint2> sk(n);
+            uint32_t A = 1, C = 0;
+            for (uint32_t k = 0; k < n; ++k) {
+                sk[k] = make_uint2(A, C);
+                for (int i = 0; i < 6; ++i) {  // compose one more LCG step: s -> a (A s + C) + c
+                    A = 1103515245u * A;
+                    C = 1103515245u * C + 12345u;
+                }
+            }
+            uint2* dsk = nullptr;
+            ALLOC(dsk, n);
+            HIPCHK(hipMemcpy(dsk, sk.data(), n * sizeof(uint2), hipMemcpyHostToDevice));
+            D.skip = dsk;
+        }
+    }
     if (G > 1 || p.exchange_cap) {  // step API (a single shard may use it too: exchange_cap != 0)
         ALLOC(D.remn, P);
         ALLOC(D.rem, P * D.ECAP);

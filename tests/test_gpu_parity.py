@@ -303,3 +303,25 @@ def test_gossip_record_path(kind, grec, monkeypatch):
     assert np.array_equal(np.sort(eng.trace(), order=key), np.sort(orc.trace(), order=key))
     if kind != "lossless":
         assert orc.stats()["drop_reliability"] > 0
+
+
+@pytest.mark.parametrize("skip", ["1", "0"])
+@pytest.mark.parametrize("cfg_kind", ["c2", "nulls"])
+def test_flat_skip_ahead_and_null_draws(skip, cfg_kind, monkeypatch):
+    """The flat pass skips a multi-event host's earlier draws with the LCG's
+    jump-ahead table (SG_SKIP=1) instead of replaying them (0).  A destination
+    draw above the last weight threshold selects no host and consumes one draw,
+    not two: k_proc marks such a host and replays it in phase A.  configs[1]'s
+    shape (every host 16 events a round; the skip path runs where hosts average
+    two or more) plain and with the host range cut to 80 % of RAND_MAX (a fifth
+    of the draws select no host, so nearly every host takes the fallback), no
+    trace (a trace turns the skip off), 12 rounds against the oracle."""
+    monkeypatch.setenv("SG_SKIP", skip)
+    cfg = phold.c2_config()  # the skip path runs where hosts average two or more due events
+    if cfg_kind == "nulls":
+        wt = np.asarray(cfg["weight_thresh"])
+        cfg["weight_thresh"] = np.minimum(wt, int(0.8 * 2147483647)).astype(wt.dtype)
+    eng, orc = _run_both(cfg, max_rounds=12)
+    gs = _assert_same(eng, orc)
+    if cfg_kind == "nulls":
+        assert gs["null_dst"] > 1000, gs["null_dst"]
