@@ -107,7 +107,9 @@ enum Hdr { H_N = 0, H_MORE, H_MIN, H_JMIN, H_OVF, H_ROUND, H_BASE };
 // overflow flags
 enum Ovf : uint64_t {
     OV_PROC = 1, OV_PART = 2, OV_POOL = 4, OV_XCHG = 8, OV_STEP = 16, OV_HORIZON = 32,
-    OV_BUG = 128  // internal inconsistency caught by a bounds guard
+    OV_BUG = 128,  // internal inconsistency caught by a bounds guard
+    // which gossip-skip guard tripped (with OV_BUG)
+    GSK_A = 1ull << 20, GSK_B = 1ull << 21, GSK_C = 1ull << 22, GSK_D = 1ull << 23, GSK_E = 1ull << 24
 };
 
 enum Ctr {
@@ -340,6 +342,7 @@ struct Dev {
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
     uint32_t grec;                // gossip: hosts record their forwards for phases B / C (SG_GREC, default 1)
+    uint32_t gskip_on;            // gossip: their draws after phase A from the jump-ahead table (SG_GSKIP)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
@@ -416,7 +419,8 @@ struct Dev {
     // flat pass: an event's earlier events in its host consumed two draws
     // each unless one selected no host (rare; detected, that host replayed in
     // phase A), so the LCG is skipped ahead instead of replayed
-    const uint2* skip;        // [FLAT_CMAX] {A, C}: the state after 2k draws is A * s + C (null: replay)
+    const uint2* skip;        // [nskip] {A, C}: the state after 2k draws is A * s + C (null: replay)
+    uint32_t nskip;
     int64_t* const* xpeer;    // [G] each shard's region in this process
     uint64_t xoff;            // int64 offset of this shard's block of this step in every region
     uint32_t xfence;          // SG_XFENCE: a system-scope fence before each arrival
@@ -2655,6 +2659,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // (the flat pass is PHOLD's: its instantiations carry none of this)
     const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
                             d.mw <= GMW && d.grec;
+    // lossy links (phases B and C apart): phase A leaves the record path's
+    // draws to a pass of one lane per send (send s of a host: draws 2s, 2s + 1
+    // after its state, by the jump-ahead table); a draw selecting no host
+    // marks the host, which one lane then redraws in order (skip_fix)
+    const bool gskip = gossip_rec && d.skip && d.pair_fmt != PAIR_DELAY && d.nskip > d.load * GMW * 32 &&
+                       d.gskip_on;
 
     uint32_t gsw[GMW];
     auto gword = [](const uint32_t (&w)[GMW], uint32_t i) __attribute__((always_inline)) {
@@ -2842,7 +2852,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             s_sb[j] = base;
             s_vh[j] = c.vh | (ns << 16);
-            sput(base, Rec{c.s.evc, HDR_REC | ((uint64_t)j << 32) | c.h});
+            // (gskip: the header also keeps the state before the draws, bits 32-63)
+            sput(base, Rec{c.s.evc | (gskip ? (uint64_t)c.s.rng << 32 : 0ull), HDR_REC | ((uint64_t)j << 32) | c.h});
             uint32_t k = base + 1;
             if (gossip_rec) {  // (a lane on this path with gossip took the gossip record path)
                 // the gossip body's draws (orc.c execute_gossip): trace digest,
@@ -2850,6 +2861,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 // when it selects a host, the reliability draw (worker.c:268-269);
                 // the message id rides in the record (bits 40-51)
                 if (st0) stamp[16] = __builtin_amdgcn_s_memrealtime();  // (the light path's slots: unused here)
+                const uint32_t rng0 = c.s.rng;
                 for (uint32_t i = 0; i < cnt; ++i) {
                     const Rec ev = seg[i];
                     const uint64_t trel = ev.a & M52, bt = S + trel;
@@ -2876,6 +2888,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     const uint32_t wv = gword(gsw, msg >> 5);
                     if (wv & bit) continue;  // a duplicate: the pop still commits
                     gset(gsw, msg >> 5, wv | bit);
+                    if (gskip) {  // {state before the draws, send index}: drawn after phase A
+                        for (uint32_t m = 0; m < d.load; ++m, ++k)
+                            sput(k, Rec{((uint64_t)j << 52) | ((uint64_t)msg << 40) | trel,
+                                        (uint64_t)rng0 | ((uint64_t)(k - base - 1) << 32)});
+                        a.ctr[C_SENDS] += d.load;
+                        continue;
+                    }
                     for (uint32_t m = 0; m < d.load; ++m) {
                         const int32_t x = dev_rand_r(c.s.rng);
                         if (x > last) {  // no host selected (test_phold.c:176-177)
@@ -2887,6 +2906,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                         sput(k++, Rec{((uint64_t)j << 52) | ((uint64_t)msg << 40) | trel,
                                       (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
                     }
+                }
+                if (gskip) {  // the state after every send's two draws (skip_fix redoes a null)
+                    const uint32_t si = k - base - 1;
+                    if (si >= d.nskip) flag(d, OV_BUG | GSK_A);
+                    const uint2 sk = d.skip[si < d.nskip ? si : 0u];
+                    c.s.rng = sk.x * rng0 + sk.y;
                 }
                 if (st0) stamp[17] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -3193,6 +3218,66 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 count_local(tn);
         }
     } else {
+        if (gskip) {  // uniform
+            // the gossip records' draws, one lane per send (bounds-checked:
+            // GSK_* name a guard that tripped)
+            for (uint32_t i = tid; i < nsend; i += K2_T) {
+                const Rec r = sget(i);
+                if (r.k & HDR_REC) continue;
+                const uint32_t si = (uint32_t)(r.k >> 32), jr = (uint32_t)(r.a >> 52);
+                if (si >= d.nskip || jr >= nacta) {
+                    flag(d, OV_BUG | (si >= d.nskip ? GSK_B : GSK_C));
+                    sput(i, Rec{0, HDR_REC | PAD_REC});  // nothing undrawn reaches phase B
+                    continue;
+                }
+                const uint2 sk = d.skip[si];
+                uint32_t st = sk.x * (uint32_t)r.k + sk.y;
+                const int32_t x = dev_rand_r(st);
+                if (x > last) {  // no host selected: this host's later draws shift by one
+                    atomicOr(&s_sb[jr], NULL_DRAW);
+                    continue;
+                }
+                const int32_t ch = dev_rand_r(st);  // worker.c:268-269
+                sput(i, Rec{r.a, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
+            }
+            __syncthreads();
+            // skip_fix: a marked host's sends drawn again in order (test_phold.c:
+            // 176-177: a draw selecting no host sends nothing and takes no
+            // reliability draw), real sends first, pads after, as phase A lays
+            // them out; its state after the draws rewritten
+            for (uint32_t j = tid; j < nacta; j += K2_T) {
+                const uint32_t sbm = s_sb[j];
+                if (sbm == UINT32_MAX || !(sbm & NULL_DRAW)) continue;
+                const uint32_t sb = sbm & ~NULL_DRAW, ns = s_vh[j] >> 16;
+                if (sb + ns >= nsend) {
+                    flag(d, OV_BUG | GSK_D);
+                    for (uint32_t k = sb + 1; k < nsend && k <= sb + ns; ++k) sput(k, Rec{0, HDR_REC | PAD_REC});
+                    s_sb[j] = sb;
+                    continue;
+                }
+                const Rec hd = sget(sb);
+                uint32_t st = (uint32_t)(hd.a >> 32);
+                uint32_t out = sb + 1, nulls = 0;
+                for (uint32_t k = sb + 1; k <= sb + ns; ++k) {
+                    const uint64_t ra = sget(k).a;  // read before any write at or below k
+                    const int32_t x = dev_rand_r(st);
+                    if (x > last) {
+                        ++nulls;
+                        continue;
+                    }
+                    const int32_t ch = dev_rand_r(st);
+                    sput(out++, Rec{ra, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
+                }
+                for (; out <= sb + ns; ++out) sput(out, Rec{0, HDR_REC | PAD_REC});
+                a.ctr[C_SENDS] -= nulls;
+                a.ctr[C_NULL] += nulls;
+                const uint32_t ha = s_act[j];
+                if (ha >= HP) flag(d, OV_BUG | GSK_E);
+                else reinterpret_cast<uint64_t*>(d.hs + sbase + ha)[0] = hs_w0(st, (uint32_t)hd.k);
+                s_sb[j] = sb;
+            }
+            __syncthreads();
+        }
         for (uint32_t i0 = tid; i0 < nsend; i0 += 2 * K2_T) {
             const uint32_t i1 = i0 + K2_T;
             const bool v1 = i1 < nsend;
@@ -3212,7 +3297,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 dst1 = dst_resolve(d, x1, g1, pb1, vd1);
             }
             asm volatile("" ::: "memory");  // both pair loads after both resolves (see phase A)
-            const uint32_t j0 = (uint32_t)(r0.a >> 52), j1 = (uint32_t)(r1.a >> 52);
+            // a header record's .a is its counter (gskip: and the host's state in
+            // bits 32-63): no active index, so its path lookup uses host 0's
+            const uint32_t j0 = (r0.k & HDR_REC) ? 0u : (uint32_t)(r0.a >> 52);
+            const uint32_t j1 = (r1.k & HDR_REC) ? 0u : (uint32_t)(r1.a >> 52);
             const PairRec pr0 = pair_of(s_vh[j0] & 0xFFFFu, vd0, want_jump);
             const PairRec pr1 = pair_of(s_vh[j1] & 0xFFFFu, vd1, want_jump);
             // gossip records carry the message id in bits 40-51; it moves to
@@ -3254,7 +3342,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 if (r.k & PAD_REC) continue;
                 // a host's header: its counter after all its kept sends
                 const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
-                uint64_t evc = r.a;
+                uint64_t evc = gskip ? r.a & 0xFFFFFFFFull : r.a;  // (gskip: the state above)
                 for (uint32_t k = i + 1; k <= i + ns; ++k) evc += sget(k).a >> 63;
                 d.hs[sbase + s_act[j]].evc = evc;
                 continue;
@@ -3262,7 +3350,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
             const uint32_t sb = s_sb[j];
             const Rec hd = sget(sb);
-            uint64_t evc = hd.a;  // the state's counter when phase A recorded the sends
+            uint64_t evc = gskip ? hd.a & 0xFFFFFFFFull : hd.a;  // the state's counter when phase A recorded the sends
             for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
             const bool keep = (r.a >> 63) != 0;
             if (!keep) {
@@ -4627,6 +4715,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.rec_all = env_u32z("SG_REC_ALL", 2 * K2_T);
     D.flat = env_u32z("SG_FLAT", 1) != 0 && D.workload == SG_WORKLOAD_PHOLD;
     D.grec = env_u32z("SG_GREC", 1) != 0 ? 1u : 0u;
+    D.gskip_on = env_u32z("SG_GSKIP", 1) != 0 ? 1u : 0u;
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
@@ -4700,7 +4789,10 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         // pass writes an event's trace record before the check).
         D.skip = nullptr;
         if (env_u32z("SG_SKIP", 1) && !p.trace_capacity) {
-            const uint32_t n = FLAT_CMAX;
+            // gossip's record path draws up to load x 128 sends per host (the
+            // first receipts of at most 128 messages) from the same table
+            const uint32_t n = std::max<uint32_t>(FLAT_CMAX, p.workload == SG_WORKLOAD_GOSSIP ? p.load * 128 + 1 : 0);
+            D.nskip = n;
             std::vector<uint2> sk(n);
             uint32_t A = 1, C = 0;
             for (uint32_t k = 0; k < n; ++k) {

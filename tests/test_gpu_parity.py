@@ -325,3 +325,26 @@ def test_flat_skip_ahead_and_null_draws(skip, cfg_kind, monkeypatch):
     gs = _assert_same(eng, orc)
     if cfg_kind == "nulls":
         assert gs["null_dst"] > 1000, gs["null_dst"]
+
+
+@pytest.mark.parametrize("skip", ["1", "0"])
+@pytest.mark.parametrize("cut", [False, True])
+def test_gossip_draws_after_phase_a(skip, cut, monkeypatch):
+    """configs[4]'s gossip record path on lossy links with SG_GSKIP=1: phase A
+    records each forward as {state, send index} and a pass of one lane per send
+    draws it with the jump-ahead table; a draw that selects no host marks its
+    host, whose sends one lane redraws in order (real sends first, pads after).
+    SG_GSKIP=0 draws in phase A.  The host range cut to 80 % of RAND_MAX makes a
+    fifth of the draws select no host, so the redraw runs for most hosts.  No
+    trace (a trace turns the table off); host states and counters against the
+    oracle."""
+    monkeypatch.setenv("SG_GSKIP", skip)
+    cfg = phold.c5_config(n_hosts=2000, V=16, msgs=40, end_time_s=0.6)
+    if cut:
+        wt = np.asarray(cfg["weight_thresh"])
+        cfg["weight_thresh"] = np.minimum(wt, int(0.8 * 2147483647)).astype(wt.dtype)
+    eng, orc = _run_both(cfg)
+    gs = _assert_same(eng, orc)
+    assert orc.stats()["drop_reliability"] > 0
+    if cut:
+        assert gs["null_dst"] > 1000, gs["null_dst"]
