@@ -1,0 +1,14 @@
+#!/bin/bash
+# World-1 RCCL step path at 125k hosts (one eighth of configs[3]) for several
+# partition sizes (SG_HP), each run twice.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out/hp
+port=29601
+for rep in 1 2; do
+  for hp in 0 977 1954; do
+    port=$((port+1))
+    SG_HP=$hp timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port $port \
+      bench.py --gpus 1 --dist --hosts 125000 --steps 200 --warmup 10 > gpurun_out/hp/d_${hp}_$rep.log 2>&1 || { tail -20 gpurun_out/hp/d_${hp}_$rep.log; exit 1; }
+    python -c "import json;d=json.loads(open('gpurun_out/hp/d_${hp}_$rep.log').read().strip().splitlines()[-1]);print('SG_HP=$hp', '%.4g'%d['value'], round(d['ms_per_step']*1e3,1),'us/step', [round(x,2) for x in d['per_rank_us_per_step']['rows'][0]])"
+  done
+done
