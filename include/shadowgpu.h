@@ -451,16 +451,17 @@ int sg_engine_set_graph(sg_engine* e, uint32_t batch);
 /* Native step loop over xGMI peer stores instead of a collective (the same
  * step, the same blocks): every shard exports one region of uncached device
  * memory (arrival counters + double-buffered receive blocks), the caller
- * all-gathers the 128-byte handles in rank order, and each step's k_xpush
- * copies block q of this shard's send buffer straight into shard q's region
- * (release at system scope, then one arrival count), k_xwait waits for every
- * sender's arrivals (bounded: 5 s, then it flags a time-out and the kernel
- * ends) and step_recv reads the region.  Replaces the ncclAllToAll of
- * sg_engine_run_steps (k_scatter's prologue does the wait when every shard
- * has a device of its own; shards sharing a device wait in a one-workgroup
- * kernel, so spinning workgroups never hold the CUs a peer needs to arrive);
- * the MIN all-reduce of scheduler.c:386-408 /
- * master.c:450-480 still rides in the block headers.
+ * all-gathers the 128-byte handles in rank order, and each step stores block q
+ * straight into shard q's region (k_proc itself by default, SG_XFUSE=0: a copy
+ * kernel after it), then adds one arrival to every peer's counter — after a
+ * system-scope release when the peer is on another GPU, after the stores'
+ * acknowledgements when every shard shares one device (SG_XFENCE=0/1 forces
+ * either).  The receiving k_scatter waits for every sender's arrivals before
+ * it reads their headers (bounded: 5 s, then it flags a time-out and the
+ * kernel ends); shards sharing a device wait in a one-workgroup kernel
+ * instead, so spinning workgroups never hold the CUs a peer needs to arrive.
+ * Replaces the ncclAllToAll of sg_engine_run_steps; the MIN all-reduce of
+ * scheduler.c:386-408 / master.c:450-480 still rides in the block headers.
  *   create   after exchange_cap is final (a later change is refused);
  *   handle   this shard's region and device, to all-gather;
  *   attach   the G handles in rank order (this shard's own is skipped);

@@ -4535,7 +4535,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     const uint32_t split_env = env_u32z("SG_SPLIT", 0);
     d.split = (G > 1 || p.exchange_cap) && split_env != 0 ? 1u : 0u;
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
-    d.xfence = env_u32z("SG_XFENCE", 0);
+    d.xfence = 0;  // set per exchange link (sg_xlink_attach: SG_XFENCE, else fenced across devices)
     d.check = env_u32("SG_CHECK", 0) != 0;
     d.snd_lds = env_u32("SG_SND_LDS", 1) != 0;
     // host partitions: HP hosts per k_proc workgroup, about one partition per
@@ -5668,6 +5668,12 @@ struct sg_xlink {
     // (one workgroup), not in k_scatter's prologue, whose spinning workgroups
     // would hold the CUs the peer's kernels need to arrive at all
     bool shared = false;
+    // a system-scope release before each arrival.  Between shards of one device
+    // (and at world 1) the blocks are uncached local memory and a store's
+    // acknowledgement orders it (measured: the fence costs 2.6 us per step); a
+    // peer on another GPU gets the full release, the ordering the memory model
+    // guarantees across xGMI.  SG_XFENCE=0 / 1 forces either.
+    bool fence = false;
     // fused push (SG_XFUSE, default 1): k_proc stores the blocks into the peers'
     // regions and its last workgroup signals them; 0: k_xpush copies x->send
     bool fuse = true;
@@ -5836,6 +5842,12 @@ int sg_xlink_attach(sg_xlink* x, const uint8_t* handles) {
         x->opened[q] = true;
     }
     HIPCHK(hipMemcpy(x->d_peer, x->peer, MAXG * sizeof(int64_t*), hipMemcpyHostToDevice));
+    bool remote = false;
+    for (uint32_t q = 0; q < x->G; ++q)
+        if (q != x->g && memcmp(handles + (size_t)q * SG_XLINK_HANDLE_BYTES + sizeof(hipIpcMemHandle_t), own, XBUS))
+            remote = true;
+    const char* fe = getenv("SG_XFENCE");
+    x->fence = fe && *fe ? strtol(fe, nullptr, 10) != 0 : remote;
     x->attached = true;
     return SG_OK;
 }
@@ -5851,7 +5863,7 @@ static int xlink_push(sg_engine* e, sg_xlink* x, const int64_t** recv, uint64_t*
     a.G = x->G;
     a.g = x->g;
     a.nw = xlink_nw(x->G);
-    a.fence = e->d.xfence;
+    a.fence = x->fence;
     const uint64_t k = x->steps + 1;  // this exchange's number since attach
     a.buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
     int rc = timed_launch(e, SG_K_EXCHANGE, [&](hipEvent_t ea, hipEvent_t eb) {
@@ -5891,6 +5903,7 @@ int sg_engine_run_steps_xlink(sg_engine* e, sg_xlink* x, uint64_t n_steps) {
             const uint64_t buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
             e->d.xpeer = x->d_peer;
             e->d.xoff = buf_off + (uint64_t)x->g * x->xrows * RW;
+            e->d.xfence = x->fence ? 1u : 0u;
             rc = sg_engine_step_send(e, x->send);
             e->d.xpeer = nullptr;
             if (rc) return rc;

@@ -110,6 +110,19 @@ def test_c4_1m_two_processes(xcap, xlink):
         assert st[0]["exchange_steps"] > r  # drain steps happened
 
 
+def test_c4_1m_two_processes_xgmi_fenced(monkeypatch):
+    """The xGMI exchange with the system-scope release before each arrival, as
+    it runs between GPUs (SG_XFENCE=1; ranks on one device default to the
+    unfenced arrival): configs[3] at round 24 against the fixture."""
+    monkeypatch.setenv("SG_XFENCE", "1")  # the spawned ranks inherit it
+    res = _run("c4", 2, None, stop_round=24, xlink=True)
+    st = [r[2] for r in res]
+    r = st[0]["rounds"]
+    rows = {row[0]: row for row in FIX["c4_1m"]["rounds"]}
+    assert sum(x["pops"] for x in st) == rows[r][1]
+    assert (sum(x[3] for x in res) & ((1 << 64) - 1)) == rows[r][2]
+
+
 @pytest.mark.parametrize("xlink", [False, True], ids=["gloo", "xgmi"])
 def test_c5_gossip_two_processes(xlink):
     res = _run("c5", 2, 8192, xlink=xlink)

@@ -118,17 +118,20 @@ def test_sharded_windows_and_trace_match_oracle():
 
 @pytest.mark.parametrize("xcap", [4096, 7])
 @pytest.mark.parametrize("fuse", ["1", "0"])
-def test_xlink_steps_world1_match_oracle(xcap, fuse, monkeypatch):
+@pytest.mark.parametrize("fence", ["", "1"])
+def test_xlink_steps_world1_match_oracle(xcap, fuse, fence, monkeypatch):
     """sg_engine_run_steps_xlink at world 1: every block goes through k_xpush
     into this shard's own exchange region (uncached memory, parity buffers,
     arrival counters) and k_xwait, after a pattern self-test; a 7-row cap
-    forces drain steps.  SG_XFUSE=1 (the default): k_proc stores the blocks
+    forces drain steps; with and without the system-scope release before each
+    arrival (SG_XFENCE=1; the default fences only across devices).  SG_XFUSE=1 (the default): k_proc stores the blocks
     into the region itself and its last workgroup signals; 0: k_xpush copies
     them after it.  Half way the link is closed (the last received blocks are
     copied back into the engine) and the run finishes on in-process block
     copies."""
     from shadow_amd.dist import EngineShard
     monkeypatch.setenv("SG_XFUSE", fuse)  # read by sg_xlink_create
+    monkeypatch.setenv("SG_XFENCE", fence)  # "": the default (no peer on another device: unfenced)
     from shadow_amd.engine import XLink
     cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
     sh = EngineShard(cfg, 0, 1, 0, exchange_cap=xcap)
