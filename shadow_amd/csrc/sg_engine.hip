@@ -73,14 +73,28 @@ constexpr int CH_SHIFT = 10;
 constexpr uint32_t CH = 1u << CH_SHIFT;  // events per chunk (16 KB)
 constexpr uint32_t RMAX = 4096;          // ring buckets (LDS bucket bins)
 // Bucket sub-lists: a reserving row appends to sub-list (row mod XS) of a
-// bucket, so about P / XS rows contend per counter.  XS = 1 measured fastest
-// since the reservations moved into k_proc (profiles/r02/knobs/xs_ab.log:
-// 58.3 us/round against 61.0 at XS = 2, 63.2 at XS = 4): fewer partly filled
-// chunks and due-list segments outweigh the contention.
+// bucket, so about P / XS rows contend per counter.  Round 2 measured XS = 1
+// fastest (profiles/r02/knobs/xs_ab.log: 58.3 us/round against 61.0 at XS = 2,
+// 63.2 at XS = 4).  Round 5, with the rest of the round 20 % shorter, the
+// returning adds of 256 rows on one counter (~11 ns each at the memory side)
+// were k_proc's reservation tail: XS = 2 takes k_proc 29.4 -> 27.7 us, and
+// with the GSpec guess carrying both sub-lists k_scatter stays within 0.5 us
+// (configs[3] 7.59 -> 7.87e9 events/s, profiles/r05/xs2).  XS = 4 gains
+// nothing more in k_proc and has no guess.
 #ifndef SG_XS
-#define SG_XS 1
+#define SG_XS 2
 #endif
 constexpr uint32_t XS = SG_XS;
+// Partition halves: k_scatter's workgroups that write a host partition's due
+// events (insert, gather, receive) reserve on one of PH counters of it, by
+// workgroup parity, each counter with its own CAPP / PH region of the
+// partition; k_proc reads both.  One counter per partition took up to ~640
+// returning adds a round at configs[3].
+#ifndef SG_PH
+#define SG_PH 1
+#endif
+constexpr uint32_t PH = SG_PH;
+static_assert(PH == 1 || PH == 2, "one or two partition halves");
 
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
@@ -307,11 +321,26 @@ constexpr uint32_t NSPEC = 1024;  // chunk ids kept (a million events)
 struct GSpec {
     uint64_t fold;  // the step it is for (rs->fold while that k_proc ran); UINT64_MAX: none
     uint64_t b;     // the bucket (absolute, low 48 bits) | its ring row << 48
-    uint32_t lo;    // its slots written before the step (bw[fold & 1])
-    uint32_t nid;   // chunk ids below: ceil(lo / CH)
-    uint32_t ids[NSPEC];
+    uint32_t lo;    // its slots written before the step (bw[fold & 1]); XS = 2: sub-list 0's
+    uint32_t nid;   // XS = 1: chunk ids below, ceil(lo / CH); XS = 2: sub-list 1's written slots
+    uint32_t ids[NSPEC];  // XS = 2: sub-list 0's ceil(lo / CH) chunk ids, then sub-list 1's
 };
 static_assert(offsetof(GSpec, ids) == 24, "ids follow three words");
+// The guess covers one or two sub-lists per bucket (XS > 2: no guess).
+constexpr bool GSPEC_XS = XS <= 2;
+struct GSpecLo {
+    uint32_t lo0, lo1;  // written slots of sub-lists 0 and 1
+    uint32_t nid0, nid; // chunk ids of sub-list 0, of both
+};
+__device__ __forceinline__ GSpecLo gspec_lo(uint64_t w2) {
+    if constexpr (XS == 1) {
+        return GSpecLo{(uint32_t)w2, 0u, (uint32_t)(w2 >> 32), (uint32_t)(w2 >> 32)};
+    } else {
+        const uint32_t lo0 = (uint32_t)w2, lo1 = (uint32_t)(w2 >> 32);
+        const uint32_t nid0 = (lo0 + CH - 1) >> CH_SHIFT;
+        return GSpecLo{lo0, lo1, nid0, nid0 + ((lo1 + CH - 1) >> CH_SHIFT)};
+    }
+}
 
 struct Dev {
     uint32_t N, V, L, lo, load, dst_rule, window_rule, G, g;
@@ -322,6 +351,7 @@ struct Dev {
     uint64_t gossip_start, gossip_interval;
     uint32_t* seen;           // [L][mw] per-host message bitsets
     uint32_t R, NCH, HP, P, CAPP, ECAP, G1, G3;
+    uint32_t CAPH;  // CAPP / PH: one partition half's records
     Div32 hpdiv;              // a local slot's partition: slot / HP (HP need not be a power of two)
     uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
                                               // events at, dynamic bytes
@@ -378,8 +408,8 @@ struct Dev {
     uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
     uint32_t split;           // several shards: the split step (k_spec beside the all-to-all, k_post after)
-    uint32_t* pcnt2;          // [P] the window's partition counts when k_post discarded k_spec's gather
-    uint32_t* pcnt;           // [P] due events of the partition this round
+    uint32_t* pcnt2;          // [PH][P] the window's partition counts when k_post discarded k_spec's gather
+    uint32_t* pcnt;           // [PH][P] due events of the partition (half) this round
     Rec* part;                // [P][CAPP]
     Rec* part2;               // [P][CAPP] sorted by host
     Rec* extras;              // [P][K2_T][XCAP]
@@ -797,9 +827,11 @@ __global__ void k_boot(Dev d) {
     }
     for (size_t j = i; j < (size_t)d.P * d.R; j += (size_t)gridDim.x * blockDim.x) d.pmin[j] = UINT32_MAX;
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
-    if (i < d.P) {
+    if (i < PH * d.P) {
         d.pcnt[i] = 0;
         d.pcnt2[i] = 0;
+    }
+    if (i < d.P) {
         d.rcnt[i] = 0;
         if (d.remn) d.remn[i] = 0;
         for (int c = 0; c < NCTR; ++c) d.pcum[(size_t)c * d.P + i] = 0;
@@ -865,7 +897,7 @@ constexpr int GUNR = 4;          // events in flight per thread (two-pass path)
 template <bool SCATTER, int GT>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
                                             uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
-                                            uint64_t& cmin, uint64_t& ntomb, uint64_t& ng) {
+                                            uint64_t& cmin, uint64_t& ntomb, uint64_t& ng, uint32_t hoff) {
     const uint32_t tot = nb * CH;
     for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += GT * GUNR) {
         Rec r[GUNR];
@@ -899,8 +931,8 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
             }
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPP)
-                st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
+            if (slot < d.CAPH)
+                st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
                 ++ntomb;
@@ -1046,9 +1078,10 @@ __device__ __forceinline__ void gspec_load(const Dev& d, uint32_t w, uint32_t nw
     if (k < 3) {
         s_gsw[k] = v;
     } else if (k < 3 + GSPEC_N) {
-        const uint32_t lo = (uint32_t)ln, nid = (uint32_t)(ln >> 32);
-        const bool ok = i < nid && i < NSPEC;
-        const uint32_t left = ok ? lo - i * CH : 0u;
+        const GSpecLo gl = gspec_lo(ln);
+        const bool ok = i < gl.nid && i < NSPEC;
+        // entry i: sub-list 0's chunk i, or (XS = 2) sub-list 1's chunk i - nid0
+        const uint32_t left = !ok ? 0u : i < gl.nid0 ? gl.lo0 - i * CH : gl.lo1 - (i - gl.nid0) * CH;
         s_de[k - 3] = DueEnt{ok ? (uint32_t)(v >> ((ic & 1) * 32)) : EMPTY, left < CH ? left : CH,
                              (b & ((1ull << 48) - 1)) * d.W};
     }
@@ -1076,6 +1109,9 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     // behind the tail as the entries are staged below (the next step's plan
     // advances the tail; nothing allocates before it).
     const uint32_t tail_r = sv.tail_r;
+    // this workgroup's partition half (PH): its counters and region offset
+    const uint32_t half = PH == 2 ? (w & 1u) : 0u, hoff = half * d.CAPH;
+    pc += (size_t)half * P;
     for (uint32_t p = threadIdx.x; p < P; p += GT) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
@@ -1086,7 +1122,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t c = s_cnt[p];
             if (c) {
                 const uint32_t base = atomicAdd(&pc[p], c);
-                if (base + c > d.CAPP) flag(d, OV_PART);
+                if (base + c > d.CAPH) flag(d, OV_PART);
                 s_cnt[p] = base;
             }
         }
@@ -1138,7 +1174,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, r[q].a, r[q].k);
+            if (slot < d.CAPH) st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, r[q].a, r[q].k);
             const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             if (de.nflags & RETAINED) {
@@ -1153,15 +1189,18 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     // since included: their due events were routed by the insert role) goes
     // back to the ring, entry i at tail + i, as the list path would put it.
     const uint64_t gb = s_gsw[1] & ((1ull << 48) - 1);
-    const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
+    const GSpecLo gl = gspec_lo(s_gsw[2]);
+    const uint32_t gnid = gl.nid;
     const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
-    if (gmode != GM_FALLBACK && XS == 1 && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb &&
+    if (gmode != GM_FALLBACK && GSPEC_XS && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb &&
         sv.ret == UINT64_MAX && !spent && gnid <= GSPEC_N * nw) {  // uniform
         const uint32_t row = (uint32_t)(s_gsw[1] >> 48);
-        const uint32_t hi = d.bk[row];  // in flight under the pool loads
+        // in flight under the pool loads: the sub-lists' reserved slots
+        const uint32_t hi = d.bk[row], hi1 = XS == 2 ? d.bk[d.R + row] : 0u;
         if (st) st[1] = __builtin_amdgcn_s_memrealtime();
         one_pass(GSPEC_N, [&]() __attribute__((always_inline)) {
-            const uint32_t nd = (hi + CH - 1) >> CH_SHIFT;
+            // ring order as the list path's: sub-list 0's chunks, then sub-list 1's
+            const uint32_t nd0 = (hi + CH - 1) >> CH_SHIFT, nd = nd0 + ((hi1 + CH - 1) >> CH_SHIFT);
             if (w == 0 && threadIdx.x == 0) {
                 if (gmode == GM_SPEC) {  // k_post keeps it on a hit (publish_step)
                     d.rs->spec_nfree = nd;
@@ -1175,8 +1214,12 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
                 st[7] = 1;
             }
             for (uint32_t i = w + threadIdx.x * nw; i < nd; i += GT * nw) {
-                const uint32_t id = threadIdx.x < GSPEC_N && i < gnid ? s_de[threadIdx.x].id
-                                                                     : d.btab[(size_t)row * d.NCH + i];
+                // entry i of the guess is sub-list 0's chunk i while i < nid0
+                // (s_de[k] holds entry w + k * nw); the rest from the chunk table
+                const bool x1 = XS == 2 && i >= nd0;
+                const uint32_t id = threadIdx.x < GSPEC_N && i < gl.nid0
+                                        ? s_de[threadIdx.x].id
+                                        : d.btab[((size_t)(x1 ? d.R : 0u) + row) * d.NCH + (x1 ? i - nd0 : i)];
                 // as the list path's free_chunk: an id past the pool (a slot
                 // whose reservation found the pool exhausted, OV_POOL) never
                 // enters the ring
@@ -1229,7 +1272,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             __syncthreads();
             if (threadIdx.x < nb) s_de[threadIdx.x] = due_entry(d, dl, s_start, s_lo, (uint32_t)(cb + threadIdx.x));
             __syncthreads();
-            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
+            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng, hoff);
         }
         __syncthreads();
         reserve();
@@ -1242,7 +1285,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
                 free_chunk(de, cb + threadIdx.x);
             }
             __syncthreads();
-            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
+            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng, hoff);
         }
     }
     }  // the list path
@@ -2249,18 +2292,23 @@ __device__ __forceinline__ uint64_t stage_received(const Dev& d, const int64_t* 
 // thread; the loads go out together.
 __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_t E) {
     const uint64_t b = E / d.W + (d.gspec_mode == 2 ? 1u : 0u);
-    const bool guess = XS == 1 && (b - (d.gspec_mode == 2 ? 1u : 0u)) * d.W == E && d.gspec_mode != 0;
-    const uint32_t row = (uint32_t)(b % d.R), i = threadIdx.x;
-    const uint32_t lo = d.bw[(size_t)(fold & 1) * XS * d.R + row];
-    const uint32_t id = d.btab[(size_t)row * d.NCH + (i < d.NCH ? i : 0u)];
-    const uint32_t nid = (lo + CH - 1) >> CH_SHIFT;
+    const bool guess = GSPEC_XS && (b - (d.gspec_mode == 2 ? 1u : 0u)) * d.W == E && d.gspec_mode != 0;
+    const uint32_t row = (uint32_t)(b % d.R), i = threadIdx.x, ic = i < d.NCH ? i : 0u;
+    const uint32_t* bw = d.bw + (size_t)(fold & 1) * XS * d.R;
+    const uint32_t lo = bw[row];
+    const uint32_t id = d.btab[(size_t)row * d.NCH + ic];
+    // XS = 2: sub-list 1's count and chunk i, loaded beside sub-list 0's
+    const uint32_t lo1 = XS == 2 ? bw[d.R + row] : 0u;
+    const uint32_t id1 = XS == 2 ? d.btab[((size_t)d.R + row) * d.NCH + ic] : 0u;
+    const uint32_t nid0 = (lo + CH - 1) >> CH_SHIFT, nid = nid0 + ((lo1 + CH - 1) >> CH_SHIFT);
     GSpec* g = d.gspec;
-    if (guess && i < nid && i < NSPEC) g->ids[i] = id;
+    if (guess && i < nid0 && i < NSPEC) g->ids[i] = id;
+    if (XS == 2 && guess && nid0 + i < nid && nid0 + i < NSPEC) g->ids[nid0 + i] = id1;
     if (i == 0) {
         g->fold = guess && nid <= NSPEC ? fold : UINT64_MAX;
         g->b = b | ((uint64_t)row << 48);
         g->lo = lo;
-        g->nid = nid;
+        g->nid = XS == 2 ? lo1 : nid;
     }
 }
 
@@ -2311,15 +2359,22 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint64_t rsv = reinterpret_cast<const uint64_t*>(rs)[(tid & 63) < RSW ? (tid & 63) : 0u];
     const Rec* part = d.part + (size_t)p * d.CAPP;
     // the first SPEC records per lane are loaded before the count arrives
-    // (CAPP >= SPEC * K2_T; records past the count are ignored)
+    // (CAPH >= K2_T; records past the count are ignored).  A lane's record q:
+    // PH = 1, entry tid + q * K2_T of the partition; PH = 2, slot
+    // tid + (q >> 1) * K2_T of half q & 1 (each half filled from its start)
     constexpr uint32_t SPEC = 2;
     constexpr uint32_t EPTF = FLAT ? SPEC : EPT;
+    auto rq_idx = [&](uint32_t q) __attribute__((always_inline)) {
+        return PH == 1 ? tid + q * K2_T : (q & 1u) * d.CAPH + tid + (q >> 1) * K2_T;
+    };
     Rec rr[EPTF];
 #pragma unroll
-    for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[tid + q * K2_T]);
+    for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[rq_idx(q)]);
     // the window's count: pcnt, or pcnt2 when a split step's k_post discarded
-    // k_spec's gather (rs->psel, known once the round state arrives)
+    // k_spec's gather (rs->psel, known once the round state arrives); PH = 2,
+    // per half
     const uint32_t n_a = d.pcnt[p], n_b = d.pcnt2[p];
+    const uint32_t n_a1 = PH == 2 ? d.pcnt[d.P + p] : 0u, n_b1 = PH == 2 ? d.pcnt2[d.P + p] : 0u;
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
     const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
     uint32_t v_first = 0, v_last = 0;  // ROWS: the partition's first and last slots' vertices
@@ -2333,7 +2388,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // compiler from sinking them below the branches (and so behind the wait)
     auto pin = [&]() __attribute__((always_inline)) {
         asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_a), "v"(n_b), "v"(stash_id), "v"(stash_n),
-                     "v"(v_first), "v"(v_last));
+                     "v"(v_first), "v"(v_last), "v"(n_a1), "v"(n_b1));
     };
     if (rsf(RSF(done))) {
         pin();
@@ -2408,8 +2463,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t n_raw = rsf(RSF(psel)) ? n_b : n_a;
-    const uint32_t n = n_raw < d.CAPP ? n_raw : d.CAPP;
+    const bool psel = rsf(RSF(psel)) != 0;
+    const uint32_t n0_raw = psel ? n_b : n_a, n1_raw = psel ? n_b1 : n_a1;
+    const uint32_t n0 = n0_raw < d.CAPH ? n0_raw : d.CAPH, n1 = n1_raw < d.CAPH ? n1_raw : d.CAPH;
+    const uint32_t n = n0 + n1;  // the partition's due events
+    // lane record q holds an event; entry i of the partition (0 <= i < n)
+    auto rq_ok = [&](uint32_t q) __attribute__((always_inline)) {
+        return PH == 1 ? tid + q * K2_T < n : tid + (q >> 1) * K2_T < ((q & 1u) ? n1 : n0);
+    };
+    auto pidx = [&](uint32_t i) __attribute__((always_inline)) { return PH == 1 || i < n0 ? i : d.CAPH + (i - n0); };
     // flat pass: a host's digest terms of its events but the last, summed in
     // LDS over s_vh / s_sb (phase A's arrays, free until phase A runs)
     unsigned long long* s_dig = reinterpret_cast<unsigned long long*>(s_vh);
@@ -2433,7 +2495,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (tid < MAXG) sh.peer[tid] = 0;
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
-    const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T);
+    const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T) &&
+                        (PH == 1 || (n0 <= (EPTF + 1) / 2 * K2_T && n1 <= EPTF / 2 * K2_T));
     // Flat pass (PHOLD, events in LDS, at most SPEC per lane; see below): the
     // states of the hosts of the lane's two due events are loaded as soon as
     // the records arrive.  Every lane's state reads have returned before the
@@ -2444,10 +2507,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     ulonglong2 pre_a0, pre_b0, pre_a1 = make_ulonglong2(0, 0), pre_b1 = make_ulonglong2(0, 0);
     if (in_lds) {
 #pragma unroll
-        for (uint32_t q = SPEC; q < EPTF; ++q) {
-            const uint32_t i = tid + q * K2_T;
-            rr[q] = i < n ? ld_stream(&part[i]) : Rec{0, 0};
-        }
+        for (uint32_t q = SPEC; q < EPTF; ++q) rr[q] = rq_ok(q) ? ld_stream(&part[rq_idx(q)]) : Rec{0, 0};
     }
     // the partition's hosts share a few vertices (slots are vertex-sorted):
     // their path rows (<= 32 KB: RQ words per lane) are loaded now into
@@ -2485,7 +2545,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             l1 = l1 < d.L ? l1 : d.L - 1;
             pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
             pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-            if (tid + K2_T < n) {  // most lanes have one event
+            if (rq_ok(1)) {  // most lanes have one event
                 pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
                 pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
             }
@@ -2503,7 +2563,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if (in_lds) {
 #pragma unroll
         for (uint32_t q = 0; q < EPTF; ++q) {
-            if (tid + q * K2_T >= n) continue;
+            if (!rq_ok(q)) continue;
             const uint32_t hl = (uint32_t)(rr[q].a >> 52);
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
@@ -2516,7 +2576,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             l1 = l1 < d.L ? l1 : d.L - 1;
             pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
             pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-            if (tid + K2_T < n) {  // most lanes have one event
+            if (rq_ok(1)) {  // most lanes have one event
                 pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
                 pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
             }
@@ -2531,7 +2591,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     } else {
         for (uint32_t i = tid; i < n; i += K2_T) {
-            const uint32_t hl = (uint32_t)(part[i].a >> 52);
+            const uint32_t hl = (uint32_t)(part[pidx(i)].a >> 52);
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
         }
@@ -2585,15 +2645,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
     }
-    if (tid == 0) {  // consumed; the next k_scatter's (or k_spec's / k_post's) gather refills them
-        d.pcnt[p] = 0;
-        d.pcnt2[p] = 0;
+    if (tid < PH) {  // consumed; the next k_scatter's (or k_spec's / k_post's) gather refills them
+        d.pcnt[tid * d.P + p] = 0;
+        d.pcnt2[tid * d.P + p] = 0;
     }
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
 #pragma unroll
         for (uint32_t q = 0; q < EPTF; ++q) {
-            if (tid + q * K2_T >= n) continue;
+            if (!rq_ok(q)) continue;
             const uint32_t hl = (uint32_t)(rr[q].a >> 52);
             if (hl >= HP) continue;
             const uint32_t pos = atomicAdd(&s_c[hl], 1u);
@@ -2601,7 +2661,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     } else {
         for (uint32_t i = tid; i < n; i += K2_T) {
-            const Rec r = part[i];
+            const Rec r = part[pidx(i)];
             const uint32_t hl = (uint32_t)(r.a >> 52);
             if (hl >= HP) continue;
             const uint32_t pos = atomicAdd(&s_c[hl], 1u);
@@ -3089,8 +3149,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         };
         const bool stf = stamp && tid == 0;
         if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
-        FlatEv f0 = flat_draw(rr[0], tid < n, pre_a0, pre_b0);
-        FlatEv f1 = flat_draw(rr[1], tid + K2_T < n, pre_a1, pre_b1);
+        FlatEv f0 = flat_draw(rr[0], rq_ok(0), pre_a0, pre_b0);
+        FlatEv f1 = flat_draw(rr[1], rq_ok(1), pre_a1, pre_b1);
         if (use_skip) {
             // a host whose draws the skip-ahead miscounted goes to phase A
             // (its rank-0 lane lists it), its events here are dropped
@@ -3598,12 +3658,14 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
     // The barriers order LDS only: the calendar and partition stores drain
     // while the workgroup goes on (nothing in the launch reads them back).
     lds_barrier();
+    const uint32_t half = PH == 2 ? (blockIdx.x & 1u) : 0u, hoff = half * d.CAPH;  // partition half
+    uint32_t* pc = d.pcnt + (size_t)half * d.P;
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) {
         const uint32_t c = s_pc[p];
         s_pk[p] = 0;
         if (c) {
-            const uint32_t base = atomicAdd(&d.pcnt[p], c);
-            if (base + c > d.CAPP) flag(d, OV_PART);
+            const uint32_t base = atomicAdd(&pc[p], c);
+            if (base + c > d.CAPH) flag(d, OV_PART);
             s_pc[p] = base;
         }
     }
@@ -3613,8 +3675,8 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (!due[q]) continue;
         const uint32_t p = part_of(d, dl[q]);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPP)
-            st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
+        if (slot < d.CAPH)
+            st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
     }
     lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
@@ -3993,7 +4055,9 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // per (workgroup, partition)); the next k_proc stages the rest
     // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
-    uint32_t* pc = split && !sv.hit ? d.pcnt2 : d.pcnt;  // where this window's counts are
+    const uint32_t half = PH == 2 ? (w & 1u) : 0u, hoff = half * d.CAPH;  // partition half
+    // where this window's counts are
+    uint32_t* pc = (split && !sv.hit ? d.pcnt2 : d.pcnt) + (size_t)half * d.P;
     if (tid == 0) s_routed = 0;
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         s_pc[p] = 0;
@@ -4013,7 +4077,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         const uint32_t c = s_pc[p];
         if (c) {
             const uint32_t base = atomicAdd(&pc[p], c);
-            if (base + c > d.CAPP) flag(d, OV_PART);
+            if (base + c > d.CAPH) flag(d, OV_PART);
             s_pc[p] = base;
             atomicAdd(&s_routed, c);
         }
@@ -4027,7 +4091,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (!recv_event(d, recv, d.xrows, s_off, s_rbase, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
         const uint32_t p = part_of(d, dl);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
+        if (slot < d.CAPH) st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
     }
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
@@ -4104,8 +4168,8 @@ __global__ __launch_bounds__(K3_T) void k_spec(Dev d) {
         J = J > 0 ? J : 10 * SG_ONE_MS;
         if (d.runahead_min > 0 && J < d.runahead_min) J = d.runahead_min;
     }
-    const uint32_t gnid = (uint32_t)(s_gsw[2] >> 32);
-    const bool guess = XS == 1 && s_gsw[0] == fold && r->phase == 0 && J == W && gnid <= GSPEC_N * G1;
+    const uint32_t gnid = gspec_lo(s_gsw[2]).nid;
+    const bool guess = GSPEC_XS && s_gsw[0] == fold && r->phase == 0 && J == W && gnid <= GSPEC_N * G1;
     if (tid == 0) {
         const uint32_t cur = (uint32_t)(fold & 1);
         sv.S = gb * W;
@@ -4227,7 +4291,7 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
     }
     if (listed) {
         const uint32_t* pc = rs->psel ? d.pcnt2 : d.pcnt;
-        for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += pc[p];
+        for (uint32_t p = threadIdx.x; p < PH * d.P; p += 1024) pend += pc[p];
     }
     for (int i = 0; i < NCTR; ++i) {
         const uint64_t t = block_sum(c[i], s16);
@@ -4643,6 +4707,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     const uint32_t per_host = std::max<uint32_t>(32, 2 * d.load);
     d.CAPP = d.HP * per_host;
+    d.CAPH = d.CAPP / PH;  // HP is a multiple of 16: CAPP divides; CAPH >= 1024 = K2_T
     d.ECAP = d.HP * per_host + 1024;
 
     sg_engine* e = new sg_engine();
@@ -4768,8 +4833,8 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.stn, D.P + D.G3);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.gspec, 1);
-    ALLOC(D.pcnt, P);
-    ALLOC(D.pcnt2, P);
+    ALLOC(D.pcnt, PH * P);
+    ALLOC(D.pcnt2, PH * P);
     ALLOC(D.part, P * D.CAPP);
     ALLOC(D.part2, P * D.CAPP);
     ALLOC(D.extras, P * K2_T * XCAP);
@@ -4985,7 +5050,8 @@ int sg_engine_boot(sg_engine* e) {
     HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
     HIPCHK(hipMemsetAsync(d.gspec, 0xFF, sizeof(GSpec), e->stream));  // no guess (fold UINT64_MAX)
-    const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH), std::max<uint32_t>(d.R, d.P + d.G3));
+    const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH),
+                                          std::max<uint32_t>(d.R, std::max<uint32_t>(d.P + d.G3, PH * d.P)));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
     HIPCHK(hipGetLastError());
     // the first window's gather (k_scatter's gather role; nothing is staged
