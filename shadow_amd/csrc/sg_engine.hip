@@ -405,6 +405,7 @@ struct Dev {
     uint32_t* stn;            // [P + G3] ids in the row's stash
     uint32_t* wbase;          // [P + G3][R] reserved base per (row, bucket) in the row's sub-list
     GSpec* gspec;             // the next gather's guessed due list (k_proc -> k_scatter)
+    uint64_t* tick;           // [8] k_scatter's plan arrivals per workgroup shard blk & 7 (SG_TICK8)
     uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
     uint32_t split;           // several shards: the split step (k_spec beside the all-to-all, k_post after)
@@ -827,6 +828,7 @@ __global__ void k_boot(Dev d) {
     }
     for (size_t j = i; j < (size_t)d.P * d.R; j += (size_t)gridDim.x * blockDim.x) d.pmin[j] = UINT32_MAX;
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
+    if (i < 8) d.tick[i] = 0;
     if (i < PH * d.P) {
         d.pcnt[i] = 0;
         d.pcnt2[i] = 0;
@@ -2343,6 +2345,18 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_FLAT_LDSB
 #define SG_FLAT_LDSB 1
 #endif
+// SG_PART_LATE: k_proc's partials and MIN atomics after its reservations (1)
+// or before them (0, default): 1 measured k_proc +1.0 us (profiles/r05/tick).
+#ifndef SG_PART_LATE
+#define SG_PART_LATE 0
+#endif
+// SG_TICK8: k_scatter's plan arrival in two levels, one counter per workgroup
+// shard blockIdx & 7 and then the plan counter (1, default), or every
+// workgroup on the plan counter (0): k_scatter 17.6 -> 17.1 us, configs[3]
+// 7.68 -> 7.80e9 events/s (profiles/r05/tick).
+#ifndef SG_TICK8
+#define SG_TICK8 1
+#endif
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
@@ -3488,21 +3502,27 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     lds_barrier();  // s_red
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     // wave 0: the partials and the MIN accumulators (the last workgroup reads
-    // them), issued before the reservations
-    if (tid < NPCTR + 2) {
-        const int i = tid;
-        uint64_t r = s_red[0][i];
-        for (int w = 1; w < K2_T / 64; ++w) {
-            const uint64_t x = s_red[w][i];
-            r = i < NPCTR ? r + x : (x < r ? x : r);
+    // them).  SG_PART_LATE: issued after the reservations, so that wave 0's
+    // returning reservation adds do not queue (vmcnt is in order) behind the
+    // MIN atomics every workgroup sends to the same two words
+    auto partials = [&]() __attribute__((always_inline)) {
+        if (tid < NPCTR + 2) {
+            const int i = tid;
+            uint64_t r = s_red[0][i];
+            for (int w = 1; w < K2_T / 64; ++w) {
+                const uint64_t x = s_red[w][i];
+                r = i < NPCTR ? r + x : (x < r ? x : r);
+            }
+            // the workgroup's own slot: an atomic add needs no load (wave 0 joins
+            // the reservations' barrier without waiting for one)
+            if (i < NPCTR) atomicAdd((unsigned long long*)&d.pcum[(size_t)i * d.P + p], (unsigned long long)r);
+            else d.p2min[(size_t)(i - NPCTR) * d.P + p] = r;
+            if (i >= NPCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NPCTR], (unsigned long long)r);
         }
-        // the workgroup's own slot: an atomic add needs no load (wave 0 joins
-        // the reservations' barrier without waiting for one)
-        if (i < NPCTR) atomicAdd((unsigned long long*)&d.pcum[(size_t)i * d.P + p], (unsigned long long)r);
-        else d.p2min[(size_t)(i - NPCTR) * d.P + p] = r;
-        if (i >= NPCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NPCTR], (unsigned long long)r);
-    }
+    };
+    if (!SG_PART_LATE) partials();
     reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
+    if (SG_PART_LATE) partials();
     if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
@@ -4098,7 +4118,20 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
 #if SG_LATE_TICKET
     if (tid == 0) {
         const uint32_t z = opaque(tid) - tid;  // 0
+#if SG_TICK8
+        // two levels (SG_TICK8): the workgroups of shard blk & 7 arrive on its
+        // own counter, the last of each on the plan counter; the last of those
+        // publishes.  Each counter takes <= 49 adds instead of one taking 386.
+        const uint32_t k = blockIdx.x & 7u, nsh = gridDim.x < 8 ? gridDim.x : 8u;
+        const uint64_t in_k = (gridDim.x - k + 7) / 8;  // workgroups b < gridDim.x with b & 7 == k
+        ticket = 0;
+        if (atomicAdd((unsigned long long*)&d.tick[k] + z, 1ull) == in_k - 1) {
+            atomicExch((unsigned long long*)&d.tick[k], 0ull);  // every arrival of the shard is in
+            if (atomicAdd((unsigned long long*)&rs->splan + z, 1ull) == nsh - 1) ticket = gridDim.x - 1;
+        }
+#else
         ticket = atomicAdd((unsigned long long*)&rs->splan + z, 1ull);
+#endif
     }
 #endif
     if (tid == 0 && ticket == gridDim.x - 1) publish_step(d, mode, sv, recv);
@@ -4833,6 +4866,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.stn, D.P + D.G3);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.gspec, 1);
+    ALLOC(D.tick, 8);
     ALLOC(D.pcnt, PH * P);
     ALLOC(D.pcnt2, PH * P);
     ALLOC(D.part, P * D.CAPP);
