@@ -42,9 +42,7 @@ from shadow_amd.roofline import HBM_PEAK_GBS, kernel_line, proc_bytes, scatter_b
 # FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = {"c4": os.path.join(ROOT, "profiles", "r05", "bench", "pmc.json"),
-            "c2": os.path.join(ROOT, "profiles", "r05", "workloads", "c2", "pmc.json"),
-            "c5": os.path.join(ROOT, "profiles", "r05", "workloads", "c5", "pmc.json")}
+PMC_JSON = {w: os.path.join(ROOT, "profiles", "r05", "final3", f"prof_{w}", "pmc.json") for w in ("c4", "c2", "c5")}
 DOMINANT = "k_proc"
 
 
