@@ -405,7 +405,7 @@ struct Dev {
     uint32_t* stn;            // [P + G3] ids in the row's stash
     uint32_t* wbase;          // [P + G3][R] reserved base per (row, bucket) in the row's sub-list
     GSpec* gspec;             // the next gather's guessed due list (k_proc -> k_scatter)
-    uint64_t* tick;           // [2][8] arrivals per workgroup shard blockIdx & 7 (SG_TICK8): k_scatter's plan, k_proc's headers
+    uint64_t* tick;           // [8] k_scatter's plan arrivals per workgroup shard blockIdx & 7 (SG_TICK8)
     uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
     uint32_t split;           // several shards: the split step (k_spec beside the all-to-all, k_post after)
@@ -828,7 +828,7 @@ __global__ void k_boot(Dev d) {
     }
     for (size_t j = i; j < (size_t)d.P * d.R; j += (size_t)gridDim.x * blockDim.x) d.pmin[j] = UINT32_MAX;
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
-    if (i < 16) d.tick[i] = 0;
+    if (i < 8) d.tick[i] = 0;
     if (i < PH * d.P) {
         d.pcnt[i] = 0;
         d.pcnt2[i] = 0;
@@ -2357,10 +2357,6 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_TICK8
 #define SG_TICK8 1
 #endif
-// SG_PTICK8: several shards, k_proc's header ticket in two levels as well
-#ifndef SG_PTICK8
-#define SG_PTICK8 0
-#endif
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
@@ -3551,23 +3547,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         // workgroup arrives (the last one signals them)
         if (wid == 0 || d.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
-#if SG_PTICK8
-            // two levels, as k_scatter's plan arrival: shard blockIdx & 7 first,
-            // the last of each on the ticket (every add is device-scope, so the
-            // last arrival still follows every workgroup's)
-            const uint32_t k = blockIdx.x & 7u, nsh = gridDim.x < 8 ? gridDim.x : 8u;
-            const uint64_t in_k = (gridDim.x - k + 7) / 8;
-            bool last = false;
-            if (atomicAdd((unsigned long long*)&d.tick[8 + k], 1ULL) == in_k - 1) {
-                atomicExch((unsigned long long*)&d.tick[8 + k], 0ULL);
-                last = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == nsh - 1;
-            }
-            s_lastwg = last;
-#else
+        // (a two-level ticket here, as k_scatter's plan arrival, hung the
+        // two-process xGMI test: profiles/r05/ptick8)
+        if (tid == 0)
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
-#endif
-        }
         __syncthreads();
         if (s_lastwg) {
             if (tid == 0) {
@@ -4885,7 +4868,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.stn, D.P + D.G3);
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.gspec, 1);
-    ALLOC(D.tick, 16);
+    ALLOC(D.tick, 8);
     ALLOC(D.pcnt, PH * P);
     ALLOC(D.pcnt2, PH * P);
     ALLOC(D.part, P * D.CAPP);
