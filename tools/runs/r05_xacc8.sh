@@ -1,9 +1,9 @@
 #!/bin/bash
-# k_proc's MIN accumulators in eight copies (SG_XACC8): parity subset on the
+# k_proc MIN accumulators in eight copies (SG_XACC8): parity subset on the
 # variant, then configs[3] interleaved with the default build.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-out=gpurun_out/xacc8; mkdir -p $out
+out=gpurun_out/xacc8b; mkdir -p $out
 SG_LIB=libshadowgpu_xacc8.so timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
   tests/test_gpu_gspec.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_sharded.py > $out/pytest.log 2>&1
 rc=$?; tail -2 $out/pytest.log; [ $rc = 0 ] || exit $rc
