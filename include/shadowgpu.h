@@ -453,31 +453,52 @@ int sg_engine_set_graph(sg_engine* e, uint32_t batch);
  * memory (arrival counters + double-buffered receive blocks), the caller
  * all-gathers the 128-byte handles in rank order, and each step stores block q
  * straight into shard q's region (k_proc itself by default, SG_XFUSE=0: a copy
- * kernel after it), then adds one arrival to every peer's counter — after a
- * system-scope release when the peer is on another GPU, after the stores'
- * acknowledgements when every shard shares one device (SG_XFENCE=0/1 forces
- * either).  The receiving k_scatter waits for every sender's arrivals before
- * it reads their headers (bounded: 5 s, then it flags a time-out and the
- * kernel ends); shards sharing a device wait in a one-workgroup kernel
- * instead, so spinning workgroups never hold the CUs a peer needs to arrive.
+ * kernel after it): every storing workgroup waits for its stores — and, when a
+ * peer is on another GPU, issues a system-scope release — before it takes a
+ * ticket, and the last one adds one arrival to every peer's counter
+ * (SG_XFENCE=0/1 forces the release off or on).  The receiving k_scatter
+ * waits for every sender's arrivals before it reads their headers (bounded:
+ * 5 s, then it flags a time-out, the run stops at the next plan, and every
+ * later wait of the link returns at once); shards sharing a device wait in a
+ * one-workgroup kernel instead, so spinning workgroups never hold the CUs a
+ * peer needs to arrive.
  * Replaces the ncclAllToAll of sg_engine_run_steps; the MIN all-reduce of
  * scheduler.c:386-408 / master.c:450-480 still rides in the block headers.
  *   create   after exchange_cap is final (a later change is refused);
  *   handle   this shard's region and device, to all-gather;
  *   attach   the G handles in rank order (this shard's own is skipped);
- *   selftest n_steps exchanges of a known pattern, checked on the device:
+ *   selftest n_steps exchanges of a known pattern through the path the steps
+ *            take (the fused push: many storing workgroups, release, ticket,
+ *            the last one's headers and arrivals), checked on the device:
  *            *bad = mismatched words (+ 2^63 if a wait timed out); every shard
  *            must call it with the same n_steps;
- *   status   synchronises the engine stream; *timed_out != 0 if a wait gave up;
+ *   status   synchronises the engine stream; *timed_out = the senders whose
+ *            arrival a wait gave up on (bit q: shard q), 0 if none;
+ *   info     how the link runs (fenced, fused, shared device) and the last
+ *            self-test's result;
  *   destroy  after every shard stopped stepping (the caller's barrier): the
- *            last received blocks are copied back into the engine first. */
+ *            last received blocks are copied back into the engine first.
+ *   debug_withhold (tests only): the fused step `step` steps from now does not
+ *            arrive at shard `peer`, whose wait then times out. */
 #define SG_XLINK_HANDLE_BYTES 128 /* the region's IPC handle + the device's PCI bus id */
 typedef struct sg_xlink sg_xlink;
+typedef struct sg_xlink_desc {
+    uint32_t fenced;          /* a system-scope release by every storing workgroup */
+    uint32_t fused;           /* k_proc stores the blocks itself (else k_xpush copies them) */
+    uint32_t shared_device;   /* a peer shares this GPU: the arrivals are awaited by k_xwait */
+    uint32_t selftest_steps;  /* the last self-test's exchanges */
+    uint32_t selftest_fused;  /* ... through the fused push */
+    uint32_t pad_;
+    uint64_t selftest_bad;    /* ... its mismatched words (+ 2^63: a wait timed out) */
+    uint64_t steps;           /* exchanges since attach (self-test included) */
+} sg_xlink_desc;
 int sg_xlink_create(sg_engine* e, sg_xlink** out);
 int sg_xlink_handle(sg_xlink* x, uint8_t out[SG_XLINK_HANDLE_BYTES]);
 int sg_xlink_attach(sg_xlink* x, const uint8_t* handles);
 int sg_xlink_selftest(sg_xlink* x, uint32_t n_steps, uint64_t* bad);
 int sg_xlink_status(sg_xlink* x, uint32_t* timed_out);
+int sg_xlink_info(sg_xlink* x, sg_xlink_desc* out);
+int sg_xlink_debug_withhold(sg_xlink* x, uint64_t step, uint32_t peer);
 int sg_xlink_destroy(sg_xlink* x);
 int sg_engine_run_steps_xlink(sg_engine* e, sg_xlink* x, uint64_t n_steps);
 

@@ -85,6 +85,15 @@ class WindowState(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("min_jump", "next_min_jump", "min_jump_config", "end_time")]
 
 
+class XLinkDesc(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("fenced", "fused", "shared_device", "selftest_steps",
+                                          "selftest_fused", "pad_")] + \
+               [("selftest_bad", C.c_uint64), ("steps", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_ if n != "pad_"}
+
+
 TRACE_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"),
                         ("pos", "<u8")])
 
@@ -108,7 +117,8 @@ EXPORTS = [
     "sg_policy_kernel_profile", "sg_policy_kernel_stats", "sg_sched_run_phold",
     "sg_sched_run_phold_paths", "sg_path_cache_create", "sg_path_cache_destroy", "sg_path_cache_lookup",
     "sg_path_cache_stats", "sg_xlink_create", "sg_xlink_handle", "sg_xlink_attach", "sg_xlink_selftest",
-    "sg_xlink_status", "sg_xlink_destroy", "sg_engine_run_steps_xlink",
+    "sg_xlink_status", "sg_xlink_info", "sg_xlink_debug_withhold", "sg_xlink_destroy",
+    "sg_engine_run_steps_xlink",
 ]
 
 
@@ -184,6 +194,8 @@ def lib():
     L.sg_xlink_attach.argtypes = [C.c_void_p, C.c_void_p]
     L.sg_xlink_selftest.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]
     L.sg_xlink_status.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
+    L.sg_xlink_info.argtypes = [C.c_void_p, C.POINTER(XLinkDesc)]
+    L.sg_xlink_debug_withhold.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
     L.sg_xlink_destroy.argtypes = [C.c_void_p]
     L.sg_engine_run_steps_xlink.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     _lib = L

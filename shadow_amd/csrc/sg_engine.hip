@@ -454,7 +454,8 @@ struct Dev {
     uint32_t nskip;
     int64_t* const* xpeer;    // [G] each shard's region in this process
     uint64_t xoff;            // int64 offset of this shard's block of this step in every region
-    uint32_t xfence;          // SG_XFENCE: a system-scope fence before each arrival
+    uint32_t xfence;          // SG_XFENCE: the peer-region stores system-coherent (sc0 sc1, xst)
+    uint32_t xskip;           // test only (sg_xlink_debug_withhold): peer + 1 whose arrival this step withholds
 };
 
 // The path record of vertex pair (sv, dv).  want_jump: the discovery minimum
@@ -1884,12 +1885,20 @@ constexpr uint64_t XWAIT_TICKS = 500000000;  // 5 s of the 100 MHz clock: a peer
 // gives up after XWAIT_TICKS and flags the exchange.  The blocks live in
 // uncached memory, so the loads issued after the loop read what the peers
 // stored; the compiler barrier keeps them after it.
+// Fail fast: once any wait of this link has given up (err != 0), no later wait
+// waits at all.  A sender that never arrives then costs one time-out, not one
+// per step: the run flags OV_XCHG, stops at the next plan, and the host raises
+// at its next status check (sg_xlink_status), naming the senders in err's bits.
 __device__ __forceinline__ void xlink_wait(const uint64_t* flags, uint32_t G, uint64_t target, uint32_t* err,
                                            uint64_t* ovf) {
     const uint32_t q = threadIdx.x;
     if (q < G) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                if (ovf) atomicOr((unsigned long long*)ovf, (unsigned long long)OV_XCHG);
+                break;  // an earlier wait gave up: the link is broken
+            }
             if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
                 atomicOr(err, 1u << (q & 31));
                 if (ovf) atomicOr((unsigned long long*)ovf, (unsigned long long)OV_XCHG);
@@ -1915,7 +1924,10 @@ __device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, con
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q) {
             const uint32_t i = lane + q * 64, j = i < nh ? i : 0u;
-            h[q] = recv[(size_t)(j / HDR_W) * d.xrows * RW + j % HDR_W];
+            // system-scope loads (sc0 sc1): the headers a peer handed off
+            // with system-coherent stores (xst) are read past every cache
+            h[q] = __hip_atomic_load(&recv[(size_t)(j / HDR_W) * d.xrows * RW + j % HDR_W], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
         }
 #pragma unroll
         for (uint32_t q = 0; q < HPL; ++q)
@@ -2085,33 +2097,48 @@ __device__ __forceinline__ uint64_t atomic_read(uint64_t* a) {
 __device__ __forceinline__ int64_t* xblock(const Dev& d, uint32_t q) {
     return d.xpeer ? d.xpeer[q] + d.xoff : d.xsend + (size_t)q * d.xrows * RW;
 }
-// Fused push: the blocks are complete at every peer (the caller's workgroup is
-// the last to arrive, and every workgroup waited for its stores before it
-// arrived); release at system scope, then one arrival per peer.
-__device__ __forceinline__ void xlink_signal(const Dev& d) {
-    // the blocks are in uncached memory: a store is acknowledged once it is
-    // performed there, so the wave's store count reaching zero orders them
-    // before the arrival; SG_XFENCE=1 adds the full system-scope release
-    // (an L2 write-back of this XCD's dirty lines, which the blocks are not)
-    if (d.xfence) __threadfence_system();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Fused push, the protocol every storing workgroup follows (k_proc's process
+// and drain steps, and k_xfused, the self-test that exercises it):
+//   1. store its rows into the peers' regions (xst);
+//   2. xlink_release: every wave drains its stores (vmcnt(0)), then the
+//      workgroup takes a device-scope ticket;
+//   3. the last workgroup writes the G headers, drains them the same way and
+//      adds one arrival to each peer's counter (xlink_arrive).
+// Across GPUs (xfence) every store of the handed-off bytes is system-coherent
+// (sc0 sc1: written through to the owner's memory at system scope) and drained
+// before the ticket / arrival — MI355X_MICROARCH.md "Correctness boundaries",
+// the valid form that replaces a release by the producers (a system-scope
+// release, __threadfence_system, is an L2 write-back + invalidate per wave:
+// it took k_proc 20.8 -> 39 us per 125k-host step, profiles/r06/g1); the
+// receiver's header loads are system-scope too.  Within one device the
+// blocks are uncached local memory and plain stores drained by vmcnt(0)
+// already order the rows before the arrival (measured).
+__device__ __forceinline__ void xst(uint32_t sys, int64_t* p, int64_t v) {
+    if (sys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
+__device__ __forceinline__ void xlink_release() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void xlink_arrive(int64_t* const* peer, uint32_t G, uint32_t g, uint32_t skip) {
+    xlink_release();
     __syncthreads();
-    if (threadIdx.x < d.G)
-        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(d.xpeer[threadIdx.x]) + d.g, 1ull,
+    if (threadIdx.x < G && threadIdx.x + 1 != skip)
+        __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(peer[threadIdx.x]) + g, 1ull,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void xlink_signal(const Dev& d) { xlink_arrive(d.xpeer, d.G, d.g, d.xskip); }
 __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t j) {
     RoundState* rs = d.rs;
+    const uint32_t sys = d.xpeer ? d.xfence : 0u;
     if (threadIdx.x < d.G) {
         const uint32_t p = threadIdx.x;
         const uint64_t left = atomic_read(&d.outn[p]) - d.sent[p];
         int64_t* blk = xblock(d, p);
-        blk[H_N] = (int64_t)(left < d.xcap ? left : d.xcap);
-        blk[H_BASE] = (int64_t)rs->S;  // the rows' time base: the step's window start
-        blk[H_MIN] = (int64_t)m;
-        blk[H_JMIN] = (int64_t)j;
-        blk[H_OVF] = (int64_t)atomic_read(&rs->overflow);
-        blk[H_ROUND] = (int64_t)rs->rounds;
+        xst(sys, blk + H_N, (int64_t)(left < d.xcap ? left : d.xcap));
+        xst(sys, blk + H_BASE, (int64_t)rs->S);  // the rows' time base: the step's window start
+        xst(sys, blk + H_MIN, (int64_t)m);
+        xst(sys, blk + H_JMIN, (int64_t)j);
+        xst(sys, blk + H_OVF, (int64_t)atomic_read(&rs->overflow));
+        xst(sys, blk + H_ROUND, (int64_t)rs->rounds);
     }
     if (threadIdx.x == 0) {
         uint64_t more = 0, peak = rs->peak_peer;
@@ -2120,7 +2147,7 @@ __device__ __forceinline__ void write_headers(const Dev& d, uint64_t m, uint64_t
             more |= (on - d.sent[q] > d.xcap) ? 1u : 0u;
             peak = q != d.g && on > peak ? on : peak;
         }
-        for (uint32_t q = 0; q < d.G; ++q) xblock(d, q)[H_MORE] = (int64_t)more;
+        for (uint32_t q = 0; q < d.G; ++q) xst(sys, xblock(d, q) + H_MORE, (int64_t)more);
         rs->peak_peer = peak;
     }
 }
@@ -2132,24 +2159,31 @@ __device__ __forceinline__ void fill_blocks(const Dev& d, uint32_t blk, uint32_t
         const uint64_t n = left < d.xcap ? left : d.xcap;
         int64_t* dst = xblock(d, p) + HDR * RW;
         const int64_t* src = d.outq + ((uint64_t)p * d.oreg + d.sent[p]) * RW;
+        const uint32_t sys = d.xpeer ? d.xfence : 0u;
         for (uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x; i < n * RW; i += (uint64_t)nblk * blockDim.x)
-            dst[i] = src[i];
+            xst(sys, dst + i, src[i]);
     }
     if (blk == 0) {
         uint64_t m, j;
         reduce_local(d, s16, m, j);  // barriers inside
         write_headers(d, m, j);
     }
-    if (d.xpeer) {  // fused push: the last workgroup to finish its copies signals the peers
-        __shared__ bool s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores performed
-        __syncthreads();
-        if (threadIdx.x == 0) s_last = atomicAdd((unsigned long long*)&d.rs->ticket, 1ULL) == nblk - 1;
-        __syncthreads();
-        if (s_last) {
-            if (threadIdx.x == 0) d.rs->ticket = 0;
-            xlink_signal(d);
-        }
+}
+// Fused push on a drain step: the last workgroup to finish arrives at the
+// peers.  Every workgroup calls it at its very end, after it staged the
+// previous step's received events: the arrival releases the peers' k_scatter
+// of this step, and their next k_proc stores into the parity buffer that
+// stage_received reads here (an arrival sent as soon as the copies
+// were done raced with that read).
+__device__ __forceinline__ void drain_arrive(const Dev& d, uint32_t nblk) {
+    __shared__ bool s_last;
+    xlink_release();  // this wave's rows performed at the peers
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd((unsigned long long*)&d.rs->ticket, 1ULL) == nblk - 1;
+    __syncthreads();
+    if (s_last) {
+        if (threadIdx.x == 0) d.rs->ticket = 0;
+        xlink_signal(d);
     }
 }
 
@@ -2448,7 +2482,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             rs->ins_local = stage_recv ? 1 : 0;
             rs->ins_S = S;
         }
-        if (!stage_recv) return;  // uniform
+        if (!stage_recv) {  // uniform
+            if (d.xpeer) drain_arrive(d, gridDim.x);
+            return;
+        }
         const uint32_t R = d.R;
         const uint64_t bS = rs_bS, bSW = bS * d.W;
         const uint32_t bSr = (uint32_t)(bS % R);
@@ -2472,6 +2509,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (sh.nloc > d.ECAP) flag(d, OV_PROC);
             d.rcnt[p] = sh.nloc < d.ECAP ? sh.nloc : d.ECAP;
         }
+        if (d.xpeer) drain_arrive(d, gridDim.x);  // after every read of the received blocks
         return;
     }
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
@@ -3470,17 +3508,25 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
         __syncthreads();
         const uint32_t nr = sh.nrem < d.ECAP ? sh.nrem : d.ECAP;
+        const bool xsys = d.xpeer && d.xfence;
         for (uint32_t i = tid; i < nr; i += K2_T) {
             const size_t so = (size_t)p * d.ECAP + i;
             const uint32_t dst = d.rem_dst[so];
             const uint32_t q = owner_of(d, dst);
             const uint64_t r = s_obase[q] + atomicAdd(&s_oslot[q], 1u);
             const Slot ev = d.rem[so];
-            int64_t* o = r < d.xcap ? xblock(d, q) + (HDR + r) * RW : d.outq + ((uint64_t)q * d.oreg + r) * RW;
+            const bool inblk = r < d.xcap;
+            int64_t* o = inblk ? xblock(d, q) + (HDR + r) * RW : d.outq + ((uint64_t)q * d.oreg + r) * RW;
             const uint64_t rel = ev.t - S;  // new events are at or after the window's end
             if (rel >> 40) a.overflow = true;  // beyond 2^40 ns (18 min) of the window start
-            o[0] = (int64_t)((rel & M40) | ((uint64_t)(dst - d.bounds[q]) << 40));
-            o[1] = (int64_t)ev.k;
+            const int64_t w0 = (int64_t)((rel & M40) | ((uint64_t)(dst - d.bounds[q]) << 40)), w1 = (int64_t)ev.k;
+            if (xsys && inblk) {  // into a peer on another GPU: system-coherent stores
+                xst(1u, o, w0);
+                xst(1u, o + 1, w1);
+            } else {
+                o[0] = w0;
+                o[1] = w1;
+            }
         }
     }
     if (stamp && tid == 0) stamp[13] = __builtin_amdgcn_s_memrealtime();
@@ -3543,12 +3589,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         // waits for another.
         __shared__ bool s_lastwg;
         __shared__ uint64_t s_mj[2];
-        // fused push: every wave's rows are performed at the peers before the
-        // workgroup arrives (the last one signals them)
-        if (wid == 0 || d.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // fused push: every wave's rows are performed (and, across GPUs,
+        // released at system scope) at the peers before the workgroup takes
+        // its ticket; the last one signals them (xlink_release / xlink_arrive)
+        if (d.xpeer) xlink_release();
+        else if (wid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // (a two-level ticket here, as k_scatter's plan arrival, hung the
-        // two-process xGMI test: profiles/r05/ptick8)
+        // two-process xGMI test in round 5; on round 6's tree it passed:
+        // profiles/r05/ptick8/README.md)
         if (tid == 0)
             s_lastwg = atomicAdd((unsigned long long*)&rs->ticket, 1ULL) == gridDim.x - 1;
         __syncthreads();
@@ -5709,10 +5758,17 @@ __global__ __launch_bounds__(256) void k_xpush(XArgs a) {
     int64_t* dst = a.peer[q] + a.buf_off + (size_t)a.g * a.xrows * RW;
     const longlong2* s2 = reinterpret_cast<const longlong2*>(src);
     longlong2* d2 = reinterpret_cast<longlong2*>(dst);
-    for (uint64_t i = (uint64_t)w * blockDim.x + threadIdx.x; i < rows; i += (uint64_t)XNW * blockDim.x) d2[i] = s2[i];
+    for (uint64_t i = (uint64_t)w * blockDim.x + threadIdx.x; i < rows; i += (uint64_t)XNW * blockDim.x) {
+        if (a.fence) {  // another GPU: system-coherent stores (xst)
+            const longlong2 v = s2[i];
+            xst(1u, dst + 2 * i, v.x);
+            xst(1u, dst + 2 * i + 1, v.y);
+        } else {
+            d2[i] = s2[i];
+        }
+    }
     // the rows are performed at the peer (uncached memory) before its counter moves
-    if (a.fence) __threadfence_system();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xlink_release();
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.peer[q]) + a.g, 1ull, __ATOMIC_RELAXED,
@@ -5738,6 +5794,39 @@ __global__ void k_xfill(int64_t* send, uint64_t xrows, uint32_t G, uint32_t g, u
         const uint32_t c = (uint32_t)(i % RW);
         send[i] = r == 0 && c == 0 ? (int64_t)n : xpattern(g, q, r, c, step);
     }
+}
+// The self-test of the fused push, the protocol real steps take (k_proc with
+// d.xpeer): XFW workgroups each store a slice of every peer's pattern rows
+// straight into the peer's region, release (xlink_release: vmcnt(0), and the
+// system-scope release when fenced) and take a device-scope ticket; the last
+// writes the G headers and arrives at every peer (xlink_arrive).
+constexpr uint32_t XFW = 128;
+struct XFArgs {
+    int64_t* peer[MAXG];  // each shard's region in this process
+    unsigned long long* ticket;
+    uint64_t xrows, buf_off, n, step;
+    uint32_t G, g, fence;
+};
+__global__ __launch_bounds__(256) void k_xfused(XFArgs a) {
+    const size_t own = a.buf_off + (size_t)a.g * a.xrows * RW;  // this sender's block in every region
+    for (uint32_t q = 0; q < a.G; ++q) {
+        int64_t* dst = a.peer[q] + own + HDR * RW;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n * RW;
+             i += (uint64_t)gridDim.x * blockDim.x)
+            xst(a.fence, dst + i, xpattern(a.g, q, HDR + i / RW, (uint32_t)(i % RW), a.step));
+    }
+    __shared__ bool s_last;
+    xlink_release();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(a.ticket, 1ull) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;  // uniform in the workgroup
+    if (threadIdx.x == 0) atomicExch(a.ticket, 0ull);
+    for (uint32_t i = threadIdx.x; i < a.G * HDR_W; i += blockDim.x) {
+        const uint32_t q = i / HDR_W, j = i % HDR_W, r = j / RW, c = j % RW;
+        xst(a.fence, a.peer[q] + own + j, r == 0 && c == 0 ? (int64_t)a.n : xpattern(a.g, q, r, c, a.step));
+    }
+    xlink_arrive(a.peer, a.G, a.g, 0);
 }
 __global__ void k_xcheck(const int64_t* recv, uint64_t xrows, uint32_t G, uint32_t g, uint64_t n, uint64_t step,
                          unsigned long long* bad) {
@@ -5770,17 +5859,26 @@ struct sg_xlink {
     // (one workgroup), not in k_scatter's prologue, whose spinning workgroups
     // would hold the CUs the peer's kernels need to arrive at all
     bool shared = false;
-    // a system-scope release before each arrival.  Between shards of one device
-    // (and at world 1) the blocks are uncached local memory and a store's
-    // acknowledgement orders it (measured: the fence costs 2.6 us per step); a
-    // peer on another GPU gets the full release, the ordering the memory model
-    // guarantees across xGMI.  SG_XFENCE=0 / 1 forces either.
+    // system-coherent stores (sc0 sc1) of every handed-off row and header,
+    // drained before each ticket and arrival (xst).  Between shards of one
+    // device (and at world 1) the blocks are uncached local memory and a plain
+    // store's acknowledgement orders it; a peer on another GPU gets the
+    // system-scope form the memory model guarantees across xGMI.
+    // SG_XFENCE=0 / 1 forces either.
     bool fence = false;
     // fused push (SG_XFUSE, default 1): k_proc stores the blocks into the peers'
     // regions and its last workgroup signals them; 0: k_xpush copies x->send
     bool fuse = true;
     int64_t** d_peer = nullptr;  // device copy of peer[] (k_proc's xblock)
     uint64_t expect = 0;         // arrivals every sender's counter holds once the last step is in
+    unsigned long long* ticket = nullptr;  // k_xfused's workgroup ticket (device)
+    // the last self-test: steps, mismatched words, which path it exercised
+    uint32_t st_steps = 0, st_fused = 0;
+    uint64_t st_bad = 0;
+    // test only (sg_xlink_debug_withhold): the fused step with this number
+    // (since attach) withholds its arrival at peer withhold_peer
+    uint64_t withhold_step = 0;
+    uint32_t withhold_peer = 0;
 };
 
 extern "C" {
@@ -5899,6 +5997,8 @@ int sg_xlink_create(sg_engine* e, sg_xlink** out) {
     if ((err = hipMemset(x->err, 0, sizeof(uint32_t))) != hipSuccess) return xlink_fail(x, "hipMemset", err);
     if ((err = hipDeviceSynchronize()) != hipSuccess) return xlink_fail(x, "hipDeviceSynchronize", err);
     if ((err = hipMalloc(&x->d_peer, MAXG * sizeof(int64_t*))) != hipSuccess) return xlink_fail(x, "hipMalloc", err);
+    if ((err = hipMalloc(&x->ticket, sizeof *x->ticket)) != hipSuccess) return xlink_fail(x, "hipMalloc", err);
+    if ((err = hipMemset(x->ticket, 0, sizeof *x->ticket)) != hipSuccess) return xlink_fail(x, "hipMemset", err);
     x->peer[x->g] = x->region;
     x->fuse = env_u32z("SG_XFUSE", 1) != 0;
     *out = x;
@@ -6006,8 +6106,10 @@ int sg_engine_run_steps_xlink(sg_engine* e, sg_xlink* x, uint64_t n_steps) {
             e->d.xpeer = x->d_peer;
             e->d.xoff = buf_off + (uint64_t)x->g * x->xrows * RW;
             e->d.xfence = x->fence ? 1u : 0u;
+            e->d.xskip = x->withhold_step == k ? x->withhold_peer + 1 : 0u;
             rc = sg_engine_step_send(e, x->send);
             e->d.xpeer = nullptr;
+            e->d.xskip = 0;
             if (rc) return rc;
             x->steps = k;
             x->expect += 1;
@@ -6047,11 +6149,38 @@ int sg_xlink_selftest(sg_xlink* x, uint32_t n_steps, uint64_t* bad) {
     const uint64_t cap = x->xrows - HDR;
     for (uint32_t i = 0; i < n_steps && rc == SG_OK; ++i) {
         const uint64_t k = x->steps + 1;
-        const uint64_t n = (k * 2654435761ull) % (cap + 1);  // rows this step, the same on every shard
-        hipLaunchKernelGGL(k_xfill, dim3(64), dim3(256), 0, e->stream, x->send, x->xrows, x->G, x->g, n, k);
+        // rows this step, the same on every shard; every fourth step a full block
+        const uint64_t n = (k & 3) == 3 ? cap : (k * 2654435761ull) % (cap + 1);
         const int64_t* recv = nullptr;
         uint64_t target = 0;
-        rc = xlink_push(e, x, &recv, &target);
+        if (x->fuse) {
+            // the fused push real steps take: many workgroups storing into the
+            // peers' regions, each releasing and taking a ticket, the last one
+            // writing the headers and arriving
+            XFArgs a;
+            for (uint32_t q = 0; q < MAXG; ++q) a.peer[q] = q < x->G ? x->peer[q] : nullptr;
+            a.ticket = x->ticket;
+            a.xrows = x->xrows;
+            a.buf_off = XFLAG_BYTES / sizeof(int64_t) + (k & 1) * (uint64_t)x->G * x->xrows * RW;
+            a.n = n;
+            a.step = k;
+            a.G = x->G;
+            a.g = x->g;
+            a.fence = x->fence ? 1u : 0u;
+            hipLaunchKernelGGL(k_xfused, dim3(XFW), dim3(256), 0, e->stream, a);
+            if (hipGetLastError() != hipSuccess) {
+                sg_set_error("sg_xlink_selftest: k_xfused launch failed");
+                rc = SG_ERR_HIP;
+                break;
+            }
+            x->steps = k;
+            x->expect += 1;
+            recv = x->region + a.buf_off;
+            target = x->expect;
+        } else {
+            hipLaunchKernelGGL(k_xfill, dim3(64), dim3(256), 0, e->stream, x->send, x->xrows, x->G, x->g, n, k);
+            rc = xlink_push(e, x, &recv, &target);
+        }
         if (rc == SG_OK) {
             hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, e->stream, (const uint64_t*)x->region, x->G, target,
                                x->err);
@@ -6067,6 +6196,9 @@ int sg_xlink_selftest(sg_xlink* x, uint32_t n_steps, uint64_t* bad) {
     if (rc) return rc;
     HIPCHK(err);
     *bad = h_bad + (h_err ? (1ull << 63) : 0ull);
+    x->st_steps = n_steps;
+    x->st_fused = x->fuse ? 1u : 0u;
+    x->st_bad = *bad;
     return SG_OK;
 }
 
@@ -6074,6 +6206,29 @@ int sg_xlink_status(sg_xlink* x, uint32_t* timed_out) {
     if (!x || !timed_out) return SG_ERR_INVAL;
     HIPCHK(hipStreamSynchronize(x->e->stream));
     HIPCHK(hipMemcpy(timed_out, x->err, sizeof *timed_out, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_xlink_info(sg_xlink* x, sg_xlink_desc* out) {
+    if (!x || !out) return SG_ERR_INVAL;
+    out->fenced = x->fence ? 1u : 0u;
+    out->fused = x->fuse ? 1u : 0u;
+    out->shared_device = x->shared ? 1u : 0u;
+    out->selftest_steps = x->st_steps;
+    out->selftest_fused = x->st_fused;
+    out->selftest_bad = x->st_bad;
+    out->steps = x->steps;
+    return SG_OK;
+}
+
+int sg_xlink_debug_withhold(sg_xlink* x, uint64_t step, uint32_t peer) {
+    if (!x || peer >= x->G) return SG_ERR_INVAL;
+    if (!x->fuse) {
+        sg_set_error("sg_xlink_debug_withhold: the fused push only (SG_XFUSE=1)");
+        return SG_ERR_STATE;
+    }
+    x->withhold_step = x->steps + step;
+    x->withhold_peer = peer;
     return SG_OK;
 }
 
@@ -6093,6 +6248,7 @@ int sg_xlink_destroy(sg_xlink* x) {
     if (x->send) (void)hipFree(x->send);
     if (x->err) (void)hipFree(x->err);
     if (x->d_peer) (void)hipFree(x->d_peer);
+    if (x->ticket) (void)hipFree(x->ticket);
     delete x;
     return rc;
 }

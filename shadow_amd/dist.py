@@ -130,13 +130,16 @@ class EngineShard:
         self.comm = comm
         self.eng.set_graph(graph_batch)
 
-    def enable_xlink(self, selftest_steps: int = 16):
+    def enable_xlink(self, selftest_steps: int = 64):
         """Exchange blocks by xGMI peer stores (sg_xlink) from now on: each rank
         exports its receive region, the 128-byte handles are all-gathered,
         every rank maps its peers', and `selftest_steps` pattern exchanges are
-        checked on every rank before the first real step.  Collective like
-        enable_native: all ranks take the link or none (RuntimeError on every
-        rank otherwise).  Call it once exchange_cap is final."""
+        checked on every rank before the first real step — through the path the
+        steps take (the fused push: many workgroups storing into the peers'
+        regions, each releasing and taking a ticket, the last one writing the
+        headers and arriving).  Collective like enable_native: all ranks take
+        the link or none (RuntimeError on every rank otherwise).  Call it once
+        exchange_cap is final."""
         from .engine import XLink
         xl, err, h = None, None, bytes(XLink.HANDLE_BYTES)
         try:
@@ -160,11 +163,16 @@ class EngineShard:
         if not self._all_ok(err is None):
             self._drop_link(xl)
             raise RuntimeError(f"mapping the peers' exchange regions failed on some rank ({err})")
-        bad = xl.selftest(selftest_steps)
+        try:
+            bad = xl.selftest(selftest_steps)
+        except Exception as exc:  # noqa: BLE001
+            bad, err = -1, exc
         if not self._all_ok(bad == 0):
             self._drop_link(xl)
-            raise RuntimeError(f"xGMI exchange self-test failed on some rank (this rank: {bad:#x})")
+            raise RuntimeError(f"xGMI exchange self-test failed on some rank (this rank: "
+                               f"{bad if bad < 0 else hex(bad)}{'' if err is None else ', ' + str(err)})")
         self.xl = xl
+        self.xl_info = xl.info()
 
     def _drop_link(self, xl):
         dist.barrier()  # no peer still stores into this rank's region
@@ -176,11 +184,11 @@ class EngineShard:
         captured graphs, then the communicator (RCCL frees captured
         collectives' resources with their graph)."""
         if getattr(self, "xl", None) is not None:
-            timed_out = self.xl.timed_out()
-            self._drop_link(self.xl)
-            self.xl = None
-            if timed_out:
-                raise RuntimeError("an xGMI exchange wait timed out (a peer never arrived)")
+            xl, self.xl = self.xl, None
+            try:
+                xl.check()
+            finally:
+                self._drop_link(xl)
         if getattr(self, "comm", None) is not None:
             self.eng.set_graph(0)
             self.sync()
@@ -191,11 +199,20 @@ class EngineShard:
     def native(self) -> bool:
         return self.xl is not None or self.comm is not None
 
-    def run_native(self, n: int):
+    def run_native(self, n: int, check: bool = True):
+        """n native steps; over the xGMI link, check=True then synchronises and
+        raises if a wait timed out (naming the senders that never arrived)."""
         if self.xl is not None:
             self.eng.run_steps_xlink(self.xl, n)
+            if check:
+                self.xl.check()
         else:
             self.eng.run_steps(self.comm, self.send.data_ptr(), self.recv.data_ptr(), n)
+
+    def check_link(self):
+        """Raises if a wait of the xGMI link timed out (no-op without one)."""
+        if getattr(self, "xl", None) is not None:
+            self.xl.check()
 
     def stream_ctx(self):
         return torch.cuda.stream(self.stream)
@@ -264,14 +281,16 @@ def run_step(shard, world: int):
     shard.post()
 
 
-def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16) -> int:
+def run(shard, world: int, max_steps: int = 1 << 62, check_every: int = 16, check_link: bool = True) -> int:
     """Run steps until the simulation is done (checked every check_every steps)
-    or max_steps; returns the steps run."""
+    or max_steps; returns the steps run.  check_link=False leaves the xGMI
+    link's time-out check to the caller (the bench's timed region: the check
+    synchronises)."""
     if getattr(shard, "native", False):
         n = 0
         while n < max_steps:
             k = min(check_every - n % check_every, max_steps - n)
-            shard.run_native(k)
+            shard.run_native(k, check=check_link)
             n += k
             if n % check_every == 0 and shard.done():
                 break
@@ -393,15 +412,18 @@ def bench(args, make_shard=None):
     shard.set_exchange_cap(cap)
     exch = "RCCL all-to-all" if native else f"{args.dist_backend} all-to-all"
     want = getattr(args, "exchange", "rccl")
+    xinfo = {"requested": want}
     if want in ("auto", "xgmi") and hasattr(shard, "enable_xlink"):
         try:
             shard.enable_xlink()
             exch = "xGMI peer stores (sg_xlink)"
+            xinfo.update(shard.xl_info, taken=True)
         except Exception as exc:  # the same on every rank (enable_xlink decides collectively)
             if want == "xgmi":
                 raise
             import sys
             print(f"xGMI exchange unavailable ({exc}); keeping the {exch}", file=sys.stderr, flush=True)
+            xinfo.update(taken=False, reason=str(exc)[:300])
     run(shard, world, 8, check_every=1 << 30)
     shard.sync()
     s0 = shard.stats()
@@ -409,10 +431,12 @@ def bench(args, make_shard=None):
     shard.sync()
     _cuda_sync()
     t0 = time.perf_counter()
-    run(shard, world, args.steps, check_every=1 << 30)
+    run(shard, world, args.steps, check_every=1 << 30, check_link=False)
     shard.sync()
     _cuda_sync()
     dt = time.perf_counter() - t0
+    if hasattr(shard, "check_link"):
+        shard.check_link()  # a timed-out exchange wait raises here, naming the sender
     dist.barrier()
     s1 = shard.stats()
     t = torch.tensor([dt], dtype=torch.float64, device=cdev)
@@ -484,6 +508,7 @@ def bench(args, make_shard=None):
                    "exchange_cap": cap,
                    "parallelism": f"hosts block-sharded {world} ways, one exchange per step: {exch}",
                    "exchange": exch,
+                   "xlink": xinfo,
                    "step_loop": "native (sg_engine_run_steps_xlink)" if exch.startswith("xGMI") else
                                 f"native (sg_engine_run_steps, hipGraph batch {args.graph})" if native
                                 else "python"},

@@ -280,10 +280,33 @@ class XLink:
         L.check(L.lib().sg_xlink_selftest(self.h, n_steps, C.byref(bad)))
         return bad.value
 
-    def timed_out(self) -> bool:
+    def timed_out_senders(self) -> list:
+        """The shards whose arrival a wait of this link gave up on (synchronises
+        the engine stream)."""
         t = C.c_uint32()
         L.check(L.lib().sg_xlink_status(self.h, C.byref(t)))
-        return t.value != 0
+        return [q for q in range(32) if t.value >> q & 1]
+
+    def timed_out(self) -> bool:
+        return bool(self.timed_out_senders())
+
+    def check(self):
+        """Raises once a wait has timed out, naming the senders that never
+        arrived (after the first time-out every later wait returns at once, so
+        the steps enqueued behind it finish quickly and the run stops)."""
+        bad = self.timed_out_senders()
+        if bad:
+            raise RuntimeError(f"xGMI exchange: no arrival from shard(s) {bad} within 5 s "
+                               f"(shard {self.eng.params.shard_index} of {self.eng.params.shard_count}); the run stopped")
+
+    def info(self) -> dict:
+        d = L.XLinkDesc()
+        L.check(L.lib().sg_xlink_info(self.h, C.byref(d)))
+        return d.as_dict()
+
+    def debug_withhold(self, step: int, peer: int):
+        """Tests only: the fused step `step` steps from now skips its arrival at `peer`."""
+        L.check(L.lib().sg_xlink_debug_withhold(self.h, step, peer))
 
     def close(self):
         if getattr(self, "h", None):

@@ -123,7 +123,7 @@ def test_xlink_steps_world1_match_oracle(xcap, fuse, fence, monkeypatch):
     """sg_engine_run_steps_xlink at world 1: every block goes through k_xpush
     into this shard's own exchange region (uncached memory, parity buffers,
     arrival counters) and k_xwait, after a pattern self-test; a 7-row cap
-    forces drain steps; with and without the system-scope release before each
+    (no event crosses a shard at world 1: only the block size changes); with and without the system-scope release before each
     arrival (SG_XFENCE=1; the default fences only across devices).  SG_XFUSE=1 (the default): k_proc stores the blocks
     into the region itself and its last workgroup signals; 0: k_xpush copies
     them after it.  Half way the link is closed (the last received blocks are
@@ -156,6 +156,60 @@ def test_xlink_steps_world1_match_oracle(xcap, fuse, fence, monkeypatch):
             assert n < 100_000
     sh.sync()
     _check(cfg, [sh])
+
+
+@pytest.mark.parametrize("fence", ["", "1"])
+def test_xlink_selftest_runs_the_fused_protocol(fence, monkeypatch):
+    """The self-test that decides between the xGMI link and RCCL exercises the
+    path real steps take (SG_XFUSE=1, the default): k_xfused's 128 workgroups
+    store into the region, release, take a ticket, and the last one writes
+    the headers and arrives; 64 exchanges (every fourth a full block) check
+    clean, fenced and unfenced, and the link reports what it ran."""
+    from shadow_amd.dist import EngineShard
+    from shadow_amd.engine import XLink
+    monkeypatch.setenv("SG_XFENCE", fence)
+    cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
+    sh = EngineShard(cfg, 0, 1, 0, exchange_cap=4096)
+    sh.boot()
+    xl = XLink(sh.eng)
+    xl.attach(xl.handle())
+    assert xl.selftest(64) == 0
+    info = xl.info()
+    assert info["fused"] == 1 and info["selftest_fused"] == 1 and info["selftest_steps"] == 64
+    assert info["selftest_bad"] == 0 and info["steps"] == 64 and info["shared_device"] == 0
+    assert info["fenced"] == (1 if fence else 0)
+    xl.close()
+
+
+@pytest.mark.timeout(60)
+def test_xlink_withheld_arrival_fails_fast():
+    """A sender that never arrives (sg_xlink_debug_withhold: the next fused
+    step skips its arrival) must fail the run fast: the wait gives up once
+    (5 s), every later wait of the link returns at once, the run stops
+    (OV_XCHG) and the host's check raises naming the missing shard — within
+    10 s for 40 steps, where a wait per step would take 200 s.  World 1: the
+    wait is k_scatter's in-kernel one, the one ranks on different GPUs take."""
+    import time
+    from shadow_amd.dist import EngineShard
+    from shadow_amd.engine import XLink
+    cfg = phold.tiny_config(n_hosts=500, V=6, load=4, end_time_s=0.4, loss=0.1)
+    sh = EngineShard(cfg, 0, 1, 0, exchange_cap=4096)
+    sh.boot()
+    xl = XLink(sh.eng)
+    xl.attach(xl.handle())
+    assert xl.selftest(4) == 0
+    sh.xl = xl
+    sh.run_native(2)
+    xl.debug_withhold(1, 0)
+    t0 = time.perf_counter()
+    with pytest.raises(RuntimeError, match=r"no arrival from shard\(s\) \[0\]"):
+        sh.run_native(40)
+    dt = time.perf_counter() - t0
+    assert dt < 10.0, dt
+    st = sh.stats()
+    assert st["overflow"] & 8 and st["done"], st  # OV_XCHG: the run stopped
+    sh.xl = None
+    xl.close()
 
 
 @pytest.mark.parametrize("graph", [0, 4])
