@@ -34,7 +34,7 @@ HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contr
              "-mllvm", "-instcombine-max-copied-from-constant-users=8000",
              "-Rpass-analysis=kernel-resource-usage"]
 SCRATCH_MAX = 256  # bytes per lane a hot kernel may spill (k_proc: 40-72)
-HOT_KERNELS = ("k_proc", "k_scatter", "k_spec")
+HOT_KERNELS = ("k_proc", "k_scatter")
 
 C_SOURCES = ["sg_host.c", "sg_policy.c", "sg_sched.c", "sg_topology.c"]
 HIP_SOURCES = ["sg_engine.hip", "sg_policy_dev.hip"]

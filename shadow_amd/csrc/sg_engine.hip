@@ -85,16 +85,9 @@ constexpr uint32_t RMAX = 4096;          // ring buckets (LDS bucket bins)
 #define SG_XS 2
 #endif
 constexpr uint32_t XS = SG_XS;
-// Partition halves: k_scatter's workgroups that write a host partition's due
-// events (insert, gather, receive) reserve on one of PH counters of it, by
-// workgroup parity, each counter with its own CAPP / PH region of the
-// partition; k_proc reads both.  One counter per partition took up to ~640
-// returning adds a round at configs[3].
-#ifndef SG_PH
-#define SG_PH 1
-#endif
-constexpr uint32_t PH = SG_PH;
-static_assert(PH == 1 || PH == 2, "one or two partition halves");
+// (Two counters per host partition for k_scatter's writers, by workgroup
+// parity, were measured in round 5: correct, k_proc +0.6 us, k_scatter
+// unchanged, profiles/r05/ph2; removed.)
 
 constexpr uint32_t HPMAX = 4096;         // hosts per partition
 constexpr uint32_t PMAX = 4096;          // partitions
@@ -145,25 +138,12 @@ struct Slot {
     uint64_t t;
     uint64_t k;
 };
-// Streamed records (read or written once per round: due-event copies, staged
-// events, host state) go through non-temporal loads / stores, so they do not
-// evict the randomly read tables (destination vertices, path records) from
-// an XCD's 4 MB L2.  SG_NT is a mask: 1 loads, 2 stores.  Measured on
-// configs[3] (profiles/r02/knobs/nt.log): 3 (both) 3.67e9 events/s against
-// 4.60e9 plain — the next kernel re-reads the streamed records from HBM; 2
-// alone, round 4: 66.8 against 52.5 us per round (profiles/r04/flatb).  Write-
-// through (sc1) stores were worse still (profiles/r04/wt): L2 merges the 16-B
-// records into whole lines only when they are written back, not through.
-#ifndef SG_NT
-#define SG_NT 0
-#endif
-// SG_ABL (timing experiments only; results are wrong with any bit set): 1 no
-// digest atomics, 2 no host-state stores, 4 no destination loads, 8 no staging
-// stores, 16 no bucket bins, 32 no digest hash, 64 no bucket-minimum atomics in
-// the reservations, 128 no returning reservation atomics (bases read, not added)
-#ifndef SG_ABL
-#define SG_ABL 0
-#endif
+// Streamed records (due-event copies, staged events, host state) use plain
+// loads and stores: non-temporal ones (the next kernel re-reads the streamed
+// records from HBM: 3.67e9 against 4.60e9 events/s, profiles/r02/knobs/nt.log;
+// stores alone 66.8 against 52.5 us per round, profiles/r04/flatb) and
+// write-through (sc1) stores (profiles/r04/wt: L2 merges the 16-B records into
+// whole lines only when it writes them back) were measured slower and removed.
 // SG_PMIN: each reserving row keeps its own minimum time offset per bucket
 // (pmin, a plain load / min / store of its own row) instead of a 64-bit
 // device-scope atomicMin on the bucket's minimum (bmin); the rmin role takes
@@ -178,33 +158,11 @@ struct Slot {
 #ifndef SG_RS_LANES
 #define SG_RS_LANES 1
 #endif
-typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ Rec ld_stream(const Rec* p) {
-#if SG_NT & 1
-    const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
-    return Rec{v.x, v.y};
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ ulonglong2 ld_stream2(const ulonglong2* p) {
-#if SG_NT & 1
-    const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
-    return make_ulonglong2(v.x, v.y);
-#else
-    return *p;
-#endif
-}
+__device__ __forceinline__ Rec ld_stream(const Rec* p) { return *p; }
+__device__ __forceinline__ ulonglong2 ld_stream2(const ulonglong2* p) { return *p; }
 // A streamed 16-B record store at a byte offset from a wave-uniform array start.
 __device__ __forceinline__ void st_rec(void* base, uint64_t off, uint64_t a, uint64_t b) {
-#if SG_NT & 2
-    u64x2_t v;
-    v.x = a;
-    v.y = b;
-    __builtin_nontemporal_store(v, reinterpret_cast<u64x2_t*>(static_cast<char*>(base) + off));
-#else
     *reinterpret_cast<ulonglong2*>(static_cast<char*>(base) + off) = make_ulonglong2(a, b);
-#endif
 }
 struct DueEnt {
     uint32_t id;      // chunk
@@ -301,12 +259,6 @@ struct RoundState {
     uint64_t xacc[2];    // emitted min, discovery min of k_proc's workgroups (atomics)
     uint64_t recv_ok;    // a several-shard k_scatter read the receive buffer: the next k_proc stages it
     uint64_t tail_r, bS_r;  // fl_tail % NCH, bS % R, kept with them (the planner's 64-bit divisions)
-    // split step (several shards): k_spec runs beside the
-    // all-to-all and gathers the guessed bucket; k_post keeps it on a hit
-    uint64_t psel;        // the current window's partition counts are in pcnt (0) or pcnt2 (1)
-    uint64_t spec_fold;   // the fold k_spec gathered the guessed bucket for, else UINT64_MAX
-    uint64_t spec_nfree;  // chunks of that bucket k_spec put into the ring behind the planned tail
-    uint64_t spec_b;      // that bucket (absolute)
 };
 
 // The gather's due list, guessed one kernel ahead.  In steady state a window
@@ -351,7 +303,6 @@ struct Dev {
     uint64_t gossip_start, gossip_interval;
     uint32_t* seen;           // [L][mw] per-host message bitsets
     uint32_t R, NCH, HP, P, CAPP, ECAP, G1, G3;
-    uint32_t CAPH;  // CAPP / PH: one partition half's records
     Div32 hpdiv;              // a local slot's partition: slot / HP (HP need not be a power of two)
     uint32_t EVL, bin_off, ev_off, proc_lds;  // k_proc LDS: due events kept, bucket bins at,
                                               // events at, dynamic bytes
@@ -408,9 +359,7 @@ struct Dev {
     uint64_t* tick;           // [8] k_scatter's plan arrivals per workgroup shard blockIdx & 7 (SG_TICK8)
     uint32_t gspec_mode;      // SG_GSPEC: 1 guess (default), 0 never, 2 a wrong bucket (tests the check)
     // partitions
-    uint32_t split;           // several shards: the split step (k_spec beside the all-to-all, k_post after)
-    uint32_t* pcnt2;          // [PH][P] the window's partition counts when k_post discarded k_spec's gather
-    uint32_t* pcnt;           // [PH][P] due events of the partition (half) this round
+    uint32_t* pcnt;           // [P] due events of the partition this round
     Rec* part;                // [P][CAPP]
     Rec* part2;               // [P][CAPP] sorted by host
     Rec* extras;              // [P][K2_T][XCAP]
@@ -830,11 +779,8 @@ __global__ void k_boot(Dev d) {
     for (size_t j = i; j < (size_t)d.P * d.R; j += (size_t)gridDim.x * blockDim.x) d.pmin[j] = UINT32_MAX;
     if (i < d.P + d.G3) d.stn[i] = 0;  // k_scatter's refill role fills the stashes
     if (i < 8) d.tick[i] = 0;
-    if (i < PH * d.P) {
-        d.pcnt[i] = 0;
-        d.pcnt2[i] = 0;
-    }
     if (i < d.P) {
+        d.pcnt[i] = 0;
         d.rcnt[i] = 0;
         if (d.remn) d.remn[i] = 0;
         for (int c = 0; c < NCTR; ++c) d.pcum[(size_t)c * d.P + i] = 0;
@@ -877,10 +823,6 @@ __global__ void k_boot(Dev d) {
         rs->ticket = 0;
         rs->xacc[0] = UINT64_MAX;
         rs->xacc[1] = UINT64_MAX;
-        rs->psel = 0;  // the boot k_scatter gathers into pcnt
-        rs->spec_fold = UINT64_MAX;
-        rs->spec_nfree = 0;
-        rs->spec_b = UINT64_MAX;
         rs->recv_ok = 0;
     }
     if (i < d.G && d.outn) {
@@ -900,7 +842,7 @@ constexpr int GUNR = 4;          // events in flight per thread (two-pass path)
 template <bool SCATTER, int GT>
 __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, uint32_t nb,
                                             uint64_t S, uint64_t E, uint32_t* s_cnt, uint32_t* s_cur,
-                                            uint64_t& cmin, uint64_t& ntomb, uint64_t& ng, uint32_t hoff) {
+                                            uint64_t& cmin, uint64_t& ntomb, uint64_t& ng) {
     const uint32_t tot = nb * CH;
     for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += GT * GUNR) {
         Rec r[GUNR];
@@ -934,8 +876,8 @@ __device__ __forceinline__ void gather_pass(const Dev& d, const DueEnt* s_de, ui
             }
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPH)
-                st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
+            if (slot < d.CAPP)
+                st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - S), r[q].k);
             if (de.nflags & RETAINED) {
                 d.pool[((size_t)de.id << CH_SHIFT) + (e & (CH - 1))].a = TOMB;
                 ++ntomb;
@@ -971,7 +913,6 @@ struct StepView {
     Window w;
     uint32_t cur, listed, ins_local, round_done, more, done, quit;
     uint32_t tail_r, bSr;    // tail % NCH, bS % R (64-bit divisions done once, by the planner)
-    uint32_t hit;            // split step: the new window is the bucket k_spec gathered
 };
 constexpr uint32_t SEGMAX = (NBMAX + 2) * XS;  // segments, at most
 // Segment j is bucket sub-list x = j % XS of the list's k-th bucket, k = j / XS:
@@ -1000,7 +941,7 @@ struct DueList {
 };
 template <int GT>
 __device__ uint32_t due_segments(const Dev& d, const StepView& sv, DueList& dl, uint32_t* s_start, uint32_t* s_lo,
-                                 uint64_t* s16, uint64_t* nfree_out, bool all_written) {
+                                 uint64_t* s16, uint64_t* nfree_out) {
     dl.bS = sv.bS;
     dl.bL = sv.bL;
     dl.pret = sv.pret;
@@ -1021,9 +962,7 @@ __device__ uint32_t due_segments(const Dev& d, const StepView& sv, DueList& dl, 
         bool events;
         dl.seg(j, b, x, flags, events);
         const uint32_t row = x * dl.R + (uint32_t)(b % dl.R);
-        // all_written (split step): k_spec wrote every reserved slot before this
-        // launch, and routed nothing, so the written count is the reserved one
-        const uint32_t hi = d.bk[row], lo = events ? (all_written ? hi : d.bw[(size_t)cur * XS * dl.R + row]) : 0u;
+        const uint32_t hi = d.bk[row], lo = events ? d.bw[(size_t)cur * XS * dl.R + row] : 0u;
         const uint32_t n = ((flags ? lo : hi) + CH - 1) >> CH_SHIFT;
         s_lo[j] = lo;
         s_start[j] = n;  // the count for now
@@ -1089,15 +1028,10 @@ __device__ __forceinline__ void gspec_load(const Dev& d, uint32_t w, uint32_t nw
                              (b & ((1ull << 48) - 1)) * d.W};
     }
 }
-// gmode: GM_PLAN (k_scatter: the guessed list when the plan confirms it, else
-// the list path), GM_SPEC (k_spec, before the plan: the guessed bucket as the
-// window sv describes, nothing otherwise; its ring count goes to spec_nfree),
-// GM_FALLBACK (k_post after a miss: the list path over every written slot).
-// pc: the partition counters the events are appended to.
-enum GMode { GM_PLAN = 0, GM_SPEC = 1, GM_FALLBACK = 2 };
+// The guessed list when the plan confirms it, else the list path.
 template <int GT>
 __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32_t nw, unsigned char* lds,
-                            const uint64_t* s_gsw, uint64_t* st, int gmode, uint32_t* pc) {
+                            const uint64_t* s_gsw, uint64_t* st) {
     constexpr int GR = 4 * (int)CH / GT;
     static_assert(GR * GT == (int)(GSPEC_N * CH), "the one-pass path holds GSPEC_N chunks");
     uint32_t* s_cnt = (uint32_t*)lds;                      // [PMAX]
@@ -1112,9 +1046,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     // behind the tail as the entries are staged below (the next step's plan
     // advances the tail; nothing allocates before it).
     const uint32_t tail_r = sv.tail_r;
-    // this workgroup's partition half (PH): its counters and region offset
-    const uint32_t half = PH == 2 ? (w & 1u) : 0u, hoff = half * d.CAPH;
-    pc += (size_t)half * P;
+    uint32_t* pc = d.pcnt;
     for (uint32_t p = threadIdx.x; p < P; p += GT) {
         s_cnt[p] = 0;
         s_cur[p] = 0;
@@ -1125,7 +1057,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t c = s_cnt[p];
             if (c) {
                 const uint32_t base = atomicAdd(&pc[p], c);
-                if (base + c > d.CAPH) flag(d, OV_PART);
+                if (base + c > d.CAPP) flag(d, OV_PART);
                 s_cnt[p] = base;
             }
         }
@@ -1177,7 +1109,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             const uint32_t p = pp[q];
             const uint32_t slot = s_cnt[p] + atomicAdd(&s_cur[p], 1u);
             ++ng;
-            if (slot < d.CAPH) st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, r[q].a, r[q].k);
+            if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, r[q].a, r[q].k);
             const uint32_t e = threadIdx.x + q * GT;
             const DueEnt de = s_de[e >> CH_SHIFT];
             if (de.nflags & RETAINED) {
@@ -1195,7 +1127,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
     const GSpecLo gl = gspec_lo(s_gsw[2]);
     const uint32_t gnid = gl.nid;
     const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
-    if (gmode != GM_FALLBACK && GSPEC_XS && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb &&
+    if (GSPEC_XS && s_gsw[0] == sv.fold && sv.bS == gb && sv.bL == gb &&
         sv.ret == UINT64_MAX && !spent && gnid <= GSPEC_N * nw) {  // uniform
         const uint32_t row = (uint32_t)(s_gsw[1] >> 48);
         // in flight under the pool loads: the sub-lists' reserved slots
@@ -1205,12 +1137,8 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             // ring order as the list path's: sub-list 0's chunks, then sub-list 1's
             const uint32_t nd0 = (hi + CH - 1) >> CH_SHIFT, nd = nd0 + ((hi1 + CH - 1) >> CH_SHIFT);
             if (w == 0 && threadIdx.x == 0) {
-                if (gmode == GM_SPEC) {  // k_post keeps it on a hit (publish_step)
-                    d.rs->spec_nfree = nd;
-                } else {
-                    d.rs->nfree2[sv.cur ^ 1] = nd;
-                    atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
-                }
+                d.rs->nfree2[sv.cur ^ 1] = nd;
+                atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
             }
             if (st) {
                 st[5] = nd;
@@ -1232,10 +1160,9 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             }
         });
     } else {
-    if (gmode == GM_SPEC) return;  // uniform: no guess to gather (k_post takes the list path)
     DueList dl;
     uint64_t nfree;
-    const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree, gmode == GM_FALLBACK);
+    const uint64_t nd = due_segments<GT>(d, sv, dl, s_start, s_lo, s16, &nfree);
     if (w == 0 && threadIdx.x == 0) {
         d.rs->nfree2[sv.cur ^ 1] = nfree;
         atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GLIST * d.P], 1ull);
@@ -1275,7 +1202,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
             __syncthreads();
             if (threadIdx.x < nb) s_de[threadIdx.x] = due_entry(d, dl, s_start, s_lo, (uint32_t)(cb + threadIdx.x));
             __syncthreads();
-            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng, hoff);
+            gather_pass<false, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
         __syncthreads();
         reserve();
@@ -1288,7 +1215,7 @@ __device__ void gather_role(const Dev& d, const StepView& sv, uint32_t w, uint32
                 free_chunk(de, cb + threadIdx.x);
             }
             __syncthreads();
-            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng, hoff);
+            gather_pass<true, GT>(d, s_de, nb, S, E, s_cnt, s_cur, cmin, ntomb, ng);
         }
     }
     }  // the list path
@@ -1675,13 +1602,13 @@ __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint
         uint32_t* pm = d.pmin + (size_t)row * R + rb;  // this row's own entry: no other row writes it
         const uint32_t pold = *pm;
 #endif
-        const uint32_t base = (SG_ABL & 128) ? bkx[rb] : atomicAdd(&bkx[rb], c);
+        const uint32_t base = atomicAdd(&bkx[rb], c);
         wb[rb] = base;
 #if SG_PMIN
         *pm = s_bm[rb] < pold ? s_bm[rb] : pold;
 #else
         const uint64_t b = bS + (rb >= bSr ? rb - bSr : rb + R - bSr);  // absolute bucket of slot rb
-        if (!(SG_ABL & 64)) atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
+        atomicMin((unsigned long long*)&d.bmin[rb], (unsigned long long)(b * W + s_bm[rb]));
 #endif
         const uint32_t f = (base + CH - 1) >> CH_SHIFT, l = (base + c - 1) >> CH_SHIFT;
         first[q] = f;
@@ -1765,8 +1692,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
 
 // mode 0: one shard, after k_proc; 1: several shards, after the all-to-all
 // (hdr: the G blocks' HDR_W header words, LDS); 2: boot (the first window is
-// listed already); 3: several shards, split step (k_post: as 1, and whether
-// the new window is the bucket k_spec gathered).  One thread, from the LDS copy of the round state
+// listed already).  One thread, from the LDS copy of the round state
 // (load_round_state), so no load of it waits for another.
 constexpr uint32_t HDR_W = HDR * RW;  // header words per exchange block
 constexpr uint32_t RSW = sizeof(RoundState) / 8;
@@ -1811,7 +1737,7 @@ __device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundSta
         m = sv.rmin0 < m ? sv.rmin0 : m;
         m = m < SIMTIME_MAX ? m : SIMTIME_MAX;
         j = jmin0 < jm ? jmin0 : jm;
-    } else if (mode == 1 || mode == 3) {
+    } else if (mode == 1) {
         uint64_t more = 0;
         // the header words from wave 0's registers when the G blocks' words fit
         // one per lane (h_lanes: G <= 8), else from their LDS copy
@@ -1833,7 +1759,6 @@ __device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundSta
     sv.ovf = ovf;
     sv.tail_r = (uint32_t)rs->tail_r;
     sv.bSr = (uint32_t)rs->bS_r;
-    sv.hit = 0;
     if (mode == 2 || sv.more) return;
     sv.round_done = 1;
     const Window w = next_window(d, m, j, mj0, nmj0);
@@ -1866,11 +1791,6 @@ __device__ __forceinline__ void step_view(const Dev& d, int mode, const RoundSta
         } else {
             sv.bSr = (uint32_t)(sv.bS % d.R);
         }
-        // split step: k_spec gathered bucket spec_b as the window [spec_b * W,
-        // (spec_b + 1) * W); a hit (the plan's window is exactly that) keeps it
-        const bool spent = sv.pret != UINT64_MAX && sv.pret < sv.bS;
-        sv.hit = mode == 3 && rs->spec_fold == sv.fold && rs->spec_b == sv.bS && sv.bL == sv.bS &&
-                 sv.ret == UINT64_MAX && !spent && sv.S == sv.bS * W;
     }
 }
 
@@ -1916,7 +1836,7 @@ __device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, con
     const uint64_t v = reinterpret_cast<const uint64_t*>(d.rs)[lane < RSW ? lane : 0u];
     constexpr uint32_t HPL = (MAXG * HDR_W + 63) / 64;  // header words per lane, at most
     int64_t h[HPL];
-    if (mode == 1 || mode == 3) {  // uniform
+    if (mode == 1) {  // uniform
         // sg_xlink: the peers' arrivals before their headers are read (the
         // round-state load above is in flight meanwhile)
         if (d.xwait) xlink_wait(d.xwait, d.G, d.xwait_target, d.xwait_err, &d.rs->overflow);
@@ -1948,7 +1868,7 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     if (sv.ovf) atomicOr((unsigned long long*)&rs->overflow, (unsigned long long)sv.ovf);
     rs->fold = sv.fold + 1;
     rs->splan = 0;
-    if (mode == 1 || mode == 3) {
+    if (mode == 1) {
         rs->recv_ok = 1;  // the next k_proc stages what this launch did not route
         if (d.check) {
             // debug (SG_CHECK=1): the MIN terms k_proc's last workgroup put in
@@ -1997,13 +1917,6 @@ __device__ void publish_step(const Dev& d, int mode, const StepView& sv, const i
     const Window& w = sv.w;
     rs->phase = 0;
     rs->jmin = sv.j;
-    if (mode == 3) {  // split step: k_spec's gather kept (its counts in pcnt), or k_post's in pcnt2
-        rs->psel = sv.hit ? 0 : 1;
-        if (sv.hit) {
-            rs->nfree2[cur ^ 1] = rs->spec_nfree;
-            atomicAdd((unsigned long long*)&d.pcum[(size_t)C_GSPEC * d.P], 1ull);
-        }
-    }
     if (d.wlog && sv.rounds0 < d.wlog_cap) {  // the window just executed
         d.wlog[2 * sv.rounds0] = sv.S0;
         d.wlog[2 * sv.rounds0 + 1] = sv.E0;
@@ -2348,12 +2261,6 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
     }
 }
 
-// SG_SORT_LDS: 1, the sort's barriers after the histogram order LDS only (the
-// flat pass's state loads stay in flight under the scan); 2, also the first
-// barrier, with the state loads issued as soon as the records arrive.
-#ifndef SG_SORT_LDS
-#define SG_SORT_LDS 0
-#endif
 // SG_INS_PRE: k_scatter's insert role loads its first staged events and its
 // reservation bases at launch, beside the plan (1, default), or after it (0).
 // With the gather dispatched after the inserts, 0 was faster (51.1-51.4
@@ -2379,11 +2286,6 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_FLAT_LDSB
 #define SG_FLAT_LDSB 1
 #endif
-// SG_PART_LATE: k_proc's partials and MIN atomics after its reservations (1)
-// or before them (0, default): 1 measured k_proc +1.0 us (profiles/r05/tick).
-#ifndef SG_PART_LATE
-#define SG_PART_LATE 0
-#endif
 // SG_TICK8: k_scatter's plan arrival in two levels, one counter per workgroup
 // shard blockIdx & 7 and then the plan counter (1, default), or every
 // workgroup on the plan counter (0): k_scatter 17.6 -> 17.1 us, configs[3]
@@ -2407,22 +2309,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const uint64_t rsv = reinterpret_cast<const uint64_t*>(rs)[(tid & 63) < RSW ? (tid & 63) : 0u];
     const Rec* part = d.part + (size_t)p * d.CAPP;
     // the first SPEC records per lane are loaded before the count arrives
-    // (CAPH >= K2_T; records past the count are ignored).  A lane's record q:
-    // PH = 1, entry tid + q * K2_T of the partition; PH = 2, slot
-    // tid + (q >> 1) * K2_T of half q & 1 (each half filled from its start)
+    // (CAPP >= K2_T; records past the count are ignored).  A lane's record q
+    // is entry tid + q * K2_T of the partition.
     constexpr uint32_t SPEC = 2;
     constexpr uint32_t EPTF = FLAT ? SPEC : EPT;
-    auto rq_idx = [&](uint32_t q) __attribute__((always_inline)) {
-        return PH == 1 ? tid + q * K2_T : (q & 1u) * d.CAPH + tid + (q >> 1) * K2_T;
-    };
+    auto rq_idx = [&](uint32_t q) __attribute__((always_inline)) { return tid + q * K2_T; };
     Rec rr[EPTF];
 #pragma unroll
     for (uint32_t q = 0; q < SPEC; ++q) rr[q] = ld_stream(&part[rq_idx(q)]);
-    // the window's count: pcnt, or pcnt2 when a split step's k_post discarded
-    // k_spec's gather (rs->psel, known once the round state arrives); PH = 2,
-    // per half
-    const uint32_t n_a = d.pcnt[p], n_b = d.pcnt2[p];
-    const uint32_t n_a1 = PH == 2 ? d.pcnt[d.P + p] : 0u, n_b1 = PH == 2 ? d.pcnt2[d.P + p] : 0u;
+    const uint32_t n_a = d.pcnt[p];  // the window's due events of the partition
     // the partition's chunk stash (reserve_buckets), loaded now, used at the end
     const uint32_t stash_id = d.stash[(size_t)p * ST + (tid & (ST - 1))], stash_n = d.stn[p];
     uint32_t v_first = 0, v_last = 0;  // ROWS: the partition's first and last slots' vertices
@@ -2435,8 +2330,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // a use of those loads on the paths that do not need them keeps the
     // compiler from sinking them below the branches (and so behind the wait)
     auto pin = [&]() __attribute__((always_inline)) {
-        asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_a), "v"(n_b), "v"(stash_id), "v"(stash_n),
-                     "v"(v_first), "v"(v_last), "v"(n_a1), "v"(n_b1));
+        asm volatile("" ::"v"(rr[0].a), "v"(rr[1].a), "v"(n_a), "v"(stash_id), "v"(stash_n), "v"(v_first),
+                     "v"(v_last));
     };
     if (rsf(RSF(done))) {
         pin();
@@ -2515,15 +2410,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint64_t* stamp = d.stamps ? d.stamps + (size_t)p * SG_STAMP_W : nullptr;
     if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     const uint64_t t_start = d.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
-    const bool psel = rsf(RSF(psel)) != 0;
-    const uint32_t n0_raw = psel ? n_b : n_a, n1_raw = psel ? n_b1 : n_a1;
-    const uint32_t n0 = n0_raw < d.CAPH ? n0_raw : d.CAPH, n1 = n1_raw < d.CAPH ? n1_raw : d.CAPH;
-    const uint32_t n = n0 + n1;  // the partition's due events
+    const uint32_t n = n_a < d.CAPP ? n_a : d.CAPP;  // the partition's due events
     // lane record q holds an event; entry i of the partition (0 <= i < n)
-    auto rq_ok = [&](uint32_t q) __attribute__((always_inline)) {
-        return PH == 1 ? tid + q * K2_T < n : tid + (q >> 1) * K2_T < ((q & 1u) ? n1 : n0);
-    };
-    auto pidx = [&](uint32_t i) __attribute__((always_inline)) { return PH == 1 || i < n0 ? i : d.CAPH + (i - n0); };
+    auto rq_ok = [&](uint32_t q) __attribute__((always_inline)) { return tid + q * K2_T < n; };
+    auto pidx = [&](uint32_t i) __attribute__((always_inline)) { return i; };
     // flat pass: a host's digest terms of its events but the last, summed in
     // LDS over s_vh / s_sb (phase A's arrays, free until phase A runs)
     unsigned long long* s_dig = reinterpret_cast<unsigned long long*>(s_vh);
@@ -2547,8 +2437,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     if (tid < MAXG) sh.peer[tid] = 0;
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
-    const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T) &&
-                        (PH == 1 || (n0 <= (EPTF + 1) / 2 * K2_T && n1 <= EPTF / 2 * K2_T));
+    const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T);
     // Flat pass (PHOLD, events in LDS, at most SPEC per lane; see below): the
     // states of the hosts of the lane's two due events are loaded as soon as
     // the records arrive.  Every lane's state reads have returned before the
@@ -2589,29 +2478,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     };
     static_assert(K2_T >= NSPEC, "one GSpec id per thread");
     if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
-    auto state_prefetch = [&]() __attribute__((always_inline)) {
-        if (flat) {  // uniform
-            const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
-            uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
-            l0 = l0 < d.L ? l0 : d.L - 1;  // a record past the count: any valid slot
-            l1 = l1 < d.L ? l1 : d.L - 1;
-            pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
-            pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-            if (rq_ok(1)) {  // most lanes have one event
-                pre_a1 = ld_stream2(&hsw[2 * (size_t)l1]);
-                pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
-            }
-        }
-    };
-#if SG_SORT_LDS >= 2
-    state_prefetch();  // as soon as the records arrive, under the row loads and the sort
-#endif
     if (stamp && tid == 0) stamp[20] = wait_stamp();
-#if SG_SORT_LDS >= 2
-    lds_barrier();  // the LDS zeroing; the row and state loads stay in flight
-#else
     __syncthreads();
-#endif
     if (in_lds) {
 #pragma unroll
         for (uint32_t q = 0; q < EPTF; ++q) {
@@ -2620,7 +2488,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
         }
-#if SG_SORT_LDS < 2
         if (flat) {  // uniform
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
             uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
@@ -2633,7 +2500,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
             }
         }
-#endif
         // the records are in registers now: re-defining them through asm keeps
         // the scatter below from waiting on the state prefetch (vmcnt(0))
 #pragma unroll
@@ -2648,11 +2514,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             else flag(d, OV_BUG);
         }
     }
-#if SG_SORT_LDS >= 1
-    lds_barrier();  // the counts; the state (and row) loads stay in flight under the scan
-#else
-    __syncthreads();
-#endif
+    __syncthreads();  // the counts (LDS-only barriers here measured no change: the waits are wave imbalance)
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
@@ -2666,7 +2528,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     uint64_t tot;
-    uint64_t run = block_excl_scan_2x32<(SG_SORT_LDS >= 1)>(mine, s16, &tot);
+    uint64_t run = block_excl_scan_2x32(mine, s16, &tot);
     for (uint32_t j = 0; j < per; ++j) {
         const uint32_t h = h0 + j * hs;
         if (h < HP) {
@@ -2677,11 +2539,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     const uint32_t nact = (uint32_t)tot;
-#if SG_SORT_LDS >= 1
-    lds_barrier();
-#else
     __syncthreads();
-#endif
     if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
     const uint32_t sbase = p * HP;  // the partition's first local slot
     // phase A's first host of every lane: state loads issued now, under the
@@ -2697,10 +2555,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
     }
-    if (tid < PH) {  // consumed; the next k_scatter's (or k_spec's / k_post's) gather refills them
-        d.pcnt[tid * d.P + p] = 0;
-        d.pcnt2[tid * d.P + p] = 0;
-    }
+    if (tid == 0) d.pcnt[p] = 0;  // consumed; the next k_scatter's gather refills it
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
 #pragma unroll
@@ -3122,7 +2977,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.bt = S + et;
             const uint32_t bsrc = (uint32_t)(ev.k >> SRC_SHIFT);
             const uint64_t bseq = ev.k & SEQ_MASK;
-            f.term = (SG_ABL & 32) ? f.bt ^ bseq : digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
+            f.term = digest_mix(pops0 + sc.rank, f.bt, bsrc, bseq);
             if (sc.rank + 1 == cnt) f.term += w23.x;  // the last event: the old digest + its term
             if (d.trace) {
                 const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
@@ -3177,25 +3032,20 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                             tn = E;
                             ++a.ctr[C_BUMPED];
                         }
-                        if (SG_ABL & 8) {
-                            a.emin = tn < a.emin ? tn : a.emin;
-                            if (!(SG_ABL & 16)) count_local(tn);
-                        } else if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)f.h << SRC_SHIFT) | sq)) {
-                            if (!(SG_ABL & 16)) count_local(tn);
-                        }
+                        if (stage_event(d, S, p, sh, a, dst, tn, ((uint64_t)f.h << SRC_SHIFT) | sq)) count_local(tn);
                     }
                 }
             } else {
                 ++a.ctr[C_NULL];
             }
             HostState* hp = d.hs + sbase + f.hl;
-            if ((f.flags & F_LAST) && !(SG_ABL & 2)) {  // the host's last event: its state after the round
+            if (f.flags & F_LAST) {  // the host's last event: its state after the round
                 const uint64_t evc = f.sq + (kept ? 1u : 0u);
                 ulonglong2* hw = reinterpret_cast<ulonglong2*>(hp);
                 st_rec(d.hs, (size_t)(sbase + f.hl) * 32, hs_w0(f.rng, f.h), hs_w1(f.pops_end, f.vh));
                 if (!(f.flags & F_MULTI)) st_rec(d.hs, (size_t)(sbase + f.hl) * 32 + 16, f.term, evc);
                 else hp->evc = evc;  // the digest after the barrier below
-            } else if (!(SG_ABL & 1)) {  // an earlier event of a multi-event host (ok: F_MULTI)
+            } else {  // an earlier event of a multi-event host (ok: F_MULTI)
                 atomicAdd(&s_dig[f.hl], (unsigned long long)f.term);
             }
         };
@@ -3226,17 +3076,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         // for that store too (vmcnt counts in order)
         uint32_t vd0 = 0, vd1 = 0, dst0 = 0, dst1 = 0;
         if constexpr (EXACT) {
-            if (SG_ABL & 4) {
-                dst0 = f0.g;
-                dst1 = f1.g;
-                vd0 = f0.g & 1023;
-                vd1 = f1.g & 1023;
-            } else {
-                const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
-                const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
-                near_resolve(d, f0.x, a0, b0, vd0, dst0);
-                near_resolve(d, f1.x, a1, b1, vd1, dst1);
-            }
+            const uint2 a0 = d.nearw[f0.g], b0 = d.nearw[f0.g + 1];
+            const uint2 a1 = d.nearw[f1.g], b1 = d.nearw[f1.g + 1];
+            near_resolve(d, f0.x, a0, b0, vd0, dst0);
+            near_resolve(d, f1.x, a1, b1, vd1, dst1);
         } else {
             const Probe pb0 = dst_probe(d, f0.g), pb1 = dst_probe(d, f1.g);
             dst0 = (f0.flags & F_OK) && (f0.flags & F_SND) ? dst_resolve(d, f0.x, f0.g, pb0, vd0) : 0u;
@@ -3548,9 +3391,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     lds_barrier();  // s_red
     if (stamp && tid == 0) stamp[14] = __builtin_amdgcn_s_memrealtime();
     // wave 0: the partials and the MIN accumulators (the last workgroup reads
-    // them).  SG_PART_LATE: issued after the reservations, so that wave 0's
-    // returning reservation adds do not queue (vmcnt is in order) behind the
-    // MIN atomics every workgroup sends to the same two words
+    // them), before the reservations (after them measured k_proc +1.0 us,
+    // profiles/r05/tick)
     auto partials = [&]() __attribute__((always_inline)) {
         if (tid < NPCTR + 2) {
             const int i = tid;
@@ -3566,9 +3408,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (i >= NPCTR && r != UINT64_MAX) atomicMin((unsigned long long*)&rs->xacc[i - NPCTR], (unsigned long long)r);
         }
     };
-    if (!SG_PART_LATE) partials();
+    partials();
     reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
-    if (SG_PART_LATE) partials();
     if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
@@ -3673,10 +3514,7 @@ struct Route {
 // One batch of up to SU events per thread (every thread of the workgroup
 // calls it): slot from the (partition, bucket) reservation cursor, chunk
 // from the reserving row's allocation; due events routed.  Returns nothing; carry min
-// and tombstones accumulate in smin / ntomb.  KEEP (k_spec, the window only
-// guessed): every event is written to its slot, a due one is also copied to
-// its partition, so k_post can discard the copies and gather the slots.
-template <bool KEEP>
+// and tombstones accumulate in smin / ntomb.
 __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint32_t x, uint32_t* s_cur, uint32_t* s_pc,
                                              uint32_t* s_pk, const bool (&v)[SU], const uint64_t (&t)[SU],
                                              const uint64_t (&k)[SU], const uint32_t (&dl)[SU], uint64_t& smin,
@@ -3705,7 +3543,7 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         pos[q] = v[q] ? atomicAdd(&s_cur[rb[q]], 1u) : 0u;
         due[q] = v[q] && ro.listed && t[q] < ro.E;
         const bool in_ret = ro.listed && b == ro.ret;
-        write[q] = v[q] && (KEEP || !due[q] || in_ret);  // fully due buckets: the slot stays empty
+        write[q] = v[q] && (!due[q] || in_ret);  // fully due buckets: the slot stays empty
         if (v[q] && !due[q] && in_ret) smin = t[q] < smin ? t[q] : smin;
         if (due[q]) atomicAdd(&s_pc[part_of(d, dl[q])], 1u);
     }
@@ -3720,8 +3558,8 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
     for (int q = 0; q < SU; ++q) {
         // no chunk only when the pool ran out (reserve_buckets flagged it)
         if (!write[q] || (pos[q] >> CH_SHIFT) >= d.NCH || id[q] >= d.NCH) continue;
-        Rec r{due[q] && !KEEP ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
-        ntomb += due[q] && !KEEP;
+        Rec r{due[q] ? TOMB : (((uint64_t)dl[q] << 40) | off[q]), k[q]};
+        ntomb += due[q];
         st_rec(d.pool, (((size_t)id[q] << CH_SHIFT) + (pos[q] & (CH - 1))) * 16, r.a, r.k);
     }
     if (!ro.listed) return;  // launch-uniform
@@ -3729,14 +3567,13 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
     // The barriers order LDS only: the calendar and partition stores drain
     // while the workgroup goes on (nothing in the launch reads them back).
     lds_barrier();
-    const uint32_t half = PH == 2 ? (blockIdx.x & 1u) : 0u, hoff = half * d.CAPH;  // partition half
-    uint32_t* pc = d.pcnt + (size_t)half * d.P;
+    uint32_t* pc = d.pcnt;
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) {
         const uint32_t c = s_pc[p];
         s_pk[p] = 0;
         if (c) {
             const uint32_t base = atomicAdd(&pc[p], c);
-            if (base + c > d.CAPH) flag(d, OV_PART);
+            if (base + c > d.CAPP) flag(d, OV_PART);
             s_pc[p] = base;
         }
     }
@@ -3746,8 +3583,8 @@ __device__ __forceinline__ void insert_batch(const Dev& d, const Route& ro, uint
         if (!due[q]) continue;
         const uint32_t p = part_of(d, dl[q]);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPH)
-            st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
+        if (slot < d.CAPP)
+            st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl[q] - p * d.HP) << 52) | (t[q] - ro.S), k[q]);
     }
     lds_barrier();
     for (uint32_t p = threadIdx.x; p < d.P; p += blockDim.x) s_pc[p] = 0;
@@ -3859,11 +3696,7 @@ __device__ __forceinline__ void refill_role(const Dev& d, uint32_t nx, uint64_t 
 }
 
 // mode: 0 one shard (after k_proc), 1 several shards (after the all-to-all; recv the
-// exchange blocks), 2 boot, 3 several shards, split step (k_post: k_spec
-// inserted the staged events, refilled the stashes and gathered the guessed
-// bucket beside the all-to-all; no insert or refill workgroups are launched,
-// and the gather workgroups take the list path only when the plan misses the
-// guess).  Every workgroup plans the step (step_view) from
+// exchange blocks), 2 boot.  Every workgroup plans the step (step_view) from
 // the state as the previous kernels left it, then arrives on a counter once its
 // reads of that state have returned; the last to arrive publishes the plan
 // (publish_step).  Nothing waits for anything: no workgroup depends on another
@@ -3878,14 +3711,13 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     __shared__ uint64_t s_gsw[3];                // gather: the GSpec header
     __shared__ uint32_t s_routed;
     __shared__ uint64_t s_rbase[MAXG];           // receive role: the received blocks' time bases
-    // role order [insert P][receive G3][gather][refill][rmin] over nv virtual
-    // workgroups; a split launch (mode 3) starts at the receive role.  SG_GFIRST
-    // dispatches the gather workgroups (the launch's long pole) first
-    const bool split = mode == 3;
-    const uint32_t off = split ? d.P : 0u, nv = gridDim.x + off;
+    // role order [insert P][receive G3][gather][refill][rmin] over the
+    // workgroups; SG_GFIRST dispatches the gather workgroups (the launch's long
+    // pole) first
+    const uint32_t nv = gridDim.x;
     const uint32_t g0 = d.P + (recv ? d.G3 : 0), gx = nv - 2;  // gather workgroups [g0, gx)
     const uint32_t ng = gx - g0, bi = blockIdx.x;
-    const uint32_t blk = SG_GFIRST ? (bi < ng ? g0 + bi : bi + off < gx ? off + (bi - ng) : bi + off) : bi + off;
+    const uint32_t blk = SG_GFIRST ? (bi < ng ? g0 + bi : bi < gx ? bi - ng : bi) : bi;
     const uint32_t R = d.R, tid = threadIdx.x;
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
@@ -4051,17 +3883,12 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         break;
     }
     if (blk == nv - 2) {
-        // the plan's tail: this launch's gather frees more behind it.  A split
-        // launch's k_spec did this already
-        if (!split) refill_role(d, sv.cur ^ 1, sv.tail, lds, st);
+        // the plan's tail: this launch's gather frees more behind it
+        refill_role(d, sv.cur ^ 1, sv.tail, lds, st);
         break;
     }
     if (blk >= g0) {
-        // split step: a hit keeps k_spec's gather; a miss gathers every written
-        // slot of the window into pcnt2 (k_spec's copies in pcnt are dropped)
-        if (ro.listed && !(split && sv.hit))
-            gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, s_gsw, st, split ? GM_FALLBACK : GM_PLAN,
-                              split ? d.pcnt2 : d.pcnt);
+        if (ro.listed) gather_role<K3_T>(d, sv, blk - g0, gx - g0, lds, s_gsw, st);
         if (st) st[3] = wait_stamp();
         break;
     }
@@ -4114,7 +3941,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
                     dl[q] = 0;
                 }
             }
-            insert_batch<false>(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
+            insert_batch(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
         }
         if (st) st[2] = wait_stamp();
         insert_finish(d, ro, smin, ntomb, s16);
@@ -4126,9 +3953,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // per (workgroup, partition)); the next k_proc stages the rest
     // (stage_received): no slot is reserved for an event about to be popped
     const uint32_t g3 = d.G3, w = blk - d.P;
-    const uint32_t half = PH == 2 ? (w & 1u) : 0u, hoff = half * d.CAPH;  // partition half
-    // where this window's counts are
-    uint32_t* pc = (split && !sv.hit ? d.pcnt2 : d.pcnt) + (size_t)half * d.P;
+    uint32_t* pc = d.pcnt;
     if (tid == 0) s_routed = 0;
     for (uint32_t p = threadIdx.x; p < d.P; p += K3_T) {
         s_pc[p] = 0;
@@ -4148,7 +3973,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         const uint32_t c = s_pc[p];
         if (c) {
             const uint32_t base = atomicAdd(&pc[p], c);
-            if (base + c > d.CAPH) flag(d, OV_PART);
+            if (base + c > d.CAPP) flag(d, OV_PART);
             s_pc[p] = base;
             atomicAdd(&s_routed, c);
         }
@@ -4162,7 +3987,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         if (!recv_event(d, recv, d.xrows, s_off, s_rbase, (uint32_t)i, t, k, dl) || t >= ro.E) continue;
         const uint32_t p = part_of(d, dl);
         const uint32_t slot = s_pc[p] + atomicAdd(&s_pk[p], 1u);
-        if (slot < d.CAPH) st_rec(d.part, ((size_t)p * d.CAPP + hoff + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
+        if (slot < d.CAPP) st_rec(d.part, ((size_t)p * d.CAPP + slot) * 16, ((uint64_t)(dl - p * d.HP) << 52) | (t - ro.S), k);
     }
     } while (0);
     // the last workgroup to arrive publishes the plan for the next kernels
@@ -4186,144 +4011,6 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     }
 #endif
     if (tid == 0 && ticket == gridDim.x - 1) publish_step(d, mode, sv, recv);
-}
-
-// ----------------------------------------------------------------- spec ----
-// Split step (several shards), launched on a second stream
-// after k_proc, beside the all-to-all: everything of k_scatter that does not
-// need the exchange's MIN.  Roles, in launch order:
-//   [0, G1)       the bucket the next window most likely is (GSpec: the
-//                 window after the executed one, one whole bucket) gathered
-//                 into the host partitions (pcnt) as that window, its chunks
-//                 into the ring behind the tail the plan will set;
-//   [G1, G1 + P)  partition p's staged events into their reserved slots, every
-//                 one of them (KEEP), those due in the guessed window also
-//                 copied into their host partitions;
-//   last          bk into the next step's bw half, the stashes refilled (the
-//                 ring usable up to the tail as it is: the last gather's
-//                 chunks join it only when the plan moves it).
-// Nothing here writes what the plan reads.  k_post plans the window from the
-// headers and keeps this launch's partitions when the window is the guessed
-// one (rs->spec_fold / spec_b, StepView::hit); otherwise it gathers every
-// written slot of the window into pcnt2, and these copies are never read.
-__global__ __launch_bounds__(K3_T) void k_spec(Dev d) {
-    __shared__ __align__(16) unsigned char lds[SCAT_LDS];
-    __shared__ StepView sv;              // the guessed window, as a plan would put it
-    __shared__ uint64_t s_rsw[RSW];      // the round state as k_proc left it
-    __shared__ uint64_t s_gsw[3];        // the GSpec header
-    const uint32_t G1 = d.G1, P = d.P, bi = blockIdx.x, tid = threadIdx.x, R = d.R;
-    const int role = bi < G1 ? 2 : bi < G1 + P ? 0 : 4;
-    const uint32_t blk = bi < G1 ? bi : bi - G1;
-    if (tid < 64) load_round_state(d, 0, nullptr, s_rsw, nullptr);
-    if ((tid >> 6) == 1) {
-        if (role == 2) gspec_load(d, blk, G1, s_gsw, (DueEnt*)(lds + GDE_OFF));
-        else if (tid - 64 < 3) s_gsw[tid - 64] = reinterpret_cast<const uint64_t*>(d.gspec)[tid - 64];
-    }
-    Rec pre[SU];
-    uint32_t pre_n = 0;
-    if (role == 0) {  // the partition's count, first SU events per thread, reservation bases
-        pre_n = d.rcnt[blk];
-        const Rec* src = d.loc + (size_t)blk * d.ECAP;  // ECAP >= SU * K3_T (host-checked)
-#pragma unroll
-        for (int q = 0; q < SU; ++q) pre[q] = ld_stream(&src[tid + q * K3_T]);
-        uint32_t* s_cur = (uint32_t*)lds;
-        uint32_t* s_pc = s_cur + RMAX;
-        const uint32_t* wb = d.wbase + (size_t)blk * R;
-        constexpr uint32_t WPT = RMAX / K3_T;
-        uint32_t wv[WPT];
-#pragma unroll
-        for (uint32_t q = 0; q < WPT; ++q) {
-            const uint32_t rb = tid + q * K3_T;
-            wv[q] = wb[rb < R ? rb : 0u];
-        }
-        for (uint32_t p = tid; p < P; p += K3_T) s_pc[p] = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < WPT; ++q)
-            if (tid + q * K3_T < R) s_cur[tid + q * K3_T] = wv[q];
-    }
-    lds_barrier();  // the round state, the guess's header (and ids) and the bases are in LDS
-    const RoundState* r = reinterpret_cast<const RoundState*>(s_rsw);
-    if (r->done) return;  // uniform
-    const uint64_t W = d.W, fold = r->fold, gb = s_gsw[1] & ((1ull << 48) - 1);
-    // the jump the plan takes if no shard lowers the discovery minimum (next_window)
-    uint64_t J = d.fixed_jump;
-    if (d.window_rule != SG_WINDOW_FIXED) {
-        J = r->jmin != UINT64_MAX ? r->jmin * SG_ONE_MS : r->next_min_jump;
-        J = J > 0 ? J : 10 * SG_ONE_MS;
-        if (d.runahead_min > 0 && J < d.runahead_min) J = d.runahead_min;
-    }
-    const uint32_t gnid = gspec_lo(s_gsw[2]).nid;
-    const bool guess = GSPEC_XS && s_gsw[0] == fold && r->phase == 0 && J == W && gnid <= GSPEC_N * G1;
-    if (tid == 0) {
-        const uint32_t cur = (uint32_t)(fold & 1);
-        sv.S = gb * W;
-        sv.E = (gb + 1) * W;
-        sv.bS = sv.bL = gb;
-        sv.ret = sv.pret = UINT64_MAX;
-        sv.fold = fold;
-        sv.cur = cur;
-        uint32_t tr = (uint32_t)r->tail_r + (uint32_t)r->nfree2[cur];  // the plan's tail (nfree <= NCH)
-        sv.tail_r = tr >= d.NCH ? tr - d.NCH : tr;
-        if (bi == 0) {
-            d.rs->spec_fold = guess ? fold : UINT64_MAX;
-            d.rs->spec_b = gb;
-        }
-    }
-    lds_barrier();
-    if (role == 2) {
-        if (guess) gather_role<K3_T>(d, sv, blk, G1, lds, s_gsw, nullptr, GM_SPEC, d.pcnt);
-        return;
-    }
-    if (role == 4) {
-        refill_role(d, (uint32_t)(fold & 1) ^ 1u, r->fl_tail, lds, nullptr);
-        return;
-    }
-    // insert role
-    const uint32_t n = pre_n;
-    if (!r->ins_local || n == 0) return;  // uniform
-    Route ro;
-    ro.listed = guess;
-    ro.cur = sv.cur;
-    ro.S = sv.S;
-    ro.E = sv.E;
-    ro.ret = UINT64_MAX;
-    ro.bS = r->bS;  // the executed window's first bucket: every staged event is at or after it
-    ro.bSW = ro.bS * W;
-    ro.bSr = (uint32_t)r->bS_r;
-    uint32_t* s_cur = (uint32_t*)lds;
-    uint32_t* s_pc = s_cur + RMAX;
-    uint32_t* s_pk = s_pc + PMAX;
-    const Rec* src = d.loc + (size_t)blk * d.ECAP;
-    const uint64_t S0 = r->ins_S;
-    uint64_t smin = UINT64_MAX, ntomb = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += K3_T * SU) {
-        Rec rr[SU];
-        if (i0 == 0) {  // uniform
-#pragma unroll
-            for (int q = 0; q < SU; ++q) rr[q] = pre[q];
-        } else {
-#pragma unroll
-            for (int q = 0; q < SU; ++q) {
-                const uint32_t i = i0 + tid + q * K3_T;
-                rr[q] = ld_stream(&src[i < n ? i : 0]);
-            }
-        }
-        bool v[SU];
-        uint64_t t[SU], k[SU];
-        uint32_t dl[SU];
-#pragma unroll
-        for (int q = 0; q < SU; ++q) {
-            v[q] = i0 + tid + q * K3_T < n;
-            t[q] = S0 + (rr[q].a & M40);
-            k[q] = rr[q].k;
-            dl[q] = (uint32_t)(rr[q].a >> 40);
-            if (v[q] && dl[q] >= d.L) {  // a staged record is always a local host: clamped, flagged
-                flag(d, OV_BUG);
-                dl[q] = 0;
-            }
-        }
-        insert_batch<true>(d, ro, blk % XS, s_cur, s_pc, s_pk, v, t, k, dl, smin, ntomb);
-    }
 }
 
 // ----------------------------------------------------------------- plan ----
@@ -4373,10 +4060,8 @@ __global__ __launch_bounds__(1024) void k_stats(Dev d, unsigned long long* pendi
         for (uint32_t x = 0; x < XS; ++x) pend += d.bk[(size_t)x * d.R + rb];
         pend -= d.btomb[rb];
     }
-    if (listed) {
-        const uint32_t* pc = rs->psel ? d.pcnt2 : d.pcnt;
-        for (uint32_t p = threadIdx.x; p < PH * d.P; p += 1024) pend += pc[p];
-    }
+    if (listed)
+        for (uint32_t p = threadIdx.x; p < d.P; p += 1024) pend += d.pcnt[p];
     for (int i = 0; i < NCTR; ++i) {
         const uint64_t t = block_sum(c[i], s16);
         if (threadIdx.x == 0) d.rs->ctr[i] = t;
@@ -4410,11 +4095,6 @@ struct sg_engine {
     int device;
     hipStream_t stream;
     bool own_stream;
-    // split step (d.split): k_spec runs on aux beside the all-to-all, ordered
-    // by ev_proc (after k_proc) and ev_spec (before k_post)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_proc = nullptr, ev_spec = nullptr;
-    bool split_same = false;  // SG_SPLIT=2 (measurement): k_spec on the engine stream, no fork / join
     bool booted;
     std::vector<void*> allocs;
     uint32_t* pcount_buf = nullptr;  // path packet counters, once enabled
@@ -4492,7 +4172,7 @@ static hipEvent_t get_event(sg_engine* e) {
 // around the kernel, so the measured duration is the kernel's.  The RCCL
 // exchange records them on the stream around the collective.
 template <typename F>
-static int timed_launch(sg_engine* e, int cls, F&& launch, hipStream_t on = nullptr) {
+static int timed_launch(sg_engine* e, int cls, F&& launch) {
     hipEvent_t a = nullptr, b = nullptr;
     const bool timed = e->timing && (e->timing_mask >> cls & 1u);
     if (timed) {
@@ -4503,7 +4183,7 @@ static int timed_launch(sg_engine* e, int cls, F&& launch, hipStream_t on = null
     launch(a, b);
     HIPCHK(hipGetLastError());
     if (e->debug_sync) {
-        const hipError_t err = hipStreamSynchronize(on ? on : e->stream);
+        const hipError_t err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) {
             static const char* names[SG_KCLASSES] = {"process", "insert", "plan", "gather", "exchange"};
             sg_set_error("kernel class %s (launch %llu) failed: %s", names[cls],
@@ -4674,14 +4354,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
         return SG_ERR_INVAL;
     }
     d.G1 = env_u32("SG_GATHER_GRID", 128);
-    // the split step for the step API (several shards, or one with exchange_cap
-    // set), SG_SPLIT=1: k_spec on a second stream beside the all-to-all.  Off by
-    // default: the fork and join between the streams cost more than the overlap
-    // saves (world-1 RCCL steps at 125k hosts 56-57 against 37.5 us, at 1M 81
-    // against 63.5 us; profiles/r05/split/).  SG_SPLIT=2 runs k_spec in stream
-    // order (measurement of the fork / join's cost)
-    const uint32_t split_env = env_u32z("SG_SPLIT", 0);
-    d.split = (G > 1 || p.exchange_cap) && split_env != 0 ? 1u : 0u;
     d.gspec_mode = env_u32z("SG_GSPEC", 1);
     d.xfence = 0;  // set per exchange link (sg_xlink_attach: SG_XFENCE, else fenced across devices)
     d.check = env_u32("SG_CHECK", 0) != 0;
@@ -4791,7 +4463,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     }
     const uint32_t per_host = std::max<uint32_t>(32, 2 * d.load);
     d.CAPP = d.HP * per_host;
-    d.CAPH = d.CAPP / PH;  // HP is a multiple of 16: CAPP divides; CAPH >= 1024 = K2_T
     d.ECAP = d.HP * per_host + 1024;
 
     sg_engine* e = new sg_engine();
@@ -4918,8 +4589,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     ALLOC(D.wbase, (size_t)(D.P + D.G3) * D.R);
     ALLOC(D.gspec, 1);
     ALLOC(D.tick, 8);
-    ALLOC(D.pcnt, PH * P);
-    ALLOC(D.pcnt2, PH * P);
+    ALLOC(D.pcnt, P);
     ALLOC(D.part, P * D.CAPP);
     ALLOC(D.part2, P * D.CAPP);
     ALLOC(D.extras, P * K2_T * XCAP);
@@ -4985,14 +4655,6 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
             return SG_ERR_HIP;
         }
         e->own_stream = true;
-    }
-    e->split_same = D.split && split_env == 2;
-    if (D.split && !e->split_same && (hipStreamCreateWithFlags(&e->aux, hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&e->ev_proc, hipEventDisableTiming) != hipSuccess ||
-                    hipEventCreateWithFlags(&e->ev_spec, hipEventDisableTiming) != hipSuccess)) {
-        sg_engine_destroy(e);
-        sg_set_error("sg_engine_create: the split step's stream / events could not be created");
-        return SG_ERR_HIP;
     }
     if (hipHostMalloc((void**)&e->h_rs, sizeof(RoundState), hipHostMallocDefault) != hipSuccess) {
         e->h_rs = nullptr;
@@ -5083,12 +4745,6 @@ int sg_engine_destroy(sg_engine* e) {
     if (e->recv_hold) (void)hipFree(e->recv_hold);
     for (hipEvent_t ev : e->batch_ev)
         if (ev) (void)hipEventDestroy(ev);
-    if (e->aux) {
-        (void)hipStreamSynchronize(e->aux);
-        (void)hipStreamDestroy(e->aux);
-    }
-    if (e->ev_proc) (void)hipEventDestroy(e->ev_proc);
-    if (e->ev_spec) (void)hipEventDestroy(e->ev_spec);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return SG_OK;
@@ -5136,7 +4792,7 @@ int sg_engine_boot(sg_engine* e) {
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
     HIPCHK(hipMemsetAsync(d.gspec, 0xFF, sizeof(GSpec), e->stream));  // no guess (fold UINT64_MAX)
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH),
-                                          std::max<uint32_t>(d.R, std::max<uint32_t>(d.P + d.G3, PH * d.P)));
+                                          std::max<uint32_t>(d.R, d.P + d.G3));
     hipLaunchKernelGGL(k_boot, dim3((n + 255) / 256), dim3(256), 0, e->stream, d);
     HIPCHK(hipGetLastError());
     // the first window's gather (k_scatter's gather role; nothing is staged
@@ -5166,39 +4822,17 @@ static int enqueue_process(sg_engine* e) {
 }
 
 // k_scatter: the staged events into the calendar, the next window planned and
-// gathered; several shards (recv): the received events due in it routed.  The
-// split step's k_post (after k_spec on the aux stream): the plan, the receive
-// role, the gather only when the guess missed, rmin.
+// gathered; several shards (recv): the received events due in it routed.
+// (Round 5 measured a split step — the window-independent half of k_scatter
+// on a second stream beside the all-to-all — at 56-57 against 37.5 us per
+// 125k-host step: the cross-stream fork and join cost more than the overlap
+// saved, profiles/r05/split/; it was removed in round 6.)
 static int enqueue_insert_plan(sg_engine* e, const int64_t* recv) {
     const Dev& d = e->d;
-    if (recv && d.split) {
-        if (!e->split_same) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_spec, 0));
-        return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
-            SG_LAUNCH(k_scatter, dim3(d.G3 + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv, 3);
-        });
-    }
     return timed_launch(e, SG_K_INSERT, [&](hipEvent_t a, hipEvent_t b) {
         SG_LAUNCH(k_scatter, dim3(d.P + (recv ? d.G3 : 0) + d.G1 + 2), dim3(K3_T), 0, e->stream, a, b, d, recv,
                   recv ? 1 : 0);
     });
-}
-
-// Split step: k_spec on the aux stream once k_proc is done, beside the
-// all-to-all the caller enqueues next on the engine stream.
-static int enqueue_spec(sg_engine* e) {
-    const Dev& d = e->d;
-    if (e->split_same)  // measurement: the same kernels in stream order, nothing beside the exchange
-        return timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {
-            SG_LAUNCH(k_spec, dim3(d.G1 + d.P + 1), dim3(K3_T), 0, e->stream, a, b, d);
-        });
-    HIPCHK(hipEventRecord(e->ev_proc, e->stream));
-    HIPCHK(hipStreamWaitEvent(e->aux, e->ev_proc, 0));
-    int rc = timed_launch(e, SG_K_GATHER, [&](hipEvent_t a, hipEvent_t b) {
-        SG_LAUNCH(k_spec, dim3(d.G1 + d.P + 1), dim3(K3_T), 0, e->aux, a, b, d);
-    }, e->aux);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev_spec, e->aux));
-    return SG_OK;
 }
 
 int sg_engine_enqueue_round(sg_engine* e) {
@@ -5316,7 +4950,6 @@ int sg_engine_enqueue_rounds(sg_engine* e, uint64_t n_rounds) {
 
 int sg_engine_sync(sg_engine* e) {
     if (!e) return SG_ERR_INVAL;
-    if (e->aux) HIPCHK(hipStreamSynchronize(e->aux));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (e->timing) harvest_timing(e);
     return SG_OK;
@@ -5537,7 +5170,6 @@ int sg_engine_step_send(sg_engine* e, int64_t* send) {
     rc = enqueue_process(e);
     e->d.xsend = nullptr;
     e->d.xrecv = nullptr;
-    if (rc == SG_OK && e->d.split) rc = enqueue_spec(e);
     return rc;
 }
 

@@ -539,13 +539,7 @@ def dist_roofline(rows, nk, steps, classes):
         us = dict(zip(classes, r[:nk]))
         pn, pb, sn, sb, xn, xb = r[nk:nk + 6]
         kp = kernel_line(pb / max(pn, 1), us["process"] * 1e-6 * steps / max(pn, 1))
-        # the split step's k_scatter is two launches: k_spec (gather class,
-        # beside the exchange) and k_post (insert class, after it); their
-        # algorithmic bytes are priced against their summed time
-        scat_us = us["insert"] + us.get("gather", 0.0)
-        ks = kernel_line(sb / max(sn, 1), scat_us * 1e-6 * steps / max(sn, 1))
-        if us.get("gather", 0.0) > 0:
-            ks.update(k_spec_us=us["gather"] * steps / max(sn, 1), k_post_us=us["insert"] * steps / max(sn, 1))
+        ks = kernel_line(sb / max(sn, 1), us["insert"] * 1e-6 * steps / max(sn, 1))
         per_rank.append({"k_proc": kp, "k_scatter": ks,
                          "exchange": {"avg_us": us["exchange"] * steps / xn if xn else None,
                                       "bytes_per_step": xb, "timed": bool(xn)}})

@@ -78,17 +78,15 @@ def test_inprocess_shards_match_oracle(world, kind, xcap):
         assert st[0]["exchange_steps"] > want["rounds"]
 
 
-@pytest.mark.parametrize("split,gspec", [("1", "1"), ("1", "0"), ("1", "2"), ("2", "1"), ("0", "1")])
-def test_split_step_modes_match_oracle(split, gspec, monkeypatch):
-    """The split step (k_spec inserts, refills and gathers the
-    guessed bucket on a second stream beside the exchange; k_post plans from
-    the headers and keeps that gather on a hit) against the oracle: with the
-    guess on (hits in steady rounds), off (SG_GSPEC=0: k_post's list path every
-    round), deliberately wrong (SG_GSPEC=2: k_spec gathers the bucket after the
-    right one, k_post must discard it), k_spec in stream order (SG_SPLIT=2) and
-    the unsplit step (SG_SPLIT=0, the default)."""
-    monkeypatch.setenv("SG_SPLIT", split)  # read when the engines are created
-    monkeypatch.setenv("SG_GSPEC", gspec)
+@pytest.mark.parametrize("gspec", ["1", "0", "2"])
+def test_sharded_gspec_modes_match_oracle(gspec, monkeypatch):
+    """The step path's gather with the GSpec guess on (hits in steady rounds),
+    off (SG_GSPEC=0: the list path every round) and deliberately wrong
+    (SG_GSPEC=2: the guess names the bucket after the right one, and the
+    gather must reject it and take the list path), 4 shards, against the
+    oracle.  (Round 5's split step, k_spec beside the exchange, was removed
+    in round 6: profiles/r05/split.)"""
+    monkeypatch.setenv("SG_GSPEC", gspec)  # read when the engines are created
     # V = 1024 as in configs[3]: the discovered minimum is 1 ms, so steady
     # windows are one whole bucket (V = 64 leaves 2-3 ms windows: no guess)
     cfg = phold.c4_config(n_hosts=60_000, end_time_s=0.15)

@@ -10,7 +10,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=${O:-gpurun_out/r06g2}
 mkdir -p $O
-for f in 1 0; do
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -n 2 $O/pytest.log
+for f in 1; do
   SG_XFENCE=$f timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
     tests/test_gpu_sharded.py -k xlink tests/test_gpu_dist.py > $O/pytest_f$f.log 2>&1 || { tail -40 $O/pytest_f$f.log; exit 1; }
   tail -n 1 $O/pytest_f$f.log
