@@ -324,6 +324,7 @@ struct Dev {
     uint32_t flat;                // PHOLD with the due events in LDS: one lane per due event (k_proc flat pass)
     uint32_t grec;                // gossip: hosts record their forwards for phases B / C (SG_GREC, default 1)
     uint32_t gskip_on;            // gossip: their draws after phase A from the jump-ahead table (SG_GSKIP)
+    uint32_t gflat;               // gossip: one lane per receipt records the forwards (SG_GFLAT, default 1)
     uint32_t dst_near;        // the uniform-position guess g is the drawn host or g + 1 for every x
                               // (host-checked): records g and g + 1 settle every draw
     uint32_t check;           // SG_CHECK=1: k_scatter's publisher re-derives the sent headers' MIN terms (debug)
@@ -1555,6 +1556,7 @@ __device__ __forceinline__ SegScan seg_scan(const Rec* seg, uint32_t cnt, uint64
 #endif
 constexpr uint32_t FLAT_CMAX = SG_FLAT_CMAX;
 constexpr uint32_t NULL_DRAW = 1u << 31;  // s_n mark: a flat-pass host whose skip-ahead miscounted
+constexpr uint32_t GF_DONE = 1u << 30;    // s_n mark: a host the gossip flat pass recorded (s_n = mark | j)
 __device__ __forceinline__ bool flat_ok(const Dev& d, uint32_t cnt, const SegScan& s, bool self_possible, uint64_t S,
                                         uint64_t E, uint32_t vh) {
     if (s.boot || cnt > FLAT_CMAX || (cnt > 1 && d.pair_fmt != PAIR_DELAY)) return false;
@@ -2597,8 +2599,29 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // Send records (phase A writes, phase B resolves, phase C commits) live in
     // the event image's unused tail while they fit, in HBM beyond it: phases
     // B and C then read them at LDS latency.
+    // gossip (configs[4]): hosts take the record path (phases B / C resolve
+    // their sends one lane each) while the message ids fit the record's 12 bits
+    // and the host's seen set GMW registers
+    constexpr uint32_t GMW = 4;
+    // (the flat pass is PHOLD's: its instantiations carry none of this)
+    const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
+                            d.mw <= GMW && d.grec;
+    // lossy links (phases B and C apart): phase A leaves the record path's
+    // draws to a pass of one lane per send (send s of a host: draws 2s, 2s + 1
+    // after its state, by the jump-ahead table); a draw selecting no host
+    // marks the host, which one lane then redraws in order (skip_fix)
+    const bool gskip = gossip_rec && d.skip && d.pair_fmt != PAIR_DELAY && d.nskip > d.load * GMW * 32 &&
+                       d.gskip_on;
+    // the gossip flat pass (below): one lane per receipt, up to GFE per lane,
+    // its per-receipt words (a digest term and a first-receipt flag, 12 B) in
+    // the event image's last records
+    constexpr uint32_t GFE = 2;
+    const uint32_t gfrec = (3 * n + 3) / 4;
+    const bool gflat = gskip && in_lds && d.gflat && n <= GFE * K2_T && d.EVL >= n + gfrec;
+    uint64_t* s_et = reinterpret_cast<uint64_t*>(s_ev + d.EVL) - (gflat ? n : 0u);
+    uint32_t* s_ef = reinterpret_cast<uint32_t*>(s_et) - (gflat ? n : 0u);
     Rec* s_snd = s_ev + (in_lds ? n : 0u);
-    const uint32_t lcap = d.snd_lds ? (in_lds ? d.EVL - n : d.EVL) : 0u;
+    const uint32_t lcap = d.snd_lds ? (in_lds ? d.EVL - n - (gflat ? gfrec : 0u) : d.EVL) : 0u;
     auto sget = [&](uint32_t i) __attribute__((always_inline)) { return i < lcap ? s_snd[i] : snd[i]; };
     auto sput = [&](uint32_t i, const Rec& r) __attribute__((always_inline)) {
         if (i < lcap) s_snd[i] = r;
@@ -2619,19 +2642,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         if (!bin_time(d, t, bS, bSW, bSr, s_bc, s_bm)) horizon = true;
     };
     uint32_t nacta = nact;  // the hosts phase A takes: s_act[0, nacta)
-    // gossip (configs[4]): hosts take the record path (phases B / C resolve
-    // their sends one lane each) while the message ids fit the record's 12 bits
-    // and the host's seen set GMW registers
-    constexpr uint32_t GMW = 4;
-    // (the flat pass is PHOLD's: its instantiations carry none of this)
-    const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
-                            d.mw <= GMW && d.grec;
-    // lossy links (phases B and C apart): phase A leaves the record path's
-    // draws to a pass of one lane per send (send s of a host: draws 2s, 2s + 1
-    // after its state, by the jump-ahead table); a draw selecting no host
-    // marks the host, which one lane then redraws in order (skip_fix)
-    const bool gskip = gossip_rec && d.skip && d.pair_fmt != PAIR_DELAY && d.nskip > d.load * GMW * 32 &&
-                       d.gskip_on;
 
     uint32_t gsw[GMW];
     auto gword = [](const uint32_t (&w)[GMW], uint32_t i) __attribute__((always_inline)) {
@@ -2656,7 +2666,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             HostCtx c;
             const bool st0 = stamp && tid == 0 && q == 0;
             if (stamp && tid == 0 && q == 1) stamp[23] = __builtin_amdgcn_s_memrealtime();
-            if (j < nacta) {
+            if (j < nacta && !(s_n[s_act[j]] & GF_DONE)) {  // (the gossip flat pass's hosts are done)
                 s_sb[j] = UINT32_MAX;
                 const uint32_t hl = s_act[j];
                 cnt = s_n[hl] & ~NULL_DRAW;
@@ -3119,6 +3129,193 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         ser = nacta != 0;
         if (ser) __syncthreads();  // phase A reuses s_vh / s_sb
         if (stf) stamp[30] = __builtin_amdgcn_s_memrealtime();
+    }
+    // ---- gossip flat pass (configs[4]): one lane per receipt, where phase A
+    // takes one lane per host (the heaviest host of a wave sets its time, and
+    // ~400 hosts fill 6 of 16 waves).  A receipt's place in its host's order
+    // is independent of the others once it knows (orc.c execute_gossip,
+    // worker.c:268-273, event.c:38):
+    //   its rank in the host's pop order (event_compare over the host's due
+    //   events in LDS), hence its trace position pops + rank and digest term;
+    //   whether it is the host's first receipt of its message (not in the seen
+    //   set as the round found it, no lower-ranked receipt of it) — a first
+    //   receipt forwards to `load` peers;
+    //   the forwards ranked before it (load x the first receipts of lower
+    //   rank), hence its sends' indices: send s of the host draws 2s, 2s + 1
+    //   after the host's state (the jump-ahead table, drawn after this pass as
+    //   on the record path).
+    // Pass 1 ranks and classifies (s_ef); pass 2: each host's rank-0 lane
+    // reserves its records (a header and load x firsts sends, exactly the
+    // record path's layout) and publishes them through s_n / s_c; pass 3
+    // writes the send records, and the host's last lane its state (rng after
+    // the draws, pops, digest) and seen set.  A host with a boot event, or
+    // one whose self event could land inside the window (host_single.c:
+    // 237-267), keeps phase A's sequential body (s_nser counts them).
+    if constexpr (!FLAT) {
+        if (gflat) {  // uniform
+            if (tid == 0) s_nser = 0;
+            // (kept small: two are live across the passes; what only a host's
+            // rank-0 or last lane needs is loaded there)
+            struct GfEv {
+                Rec ev;
+                uint32_t hl, cnt, start, rank;
+                uint32_t rng0, h, vh, seenw;
+                uint64_t pops0;
+                bool valid, ok, first;
+            };
+            GfEv g[GFE];
+            const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {  // loads first, every one unconditional (clamped)
+                const uint32_t i = tid + q * K2_T;
+                g[q].valid = i < n;
+                g[q].ev = s_ev[g[q].valid ? i : 0u];
+                g[q].hl = (uint32_t)(g[q].ev.a >> 52);
+                const uint32_t hl = g[q].hl < HP ? g[q].hl : 0u, lh = sbase + hl < d.L ? sbase + hl : 0u;
+                const ulonglong2 w01 = hsw[2 * (size_t)lh];
+                g[q].rng0 = (uint32_t)w01.x;
+                g[q].h = (uint32_t)(w01.x >> 32);
+                g[q].pops0 = w01.y & M48;
+                g[q].vh = (uint32_t)(w01.y >> 48);
+                const uint32_t mw = (uint32_t)(g[q].ev.k & 0xFFFFu) >> 5;  // the message's seen word
+                g[q].seenw = d.seen[(size_t)lh * d.mw + (mw < d.mw ? mw : 0u)];
+            }
+            // pass 1: rank, first receipt, the host's eligibility
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {
+                GfEv& f = g[q];
+                f.ok = f.first = false;
+                f.rank = 0;
+                if (!f.valid) continue;
+                if (f.hl >= HP) {
+                    flag(d, OV_BUG);
+                    f.valid = false;
+                    continue;
+                }
+                f.cnt = s_n[f.hl] & ~NULL_DRAW;
+                f.start = s_c[f.hl] - f.cnt;
+                const uint64_t et = f.ev.a & M52, ek = f.ev.k;
+                const uint32_t msg = (uint32_t)(ek & 0xFFFFu);
+                uint64_t tmin = et;
+                bool boot = (ek & SEQ_MASK) == 0, dup = false;
+                for (uint32_t k = 0; k < f.cnt; ++k) {
+                    const Rec r = s_ev[f.start + k];
+                    const uint64_t rt = r.a & M52;
+                    const bool lt = key_less(rt, r.k, et, ek);
+                    f.rank += lt ? 1u : 0u;
+                    dup |= lt & ((uint32_t)(r.k & 0xFFFFu) == msg);
+                    tmin = rt < tmin ? rt : tmin;
+                    boot |= (r.k & SEQ_MASK) == 0;
+                }
+                f.ok = !boot && !(self_possible && S + tmin + d.vself[f.vh] < E);
+                f.first = f.ok && !dup && !(f.seenw & (1u << (msg & 31)));
+                // by rank: the host's receipts in pop order
+                s_ef[f.start + f.rank] = f.first ? 1u : 0u;
+                s_et[f.start + f.rank] = digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
+                                                    (ek & SEQ_MASK) >> d.msg_shift);
+            }
+            lds_barrier();
+            // pass 2: each host's rank-0 lane reserves its records
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {
+                const GfEv& f = g[q];
+                if (!f.valid || f.rank != 0) continue;
+                if (!f.ok) {
+                    atomicAdd(&s_nser, 1u);  // phase A's sequential body takes it
+                    continue;
+                }
+                uint32_t nf = 0;
+                for (uint32_t k = 0; k < f.cnt; ++k) nf += s_ef[f.start + k];
+                // the host's active index: s_act is ascending
+                uint32_t lo = 0, hi = nact;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_act[mid] < f.hl) lo = mid + 1;
+                    else hi = mid;
+                }
+                const uint32_t j = lo, ns = nf * d.load;
+                const uint32_t base = atomicAdd(&s_nsend, ns + 1);
+                const bool bad = j >= nact || s_act[j < nact ? j : 0u] != f.hl || ns > 0xFFFFu ||
+                                 base + ns + 1 > d.ECAP;
+                if (bad) {
+                    a.overflow = true;
+                    if (j < nact) s_sb[j] = UINT32_MAX;
+                } else {
+                    s_sb[j] = base;
+                    s_vh[j] = f.vh | (ns << 16);
+                    const uint64_t evc0 = d.hs[sbase + f.hl].evc;
+                    sput(base, Rec{evc0 | ((uint64_t)f.rng0 << 32), HDR_REC | ((uint64_t)j << 32) | f.h});
+                }
+                ++a.ctr[C_ACTIVE];
+                s_c[f.hl] = bad ? UINT32_MAX : base;
+                s_n[f.hl] = GF_DONE | j;
+            }
+            lds_barrier();
+            // pass 3: the sends of every first receipt, the trace, and the
+            // host's state by its last lane
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {
+                const GfEv& f = g[q];
+                if (!f.valid || !f.ok) continue;
+                const uint32_t base = s_c[f.hl], j = s_n[f.hl] & 0xFFFFu;
+                const uint64_t trel = f.ev.a & M52, bt = S + trel;
+                const uint32_t bsrc = (uint32_t)(f.ev.k >> SRC_SHIFT);
+                const uint64_t bseq = (f.ev.k & SEQ_MASK) >> d.msg_shift;
+                if (d.trace) {
+                    const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
+                    if (ts < d.trace_cap) {
+                        sg_trace_rec tr;
+                        tr.time = bt;
+                        tr.seq = bseq;
+                        tr.host = f.h;
+                        tr.src = bsrc;
+                        tr.pos = f.pops0 + f.rank;
+                        d.trace[ts] = tr;
+                    } else {
+                        a.overflow = true;
+                    }
+                }
+                ++a.ctr[C_POPS];
+                if (base == UINT32_MAX) continue;  // overflow (flagged)
+                if (f.first) {
+                    uint32_t fb = 0;  // first receipts before this one
+                    for (uint32_t k = 0; k < f.rank; ++k) fb += s_ef[f.start + k];
+                    const uint64_t msg = f.ev.k & 0xFFFu;
+                    for (uint32_t m = 0; m < d.load; ++m) {
+                        const uint32_t si = fb * d.load + m;  // the send's index in the host's list
+                        sput(base + 1 + si, Rec{((uint64_t)j << 52) | (msg << 40) | trel,
+                                                (uint64_t)f.rng0 | ((uint64_t)si << 32)});
+                    }
+                    a.ctr[C_SENDS] += d.load;
+                }
+                if (f.rank + 1 != f.cnt) continue;
+                // the host's last receipt: its state after the round (the
+                // counter comes with phase C, from the header record)
+                const uint32_t lh = sbase + f.hl;
+                uint32_t nf = 0, sw[GMW];
+                uint64_t dig = d.hs[lh].digest;
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) sw[w] = w < d.mw ? d.seen[(size_t)lh * d.mw + w] : 0u;
+                for (uint32_t k = 0; k < f.cnt; ++k) {
+                    dig += s_et[f.start + k];
+                    nf += s_ef[f.start + k];
+                    const uint32_t m = (uint32_t)(s_ev[f.start + k].k & 0xFFFFu);
+                    gset(sw, m >> 5, gword(sw, m >> 5) | (1u << (m & 31)));
+                }
+                const uint32_t ns = nf * d.load;
+                if (ns >= d.nskip) flag(d, OV_BUG | GSK_A);
+                const uint2 sk = d.skip[ns < d.nskip ? ns : 0u];
+                HostState* hp = d.hs + lh;
+                reinterpret_cast<ulonglong2*>(hp)[0] =
+                    make_ulonglong2(hs_w0(sk.x * f.rng0 + sk.y, f.h), hs_w1(f.pops0 + f.cnt, f.vh));
+                hp->digest = dig;
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w)
+                    if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = sw[w];
+            }
+            lds_barrier();  // s_nsend, s_nser, the records
+            ser = s_nser != 0;
+        }
     }
     if (!ser) {
     } else if (in_lds) phase_a(std::true_type{});
@@ -4536,6 +4733,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     D.flat = env_u32z("SG_FLAT", 1) != 0 && D.workload == SG_WORKLOAD_PHOLD;
     D.grec = env_u32z("SG_GREC", 1) != 0 ? 1u : 0u;
     D.gskip_on = env_u32z("SG_GSKIP", 1) != 0 ? 1u : 0u;
+    D.gflat = env_u32z("SG_GFLAT", 1) != 0 ? 1u : 0u;
     // near guess: with the weights rule, every host's x range [wt[i-1]+1, wt[i]]
     // must map to i - 1 or i under the (monotone) guess, so checking both ends
     // suffices; the floor rule's guess is its answer
