@@ -3154,17 +3154,20 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if constexpr (!FLAT) {
         if (gflat) {  // uniform
             if (tid == 0) s_nser = 0;
-            // (kept small: two are live across the passes; what only a host's
-            // rank-0 or last lane needs is loaded there)
+            // (kept small: two are live across the passes; the host's digest,
+            // counter and seen words go to LDS at the end of pass 1, from the
+            // lane that finds itself rank 0)
             struct GfEv {
                 Rec ev;
                 uint32_t hl, cnt, start, rank;
-                uint32_t rng0, h, vh, seenw;
+                uint32_t rng0, h, vh;
                 uint64_t pops0;
                 bool valid, ok, first;
             };
             GfEv g[GFE];
+            uint32_t seenw[GFE];
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
+            const bool stf = stamp && tid == 0;
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {  // loads first, every one unconditional (clamped)
                 const uint32_t i = tid + q * K2_T;
@@ -3178,7 +3181,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 g[q].pops0 = w01.y & M48;
                 g[q].vh = (uint32_t)(w01.y >> 48);
                 const uint32_t mw = (uint32_t)(g[q].ev.k & 0xFFFFu) >> 5;  // the message's seen word
-                g[q].seenw = d.seen[(size_t)lh * d.mw + (mw < d.mw ? mw : 0u)];
+                seenw[q] = d.seen[(size_t)lh * d.mw + (mw < d.mw ? mw : 0u)];
             }
             // pass 1: rank, first receipt, the host's eligibility
 #pragma unroll
@@ -3208,17 +3211,31 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     boot |= (r.k & SEQ_MASK) == 0;
                 }
                 f.ok = !boot && !(self_possible && S + tmin + d.vself[f.vh] < E);
-                f.first = f.ok && !dup && !(f.seenw & (1u << (msg & 31)));
+                f.first = f.ok && !dup && !(seenw[q] & (1u << (msg & 31)));
                 // by rank: the host's receipts in pop order
                 s_ef[f.start + f.rank] = f.first ? 1u : 0u;
                 s_et[f.start + f.rank] = digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
                                                     (ek & SEQ_MASK) >> d.msg_shift);
             }
+            if (stf) stamp[16] = wait_stamp();
             lds_barrier();
-            // pass 2: each host's rank-0 lane reserves its records
+            // pass 2: each host's rank-0 lane reserves its records, writes the
+            // header, and issues the load of its state after the draws (the
+            // jump-ahead entry for its sends), used in pass 3
+            uint2 skx[GFE];
+            ulonglong2 w23x[GFE];
+            uint32_t swx[GFE][GMW];
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
                 const GfEv& f = g[q];
+                // the host's {digest, evc} and seen words, for its rank-0 lane in
+                // pass 3 (loaded by every lane: a select of loads, not a
+                // conditional load, which would wait where it is issued)
+                const uint32_t lh = sbase + (f.hl < HP ? f.hl : 0u) < d.L ? sbase + (f.hl < HP ? f.hl : 0u) : 0u;
+                w23x[q] = reinterpret_cast<const ulonglong2*>(d.hs + lh)[1];
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) swx[q][w] = d.seen[(size_t)lh * d.mw + (w < d.mw ? w : 0u)];
+                skx[q] = d.skip[0];
                 if (!f.valid || f.rank != 0) continue;
                 if (!f.ok) {
                     atomicAdd(&s_nser, 1u);  // phase A's sequential body takes it
@@ -3234,6 +3251,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     else hi = mid;
                 }
                 const uint32_t j = lo, ns = nf * d.load;
+                if (ns >= d.nskip) flag(d, OV_BUG | GSK_A);
+                skx[q] = d.skip[ns < d.nskip ? ns : 0u];  // in flight until pass 3
                 const uint32_t base = atomicAdd(&s_nsend, ns + 1);
                 const bool bad = j >= nact || s_act[j < nact ? j : 0u] != f.hl || ns > 0xFFFFu ||
                                  base + ns + 1 > d.ECAP;
@@ -3243,32 +3262,29 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 } else {
                     s_sb[j] = base;
                     s_vh[j] = f.vh | (ns << 16);
-                    const uint64_t evc0 = d.hs[sbase + f.hl].evc;
-                    sput(base, Rec{evc0 | ((uint64_t)f.rng0 << 32), HDR_REC | ((uint64_t)j << 32) | f.h});
                 }
                 ++a.ctr[C_ACTIVE];
                 s_c[f.hl] = bad ? UINT32_MAX : base;
                 s_n[f.hl] = GF_DONE | j;
             }
+            if (stf) stamp[17] = wait_stamp();
             lds_barrier();
-            // pass 3: the sends of every first receipt, the trace, and the
-            // host's state by its last lane
+            // pass 3: the sends of every first receipt and the trace; the
+            // host's header and state by its rank-0 lane
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
                 const GfEv& f = g[q];
                 if (!f.valid || !f.ok) continue;
                 const uint32_t base = s_c[f.hl], j = s_n[f.hl] & 0xFFFFu;
                 const uint64_t trel = f.ev.a & M52, bt = S + trel;
-                const uint32_t bsrc = (uint32_t)(f.ev.k >> SRC_SHIFT);
-                const uint64_t bseq = (f.ev.k & SEQ_MASK) >> d.msg_shift;
                 if (d.trace) {
                     const uint64_t ts = atomicAdd((unsigned long long*)&rs->trace_len, 1ULL);
                     if (ts < d.trace_cap) {
                         sg_trace_rec tr;
                         tr.time = bt;
-                        tr.seq = bseq;
+                        tr.seq = (f.ev.k & SEQ_MASK) >> d.msg_shift;
                         tr.host = f.h;
-                        tr.src = bsrc;
+                        tr.src = (uint32_t)(f.ev.k >> SRC_SHIFT);
                         tr.pos = f.pops0 + f.rank;
                         d.trace[ts] = tr;
                     } else {
@@ -3288,32 +3304,33 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     }
                     a.ctr[C_SENDS] += d.load;
                 }
-                if (f.rank + 1 != f.cnt) continue;
-                // the host's last receipt: its state after the round (the
-                // counter comes with phase C, from the header record)
+                if (f.rank != 0) continue;
+                // the host's rank-0 lane: its header and its state after the
+                // round (the counter comes with phase C, from the header)
                 const uint32_t lh = sbase + f.hl;
-                uint32_t nf = 0, sw[GMW];
-                uint64_t dig = d.hs[lh].digest;
+                HostState* hp = d.hs + lh;
+                const ulonglong2 w23 = w23x[q];  // {digest, evc}
+                uint32_t sw[GMW];
 #pragma unroll
-                for (uint32_t w = 0; w < GMW; ++w) sw[w] = w < d.mw ? d.seen[(size_t)lh * d.mw + w] : 0u;
+                for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w];
+                uint64_t dig = 0;
                 for (uint32_t k = 0; k < f.cnt; ++k) {
                     dig += s_et[f.start + k];
-                    nf += s_ef[f.start + k];
                     const uint32_t m = (uint32_t)(s_ev[f.start + k].k & 0xFFFFu);
                     gset(sw, m >> 5, gword(sw, m >> 5) | (1u << (m & 31)));
                 }
-                const uint32_t ns = nf * d.load;
-                if (ns >= d.nskip) flag(d, OV_BUG | GSK_A);
-                const uint2 sk = d.skip[ns < d.nskip ? ns : 0u];
-                HostState* hp = d.hs + lh;
+                sput(base, Rec{w23.y | ((uint64_t)f.rng0 << 32), HDR_REC | ((uint64_t)j << 32) | f.h});
+                const uint2 sk = skx[q];
                 reinterpret_cast<ulonglong2*>(hp)[0] =
                     make_ulonglong2(hs_w0(sk.x * f.rng0 + sk.y, f.h), hs_w1(f.pops0 + f.cnt, f.vh));
-                hp->digest = dig;
+                hp->digest = w23.x + dig;
 #pragma unroll
                 for (uint32_t w = 0; w < GMW; ++w)
                     if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = sw[w];
             }
+            if (stf) stamp[18] = wait_stamp();
             lds_barrier();  // s_nsend, s_nser, the records
+            if (stf) stamp[19] = stamp[30] = __builtin_amdgcn_s_memrealtime();
             ser = s_nser != 0;
         }
     }
@@ -3577,7 +3594,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     const int lane = tid & 63, wid = tid >> 6;
     uint64_t v[NPCTR + 2];
 #pragma unroll
-    for (int i = 0; i < NPCTR; ++i) v[i] = wave_sum_u32(a.ctr[i]);
+    // a wave's sum as a signed 32-bit value: a lane's counter may be negative
+    // (the gossip flat pass counts a host's sends on its receipts' lanes, the
+    // null-draw fix takes them back on the host's lane), the wave's never is
+    for (int i = 0; i < NPCTR; ++i) v[i] = (uint64_t)(int64_t)(int32_t)wave_sum_u32(a.ctr[i]);
     v[NPCTR] = wave_min(a.emin);
     v[NPCTR + 1] = wave_min(a.jmin);
     if (lane == 0) {
