@@ -2644,15 +2644,21 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     uint32_t nacta = nact;  // the hosts phase A takes: s_act[0, nacta)
 
     uint32_t gsw[GMW];
+    // A seen word by a runtime index, as selects of register values: left to
+    // itself the compiler turned the select chain into an indexed private
+    // array, i.e. a scratch store of the four words and a scratch load per
+    // access — a memory round trip per receipt in phase A's gossip loops.
+    // opaque() keeps every word a register value.
+    static_assert(GMW == 4, "four seen words");
     auto gword = [](const uint32_t (&w)[GMW], uint32_t i) __attribute__((always_inline)) {
-        uint32_t v = w[0];
-#pragma unroll
-        for (uint32_t k = 1; k < GMW; ++k) v = i == k ? w[k] : v;
-        return v;
+        const uint32_t w0 = opaque(w[0]), w1 = opaque(w[1]), w2 = opaque(w[2]), w3 = opaque(w[3]);
+        return i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
     };
     auto gset = [](uint32_t (&w)[GMW], uint32_t i, uint32_t v) __attribute__((always_inline)) {
-#pragma unroll
-        for (uint32_t k = 0; k < GMW; ++k) w[k] = i == k ? v : w[k];
+        w[0] = opaque(i == 0 ? v : w[0]);
+        w[1] = opaque(i == 1 ? v : w[1]);
+        w[2] = opaque(i == 2 ? v : w[2]);
+        w[3] = opaque(i == 3 ? v : w[3]);
     };
     auto phase_a = [&](auto seg_in_lds) __attribute__((always_inline)) {
         Rec* segs = decltype(seg_in_lds)::value ? s_ev : part2;
