@@ -318,6 +318,7 @@ struct Dev {
     uint32_t lds_rows;        // k_proc stages its partition's path rows in LDS
     const void* prow;         // [V][V] full row-major records (4 or 8 B) the rows are staged from
     uint32_t rows_max, row_off;  // rows per partition at most; their LDS offset
+    uint32_t row_pieces;         // 16-B pieces the LDS rows region holds (whole 1 KB wave pieces)
     bool snd_lds;                // k_proc's send records in LDS while they fit
     uint32_t light_max, light_q;  // inline bodies: hosts with <= light_max sends, lanes' first light_q hosts
     uint32_t rec_all;             // a partition with due events + active hosts <= rec_all records every host
@@ -2295,6 +2296,17 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_TICK8
 #define SG_TICK8 1
 #endif
+// SG_STATE_LATE: the flat pass's host-state loads issued after the sort's
+// scan (1) instead of with the histogram (0): a spill reload in the scan
+// waits vmcnt(0), i.e. for those loads, when they are already in flight
+#ifndef SG_STATE_LATE
+#define SG_STATE_LATE 0
+#endif
+// SG_ROWS_GLDS: k_proc's path rows go global -> LDS by global_load_lds (1),
+// or through 8 VGPRs per lane held through the sort (0)
+#ifndef SG_ROWS_GLDS
+#define SG_ROWS_GLDS 1
+#endif
 // FLAT: d.flat (PHOLD): a partition with at most SPEC due events per lane runs
 // the flat pass; its event image holds only those (EPTF registers per lane), a
 // bigger one sorts through part2 and runs phase A.
@@ -2457,13 +2469,32 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // registers, every load unconditional so the sort below waits for none of
     // them, and stored into LDS after the scatter
     constexpr uint32_t RQ = (32u << 10) / 4 / K2_T;
-    uint32_t vlo = 0, rw[RQ], nwords = 0;
+    uint32_t vlo = 0, nwords = 0;
+#if !SG_ROWS_GLDS
+    uint32_t rw[RQ];
+#endif
     if constexpr (ROWS) {
         vlo = v_first;
         const uint32_t nrow = v_last - vlo + 1;
         const uint32_t wpe = d.pair_fmt == PAIR_NARROW ? 2u : 1u;  // words per record
         nwords = (nrow < d.rows_max ? nrow : d.rows_max) * d.V * wpe;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(d.prow) + (size_t)vlo * d.V * wpe;
+#if SG_ROWS_GLDS
+        // straight into LDS (global_load_lds_dwordx4, 16 B a lane, each wave
+        // instruction 1 KB lane-linear): no VGPRs held through the sort.  The
+        // LDS region holds whole 1 KB wave pieces (row_pieces); pieces past the
+        // rows re-read their last one (prow is padded to a whole piece)
+        const uint32_t lastp = (nwords + 3) / 4 - 1;
+#pragma unroll
+        for (uint32_t q = 0; q < RQ / 4; ++q) {
+            const uint32_t w0 = (tid & ~63u) + q * K2_T;  // the wave's first piece
+            if (w0 >= d.row_pieces) continue;                // wave-uniform
+            const uint32_t i = tid + q * K2_T, ic = i < lastp ? i : lastp;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * (size_t)ic),
+                                             (__attribute__((address_space(3))) void*)(dyn + d.row_off + (size_t)w0 * 16),
+                                             16, 0, 0);
+        }
+#else
         // clamped to the partition's own rows (nwords >= V): the loads past
         // them re-read its last word instead of fetching rows nobody uses
         const uint32_t last = nwords - 1;
@@ -2472,6 +2503,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t i = tid + q * K2_T;
             rw[q] = src[i < last ? i : last];
         }
+#endif
         if (nrow > d.rows_max && tid == 0) flag(d, OV_BUG);  // the host sized rows_max
     }
     auto pair_of = [&](uint32_t sv, uint32_t dv, bool wj) __attribute__((always_inline)) {
@@ -2481,15 +2513,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     static_assert(K2_T >= NSPEC, "one GSpec id per thread");
     if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
     if (stamp && tid == 0) stamp[20] = wait_stamp();
-    __syncthreads();
-    if (in_lds) {
-#pragma unroll
-        for (uint32_t q = 0; q < EPTF; ++q) {
-            if (!rq_ok(q)) continue;
-            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
-            if (hl < HP) atomicAdd(&s_n[hl], 1u);
-            else flag(d, OV_BUG);
-        }
+    // the flat pass's host states, loaded as soon as the records are in (the
+    // histogram), or (SG_STATE_LATE) after the scan, under the scatter only
+    auto flat_prefetch = [&]() __attribute__((always_inline)) {
         if (flat) {  // uniform
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
             uint32_t l0 = p * HP + (uint32_t)(rr[0].a >> 52), l1 = p * HP + (uint32_t)(rr[1].a >> 52);
@@ -2502,6 +2528,17 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 pre_b1 = ld_stream2(&hsw[2 * (size_t)l1 + 1]);
             }
         }
+    };
+    __syncthreads();
+    if (in_lds) {
+#pragma unroll
+        for (uint32_t q = 0; q < EPTF; ++q) {
+            if (!rq_ok(q)) continue;
+            const uint32_t hl = (uint32_t)(rr[q].a >> 52);
+            if (hl < HP) atomicAdd(&s_n[hl], 1u);
+            else flag(d, OV_BUG);
+        }
+        if (!SG_STATE_LATE) flat_prefetch();
         // the records are in registers now: re-defining them through asm keeps
         // the scatter below from waiting on the state prefetch (vmcnt(0))
 #pragma unroll
@@ -2557,6 +2594,14 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
     }
+    if (SG_STATE_LATE && in_lds) {
+        flat_prefetch();
+#pragma unroll
+        for (uint32_t q = 0; q < EPTF; ++q) {  // (the scatter below does not wait for those loads)
+            rr[q].a = opaque(rr[q].a);
+            rr[q].k = opaque(rr[q].k);
+        }
+    }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; the next k_scatter's gather refills it
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
     if (in_lds) {
@@ -2577,6 +2622,10 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (pos < n) part2[pos] = r;
         }
     }
+#if SG_ROWS_GLDS
+    // the rows' LDS-DMA (and the flat pass's state reads) have landed
+    if (ROWS || flat) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
     if constexpr (ROWS) {
 #pragma unroll
         for (uint32_t q = 0; q < RQ; ++q) {
@@ -2585,6 +2634,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     if (flat) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flat pass's state reads have returned
+#endif
     __syncthreads();  // the grouped events (and rows) are read back by other lanes
     if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
 
@@ -3160,18 +3210,22 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if constexpr (!FLAT) {
         if (gflat) {  // uniform
             if (tid == 0) s_nser = 0;
-            // (kept small: two are live across the passes; the host's digest,
-            // counter and seen words go to LDS at the end of pass 1, from the
-            // lane that finds itself rank 0)
+            // Every global load is issued at the start (a host's {digest,
+            // counter} and seen words by each of its lanes: the one that finds
+            // itself rank 0 uses them); nothing after pass 1 waits for memory.
+            // A host's state after its draws (rng) is written by the lane that
+            // draws its last send (the draws pass after this one); a host with
+            // no forwards keeps its rng.
             struct GfEv {
                 Rec ev;
                 uint32_t hl, cnt, start, rank;
-                uint32_t rng0, h, vh;
+                uint32_t rng0, h, vh, seenw;
                 uint64_t pops0;
                 bool valid, ok, first;
             };
             GfEv g[GFE];
-            uint32_t seenw[GFE];
+            ulonglong2 w23x[GFE];
+            uint32_t swx[GFE][GMW];
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
             const bool stf = stamp && tid == 0;
 #pragma unroll
@@ -3182,12 +3236,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 g[q].hl = (uint32_t)(g[q].ev.a >> 52);
                 const uint32_t hl = g[q].hl < HP ? g[q].hl : 0u, lh = sbase + hl < d.L ? sbase + hl : 0u;
                 const ulonglong2 w01 = hsw[2 * (size_t)lh];
+                w23x[q] = hsw[2 * (size_t)lh + 1];
                 g[q].rng0 = (uint32_t)w01.x;
                 g[q].h = (uint32_t)(w01.x >> 32);
                 g[q].pops0 = w01.y & M48;
                 g[q].vh = (uint32_t)(w01.y >> 48);
-                const uint32_t mw = (uint32_t)(g[q].ev.k & 0xFFFFu) >> 5;  // the message's seen word
-                seenw[q] = d.seen[(size_t)lh * d.mw + (mw < d.mw ? mw : 0u)];
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) swx[q][w] = d.seen[(size_t)lh * d.mw + (w < d.mw ? w : 0u)];
             }
             // pass 1: rank, first receipt, the host's eligibility
 #pragma unroll
@@ -3217,7 +3272,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     boot |= (r.k & SEQ_MASK) == 0;
                 }
                 f.ok = !boot && !(self_possible && S + tmin + d.vself[f.vh] < E);
-                f.first = f.ok && !dup && !(seenw[q] & (1u << (msg & 31)));
+                f.first = f.ok && !dup && !(gword(swx[q], msg >> 5) & (1u << (msg & 31)));
                 // by rank: the host's receipts in pop order
                 s_ef[f.start + f.rank] = f.first ? 1u : 0u;
                 s_et[f.start + f.rank] = digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
@@ -3226,29 +3281,25 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (stf) stamp[16] = wait_stamp();
             lds_barrier();
             // pass 2: each host's rank-0 lane reserves its records, writes the
-            // header, and issues the load of its state after the draws (the
-            // jump-ahead entry for its sends), used in pass 3
-            uint2 skx[GFE];
-            ulonglong2 w23x[GFE];
-            uint32_t swx[GFE][GMW];
+            // header and the host's state but the rng
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
                 const GfEv& f = g[q];
-                // the host's {digest, evc} and seen words, for its rank-0 lane in
-                // pass 3 (loaded by every lane: a select of loads, not a
-                // conditional load, which would wait where it is issued)
-                const uint32_t lh = sbase + (f.hl < HP ? f.hl : 0u) < d.L ? sbase + (f.hl < HP ? f.hl : 0u) : 0u;
-                w23x[q] = reinterpret_cast<const ulonglong2*>(d.hs + lh)[1];
-#pragma unroll
-                for (uint32_t w = 0; w < GMW; ++w) swx[q][w] = d.seen[(size_t)lh * d.mw + (w < d.mw ? w : 0u)];
-                skx[q] = d.skip[0];
                 if (!f.valid || f.rank != 0) continue;
                 if (!f.ok) {
                     atomicAdd(&s_nser, 1u);  // phase A's sequential body takes it
                     continue;
                 }
-                uint32_t nf = 0;
-                for (uint32_t k = 0; k < f.cnt; ++k) nf += s_ef[f.start + k];
+                uint32_t nf = 0, sw[GMW];
+                uint64_t dig = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w];
+                for (uint32_t k = 0; k < f.cnt; ++k) {
+                    nf += s_ef[f.start + k];
+                    dig += s_et[f.start + k];
+                    const uint32_t m = (uint32_t)(s_ev[f.start + k].k & 0xFFFFu);
+                    gset(sw, m >> 5, gword(sw, m >> 5) | (1u << (m & 31)));
+                }
                 // the host's active index: s_act is ascending
                 uint32_t lo = 0, hi = nact;
                 while (lo < hi) {
@@ -3257,26 +3308,35 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     else hi = mid;
                 }
                 const uint32_t j = lo, ns = nf * d.load;
-                if (ns >= d.nskip) flag(d, OV_BUG | GSK_A);
-                skx[q] = d.skip[ns < d.nskip ? ns : 0u];  // in flight until pass 3
                 const uint32_t base = atomicAdd(&s_nsend, ns + 1);
                 const bool bad = j >= nact || s_act[j < nact ? j : 0u] != f.hl || ns > 0xFFFFu ||
-                                 base + ns + 1 > d.ECAP;
+                                 ns >= d.nskip || base + ns + 1 > d.ECAP;
                 if (bad) {
                     a.overflow = true;
                     if (j < nact) s_sb[j] = UINT32_MAX;
                 } else {
                     s_sb[j] = base;
                     s_vh[j] = f.vh | (ns << 16);
+                    sput(base, Rec{w23x[q].y | ((uint64_t)f.rng0 << 32), HDR_REC | ((uint64_t)j << 32) | f.h});
                 }
                 ++a.ctr[C_ACTIVE];
                 s_c[f.hl] = bad ? UINT32_MAX : base;
                 s_n[f.hl] = GF_DONE | j;
+                // the state after the round: pops, digest, seen set; the rng
+                // here only when the host draws nothing (the last send's lane
+                // writes it otherwise), the counter with phase C
+                const uint32_t lh = sbase + f.hl;
+                HostState* hp = d.hs + lh;
+                if (ns == 0) reinterpret_cast<ulonglong2*>(hp)[0] = make_ulonglong2(hs_w0(f.rng0, f.h), hs_w1(f.pops0 + f.cnt, f.vh));
+                else reinterpret_cast<uint64_t*>(hp)[1] = hs_w1(f.pops0 + f.cnt, f.vh);
+                hp->digest = w23x[q].x + dig;
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w)
+                    if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = sw[w];
             }
             if (stf) stamp[17] = wait_stamp();
             lds_barrier();
-            // pass 3: the sends of every first receipt and the trace; the
-            // host's header and state by its rank-0 lane
+            // pass 3: the sends of every first receipt, and the trace
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
                 const GfEv& f = g[q];
@@ -3298,41 +3358,16 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     }
                 }
                 ++a.ctr[C_POPS];
-                if (base == UINT32_MAX) continue;  // overflow (flagged)
-                if (f.first) {
-                    uint32_t fb = 0;  // first receipts before this one
-                    for (uint32_t k = 0; k < f.rank; ++k) fb += s_ef[f.start + k];
-                    const uint64_t msg = f.ev.k & 0xFFFu;
-                    for (uint32_t m = 0; m < d.load; ++m) {
-                        const uint32_t si = fb * d.load + m;  // the send's index in the host's list
-                        sput(base + 1 + si, Rec{((uint64_t)j << 52) | (msg << 40) | trel,
-                                                (uint64_t)f.rng0 | ((uint64_t)si << 32)});
-                    }
-                    a.ctr[C_SENDS] += d.load;
+                if (base == UINT32_MAX || !f.first) continue;  // (UINT32_MAX: overflow, flagged)
+                uint32_t fb = 0;  // first receipts before this one
+                for (uint32_t k = 0; k < f.rank; ++k) fb += s_ef[f.start + k];
+                const uint64_t msg = f.ev.k & 0xFFFu;
+                for (uint32_t m = 0; m < d.load; ++m) {
+                    const uint32_t si = fb * d.load + m;  // the send's index in the host's list
+                    sput(base + 1 + si, Rec{((uint64_t)j << 52) | (msg << 40) | trel,
+                                            (uint64_t)f.rng0 | ((uint64_t)si << 32)});
                 }
-                if (f.rank != 0) continue;
-                // the host's rank-0 lane: its header and its state after the
-                // round (the counter comes with phase C, from the header)
-                const uint32_t lh = sbase + f.hl;
-                HostState* hp = d.hs + lh;
-                const ulonglong2 w23 = w23x[q];  // {digest, evc}
-                uint32_t sw[GMW];
-#pragma unroll
-                for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w];
-                uint64_t dig = 0;
-                for (uint32_t k = 0; k < f.cnt; ++k) {
-                    dig += s_et[f.start + k];
-                    const uint32_t m = (uint32_t)(s_ev[f.start + k].k & 0xFFFFu);
-                    gset(sw, m >> 5, gword(sw, m >> 5) | (1u << (m & 31)));
-                }
-                sput(base, Rec{w23.y | ((uint64_t)f.rng0 << 32), HDR_REC | ((uint64_t)j << 32) | f.h});
-                const uint2 sk = skx[q];
-                reinterpret_cast<ulonglong2*>(hp)[0] =
-                    make_ulonglong2(hs_w0(sk.x * f.rng0 + sk.y, f.h), hs_w1(f.pops0 + f.cnt, f.vh));
-                hp->digest = w23.x + dig;
-#pragma unroll
-                for (uint32_t w = 0; w < GMW; ++w)
-                    if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = sw[w];
+                a.ctr[C_SENDS] += d.load;
             }
             if (stf) stamp[18] = wait_stamp();
             lds_barrier();  // s_nsend, s_nser, the records
@@ -3414,6 +3449,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 }
                 const int32_t ch = dev_rand_r(st);  // worker.c:268-269
                 sput(i, Rec{r.a, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)ch << 32)});
+                // the host's last send: its rng after every draw (the gossip
+                // flat pass leaves it to this lane; skip_fix redoes a host
+                // with a null draw)
+                if (si + 1 == (s_vh[jr] >> 16)) {
+                    const uint32_t sb = s_sb[jr] & ~NULL_DRAW, ha = s_act[jr];
+                    if (ha < HP) reinterpret_cast<uint64_t*>(d.hs + sbase + ha)[0] = hs_w0(st, (uint32_t)sget(sb).k);
+                }
             }
             __syncthreads();
             // skip_fix: a marked host's sends drawn again in order (test_phold.c:
@@ -4667,7 +4709,11 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     // partitions than CUs.
     d.bin_off = (d.HP * 18 + 15) & ~15u;
     d.row_off = d.bin_off + ((8 * d.R + 15) & ~15u);
-    d.ev_off = d.row_off + (d.lds_rows ? (uint32_t)((row_bytes + 15) & ~15ull) : 0u);
+    // (the rows region in whole 1 KB pieces: one global_load_lds wave
+    // instruction fills 1 KB)
+    const uint32_t row_region = d.lds_rows ? (uint32_t)((row_bytes + 1023) & ~1023ull) : 0u;
+    d.row_pieces = row_region / 16;
+    d.ev_off = d.row_off + row_region;
     {
         uint32_t wgs = d.P > 256 ? 2 : 1, evl = 0;
         for (;;) {
@@ -4742,7 +4788,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     void* prow = nullptr;
     if (D.lds_rows) {
         unsigned char* pr_ = nullptr;
-        ALLOC(pr_, VV * resz);
+        ALLOC(pr_, VV * resz + 16);  // + a 16-B piece: k_proc's row pieces may read past the last row
         prow = pr_;
     }
     D.prow = prow;
