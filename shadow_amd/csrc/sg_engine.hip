@@ -2296,12 +2296,6 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_TICK8
 #define SG_TICK8 1
 #endif
-// SG_STATE_LATE: the flat pass's host-state loads issued after the sort's
-// scan (1) instead of with the histogram (0): a spill reload in the scan
-// waits vmcnt(0), i.e. for those loads, when they are already in flight
-#ifndef SG_STATE_LATE
-#define SG_STATE_LATE 0
-#endif
 // SG_ROWS_GLDS: k_proc's path rows go global -> LDS by global_load_lds (1),
 // or through 8 VGPRs per lane held through the sort (0)
 #ifndef SG_ROWS_GLDS
@@ -2514,7 +2508,8 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
     if (stamp && tid == 0) stamp[20] = wait_stamp();
     // the flat pass's host states, loaded as soon as the records are in (the
-    // histogram), or (SG_STATE_LATE) after the scan, under the scatter only
+    // histogram; issued after the scan instead, under the scatter only, the
+    // scatter took what the histogram gave back: profiles/r06/g5)
     auto flat_prefetch = [&]() __attribute__((always_inline)) {
         if (flat) {  // uniform
             const ulonglong2* hsw = reinterpret_cast<const ulonglong2*>(d.hs);
@@ -2538,7 +2533,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             if (hl < HP) atomicAdd(&s_n[hl], 1u);
             else flag(d, OV_BUG);
         }
-        if (!SG_STATE_LATE) flat_prefetch();
+        flat_prefetch();
         // the records are in registers now: re-defining them through asm keeps
         // the scatter below from waiting on the state prefetch (vmcnt(0))
 #pragma unroll
@@ -2593,14 +2588,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         l0 = l0 < d.L ? l0 : d.L - 1;
         pre_a0 = ld_stream2(&hsw[2 * (size_t)l0]);
         pre_b0 = ld_stream2(&hsw[2 * (size_t)l0 + 1]);
-    }
-    if (SG_STATE_LATE && in_lds) {
-        flat_prefetch();
-#pragma unroll
-        for (uint32_t q = 0; q < EPTF; ++q) {  // (the scatter below does not wait for those loads)
-            rr[q].a = opaque(rr[q].a);
-            rr[q].k = opaque(rr[q].k);
-        }
     }
     if (tid == 0) d.pcnt[p] = 0;  // consumed; the next k_scatter's gather refills it
     if (p == d.P - 1) reset_consumed(d);  // stores only (the last partition is the lightest)
@@ -3551,25 +3538,58 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
 
         // ---- phase C: one lane per send record.  A send's srcHostEventID is its
         // host's counter plus the kept sends before it in the host's order
-        // (worker.c:268-279, event.c:38): a short walk back over the host's
-        // records; then endTime drop, barrier bump, staging.
-        for (uint32_t i = tid; i < nsend; i += K2_T) {
+        // (worker.c:268-279, event.c:38), from a block-wide exclusive scan of
+        // the records' keep bits: each thread takes a contiguous run of
+        // records, a host's header records the scan's value at it (s_c by
+        // host, free since phase A), and a send counts the kept sends between
+        // its header and itself from the two (a walk back over the host's
+        // records, as before, was quadratic in its sends); then endTime drop,
+        // barrier bump, staging.  A host's kept sends are also counted into
+        // s_n by host (free since phase A): its header writes its counter.
+        for (uint32_t j = tid; j < nacta; j += K2_T) s_n[s_act[j]] = 0;
+        __syncthreads();
+        const uint32_t cper = (nsend + K2_T - 1) / K2_T, ci0 = tid * cper < nsend ? tid * cper : nsend;
+        const uint32_t ci1 = ci0 + cper < nsend ? ci0 + cper : nsend;
+        uint32_t kc = 0;
+        for (uint32_t i = ci0; i < ci1; ++i) {
+            const Rec r = sget(i);
+            if (!(r.k & HDR_REC) && (r.a >> 63)) {
+                ++kc;
+                atomicAdd(&s_n[s_act[(uint32_t)(r.a >> 40) & 0xFFFFu]], 1u);
+            }
+        }
+        uint64_t ktot;
+        const uint32_t kpre = (uint32_t)block_excl_scan_2x32((uint64_t)kc, s16, &ktot);  // barriers inside
+        {
+            uint32_t pre = kpre;
+            for (uint32_t i = ci0; i < ci1; ++i) {
+                const Rec r = sget(i);
+                if (r.k & HDR_REC) {
+                    if (!(r.k & PAD_REC)) s_c[s_act[(uint32_t)(r.k >> 32) & 0xFFFFu]] = pre;
+                } else {
+                    pre += (uint32_t)(r.a >> 63);
+                }
+            }
+        }
+        __syncthreads();  // every header's scan value
+        uint32_t pre = kpre;
+        for (uint32_t i = ci0; i < ci1; ++i) {
             const Rec r = sget(i);
             if (r.k & HDR_REC) {
                 if (r.k & PAD_REC) continue;
                 // a host's header: its counter after all its kept sends
-                const uint32_t j = (uint32_t)(r.k >> 32) & 0xFFFFu, ns = s_vh[j] >> 16;
-                uint64_t evc = gskip ? r.a & 0xFFFFFFFFull : r.a;  // (gskip: the state above)
-                for (uint32_t k = i + 1; k <= i + ns; ++k) evc += sget(k).a >> 63;
-                d.hs[sbase + s_act[j]].evc = evc;
+                const uint32_t ha = s_act[(uint32_t)(r.k >> 32) & 0xFFFFu];
+                d.hs[sbase + ha].evc = (gskip ? r.a & 0xFFFFFFFFull : r.a) + s_n[ha];
                 continue;
             }
-            const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
-            const uint32_t sb = s_sb[j];
-            const Rec hd = sget(sb);
-            uint64_t evc = gskip ? hd.a & 0xFFFFFFFFull : hd.a;  // the state's counter when phase A recorded the sends
-            for (uint32_t k = sb + 1; k < i; ++k) evc += sget(k).a >> 63;
+            const uint32_t kept_before = pre;
             const bool keep = (r.a >> 63) != 0;
+            pre += keep ? 1u : 0u;
+            const uint32_t j = (uint32_t)(r.a >> 40) & 0xFFFFu;
+            const uint32_t sb = s_sb[j], ha = s_act[j];
+            const Rec hd = sget(sb);
+            const uint64_t evc0 = gskip ? hd.a & 0xFFFFFFFFull : hd.a;  // the counter when phase A recorded the sends
+            const uint64_t evc = evc0 + (kept_before - s_c[ha]);
             if (!keep) {
                 ++a.ctr[C_DROPREL];
                 continue;
@@ -3582,7 +3602,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
             const uint32_t dst = (uint32_t)r.k;
             const uint64_t msg = r.k >> 32;  // gossip: the message id (0 for PHOLD)
-            const uint32_t sg = d.lo + sbase + s_act[j];
+            const uint32_t sg = d.lo + sbase + ha;
             if (dst == sg && tn < E) a.overflow = true;  // excluded by the phase A test
             if (dst != sg && tn < E) {              // host_single.c:180-184
                 tn = E;
