@@ -3265,8 +3265,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 s_et[f.start + f.rank] = digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
                                                     (ek & SEQ_MASK) >> d.msg_shift);
             }
-            if (stf) stamp[16] = wait_stamp();
+            if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
             lds_barrier();
+            if (stf) stamp[31] = __builtin_amdgcn_s_memrealtime();
             // pass 2: each host's rank-0 lane reserves its records, writes the
             // header and the host's state but the rng
 #pragma unroll
@@ -3321,8 +3322,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 for (uint32_t w = 0; w < GMW; ++w)
                     if (w < d.mw) d.seen[(size_t)lh * d.mw + w] = sw[w];
             }
-            if (stf) stamp[17] = wait_stamp();
+            if (stf) stamp[17] = __builtin_amdgcn_s_memrealtime();
             lds_barrier();
+            if (stf) stamp[18] = __builtin_amdgcn_s_memrealtime();
             // pass 3: the sends of every first receipt, and the trace
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
@@ -3356,9 +3358,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 }
                 a.ctr[C_SENDS] += d.load;
             }
-            if (stf) stamp[18] = wait_stamp();
+            if (stf) stamp[19] = __builtin_amdgcn_s_memrealtime();
             lds_barrier();  // s_nsend, s_nser, the records
-            if (stf) stamp[19] = stamp[30] = __builtin_amdgcn_s_memrealtime();
+            if (stf) stamp[30] = __builtin_amdgcn_s_memrealtime();
             ser = s_nser != 0;
         }
     }

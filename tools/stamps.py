@@ -44,6 +44,10 @@ for r in range(3):
     if fl.any():  # k_proc's flat pass ran (stamp 30 at its end)
         print("   flat pass (median us): %.2f in %d WGs; phase A after it %.2f"
               % (np.median(st[fl, 30] - st[fl, 1]) / 100, int(fl.sum()), np.median(st[fl, 2] - st[fl, 30]) / 100))
+        if os.environ.get("STAMPS_WL") == "c5":  # the gossip flat pass (stamps without waits)
+            y = np.diff(st[fl][:, [1, 16, 31, 17, 18, 19, 30]], axis=1) / 100
+            print("   gossip flat pass, lane 0 (median us): loads+pass 1 %.2f  barrier %.2f  pass 2 %.2f  "
+                  "barrier %.2f  pass 3 %.2f  barrier %.2f" % tuple(np.median(y, axis=0)))
         x = np.diff(st[fl][:, [1, 16, 17, 18, 19, 30]], axis=1) / 100
         print("   flat pass, lane 0 (median us): start %.2f  draws %.2f  dst loads %.2f  sends %.2f  barrier %.2f"
               % tuple(np.median(x, axis=0)))
