@@ -2550,6 +2550,31 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     }
     __syncthreads();  // the counts (LDS-only barriers here measured no change: the waits are wave imbalance)
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
+    // gossip (configs[4]): hosts take the record path (phases B / C resolve
+    // their sends one lane each) while the message ids fit the record's 12 bits
+    // and the host's seen set GMW registers
+    constexpr uint32_t GMW = 4;
+    // (the flat pass is PHOLD's: its instantiations carry none of this)
+    const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
+                            d.mw <= GMW && d.grec;
+    // lossy links (phases B and C apart): phase A leaves the record path's
+    // draws to a pass of one lane per send (send s of a host: draws 2s, 2s + 1
+    // after its state, by the jump-ahead table); a draw selecting no host
+    // marks the host, which one lane then redraws in order (skip_fix)
+    const bool gskip = gossip_rec && d.skip && d.pair_fmt != PAIR_DELAY && d.nskip > d.load * GMW * 32 &&
+                       d.gskip_on;
+    // the gossip flat pass (below): one lane per receipt, up to GFE per lane;
+    // in the event image's last records, per host (by partition slot) its
+    // digest terms' sum, first receipts, the messages it received and its
+    // active index, and per receipt (by host and rank) a first-receipt flag
+    constexpr uint32_t GFE = 2;
+    const uint32_t gfrec = (32 * HP + 4 * n + 15) / 16;
+    const bool gflat = gskip && in_lds && d.gflat && n <= GFE * K2_T && d.EVL >= n + gfrec;
+    unsigned long long* s_hdig = reinterpret_cast<unsigned long long*>(s_ev + d.EVL) - (gflat ? HP : 0u);
+    uint32_t* s_hcnt = reinterpret_cast<uint32_t*>(s_hdig) - (gflat ? HP : 0u);
+    uint32_t* s_jof = s_hcnt - (gflat ? HP : 0u);
+    uint32_t* s_hsw = s_jof - (gflat ? GMW * HP : 0u);  // [HP][GMW]
+    uint32_t* s_ef = s_hsw - (gflat ? n : 0u);
     // exclusive scan of (count, active) over the HP hosts, HP/K2_T per thread
     const uint32_t per = (HP + K2_T - 1) / K2_T;
     const uint32_t h0 = tid * per, hs = 1;  // (strided hosts measured: no change, profiles/r04/insert_pre)
@@ -2569,6 +2594,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             const uint32_t c = s_n[h];
             s_c[h] = (uint32_t)(run >> 32);
             if (c) s_act[(uint32_t)run] = (uint16_t)h;
+            if (gflat) {  // uniform: the gossip flat pass's per-host words
+                s_jof[h] = (uint32_t)run;
+                s_hdig[h] = 0;
+                s_hcnt[h] = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) s_hsw[h * GMW + w] = 0;
+            }
             run += ((uint64_t)c << 32) | (c ? 1u : 0u);
         }
     }
@@ -2636,27 +2668,6 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // Send records (phase A writes, phase B resolves, phase C commits) live in
     // the event image's unused tail while they fit, in HBM beyond it: phases
     // B and C then read them at LDS latency.
-    // gossip (configs[4]): hosts take the record path (phases B / C resolve
-    // their sends one lane each) while the message ids fit the record's 12 bits
-    // and the host's seen set GMW registers
-    constexpr uint32_t GMW = 4;
-    // (the flat pass is PHOLD's: its instantiations carry none of this)
-    const bool gossip_rec = !FLAT && d.workload == SG_WORKLOAD_GOSSIP && d.gossip_msgs <= 4096 &&
-                            d.mw <= GMW && d.grec;
-    // lossy links (phases B and C apart): phase A leaves the record path's
-    // draws to a pass of one lane per send (send s of a host: draws 2s, 2s + 1
-    // after its state, by the jump-ahead table); a draw selecting no host
-    // marks the host, which one lane then redraws in order (skip_fix)
-    const bool gskip = gossip_rec && d.skip && d.pair_fmt != PAIR_DELAY && d.nskip > d.load * GMW * 32 &&
-                       d.gskip_on;
-    // the gossip flat pass (below): one lane per receipt, up to GFE per lane,
-    // its per-receipt words (a digest term and a first-receipt flag, 12 B) in
-    // the event image's last records
-    constexpr uint32_t GFE = 2;
-    const uint32_t gfrec = (3 * n + 3) / 4;
-    const bool gflat = gskip && in_lds && d.gflat && n <= GFE * K2_T && d.EVL >= n + gfrec;
-    uint64_t* s_et = reinterpret_cast<uint64_t*>(s_ev + d.EVL) - (gflat ? n : 0u);
-    uint32_t* s_ef = reinterpret_cast<uint32_t*>(s_et) - (gflat ? n : 0u);
     Rec* s_snd = s_ev + (in_lds ? n : 0u);
     const uint32_t lcap = d.snd_lds ? (in_lds ? d.EVL - n - (gflat ? gfrec : 0u) : d.EVL) : 0u;
     auto sget = [&](uint32_t i) __attribute__((always_inline)) { return i < lcap ? s_snd[i] : snd[i]; };
@@ -3260,10 +3271,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 }
                 f.ok = !boot && !(self_possible && S + tmin + d.vself[f.vh] < E);
                 f.first = f.ok && !dup && !(gword(swx[q], msg >> 5) & (1u << (msg & 31)));
-                // by rank: the host's receipts in pop order
+                // by rank: the host's receipts in pop order; the host's sums by
+                // LDS atomics (its rank-0 lane reads them after the barrier)
                 s_ef[f.start + f.rank] = f.first ? 1u : 0u;
-                s_et[f.start + f.rank] = digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
-                                                    (ek & SEQ_MASK) >> d.msg_shift);
+                atomicAdd(&s_hdig[f.hl], (unsigned long long)digest_mix(f.pops0 + f.rank, S + et, (uint32_t)(ek >> SRC_SHIFT),
+                                                                         (ek & SEQ_MASK) >> d.msg_shift));
+                if (f.first) atomicAdd(&s_hcnt[f.hl], 1u);
+                atomicOr(&s_hsw[f.hl * GMW + (msg >> 5) % GMW], 1u << (msg & 31));
             }
             if (stf) stamp[16] = __builtin_amdgcn_s_memrealtime();
             lds_barrier();
@@ -3278,24 +3292,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                     atomicAdd(&s_nser, 1u);  // phase A's sequential body takes it
                     continue;
                 }
-                uint32_t nf = 0, sw[GMW];
-                uint64_t dig = 0;
+                const uint32_t nf = s_hcnt[f.hl];
+                const uint64_t dig = s_hdig[f.hl];
+                uint32_t sw[GMW];
 #pragma unroll
-                for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w];
-                for (uint32_t k = 0; k < f.cnt; ++k) {
-                    nf += s_ef[f.start + k];
-                    dig += s_et[f.start + k];
-                    const uint32_t m = (uint32_t)(s_ev[f.start + k].k & 0xFFFFu);
-                    gset(sw, m >> 5, gword(sw, m >> 5) | (1u << (m & 31)));
-                }
-                // the host's active index: s_act is ascending
-                uint32_t lo = 0, hi = nact;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_act[mid] < f.hl) lo = mid + 1;
-                    else hi = mid;
-                }
-                const uint32_t j = lo, ns = nf * d.load;
+                for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w] | s_hsw[f.hl * GMW + w];
+                const uint32_t j = s_jof[f.hl], ns = nf * d.load;  // the host's active index
                 const uint32_t base = atomicAdd(&s_nsend, ns + 1);
                 const bool bad = j >= nact || s_act[j < nact ? j : 0u] != f.hl || ns > 0xFFFFu ||
                                  ns >= d.nskip || base + ns + 1 > d.ECAP;
