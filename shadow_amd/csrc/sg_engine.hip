@@ -2029,9 +2029,14 @@ __device__ __forceinline__ int64_t* xblock(const Dev& d, uint32_t q) {
 // receiver's header loads are system-scope too.  Within one device the
 // blocks are uncached local memory and plain stores drained by vmcnt(0)
 // already order the rows before the arrival (measured).
+// (through a global-address-space pointer: a generic one — these come from
+// a table of peer regions or a select between two arrays — compiles to flat
+// stores, which count on lgkmcnt too and make later LDS accesses wait vmcnt(0))
+typedef __attribute__((address_space(1))) int64_t gint64_t;
 __device__ __forceinline__ void xst(uint32_t sys, int64_t* p, int64_t v) {
-    if (sys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else *p = v;
+    gint64_t* g = (gint64_t*)p;  // (a C-style cast: reinterpret_cast cannot change address spaces)
+    if (sys) __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *g = v;
 }
 __device__ __forceinline__ void xlink_release() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void xlink_arrive(int64_t* const* peer, uint32_t G, uint32_t g, uint32_t skip) {
@@ -2670,10 +2675,26 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // B and C then read them at LDS latency.
     Rec* s_snd = s_ev + (in_lds ? n : 0u);
     const uint32_t lcap = d.snd_lds ? (in_lds ? d.EVL - n - (gflat ? gfrec : 0u) : d.EVL) : 0u;
-    auto sget = [&](uint32_t i) __attribute__((always_inline)) { return i < lcap ? s_snd[i] : snd[i]; };
+    // The HBM side uses a different instruction (non-temporal) from the LDS
+    // side, so the compiler cannot merge the two into one flat access: a flat
+    // store counts on vmcnt as well, and every later LDS access then waited
+    // vmcnt(0) — for all of the wave's outstanding global stores — behind it
+    // (2-3 us of the gossip flat pass and phases B / C, profiles/r06/g8).
+    typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+    auto sget = [&](uint32_t i) __attribute__((always_inline)) {
+        if (i < lcap) return s_snd[i];
+        const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(snd + i));
+        return Rec{v.x, v.y};
+    };
     auto sput = [&](uint32_t i, const Rec& r) __attribute__((always_inline)) {
-        if (i < lcap) s_snd[i] = r;
-        else snd[i] = r;
+        if (i < lcap) {
+            s_snd[i] = r;
+        } else {
+            u64x2_t v;
+            v.x = r.a;
+            v.y = r.k;
+            __builtin_nontemporal_store(v, reinterpret_cast<u64x2_t*>(snd + i));
+        }
     };
     const int32_t last = s_last;
 
@@ -3653,8 +3674,9 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
                 xst(1u, o, w0);
                 xst(1u, o + 1, w1);
             } else {
-                o[0] = w0;
-                o[1] = w1;
+                gint64_t* og = (gint64_t*)o;
+                og[0] = w0;
+                og[1] = w1;
             }
         }
     }
