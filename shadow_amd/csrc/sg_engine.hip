@@ -3304,22 +3304,47 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             lds_barrier();
             if (stf) stamp[31] = __builtin_amdgcn_s_memrealtime();
             // pass 2: each host's rank-0 lane reserves its records, writes the
-            // header and the host's state but the rng
+            // header and the host's state but the rng.  The start's loads are
+            // taken into registers first, before any store: a use of them
+            // after the stores made the compiler wait vmcnt(0), i.e. for those
+            // stores too (vmcnt counts in order)
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {
+                w23x[q].x = opaque(w23x[q].x);
+                w23x[q].y = opaque(w23x[q].y);
+#pragma unroll
+                for (uint32_t w = 0; w < GMW; ++w) swx[q][w] = opaque(swx[q][w]);
+            }
+            // The records are reserved in converged code: a DPP scan of the
+            // lane's two counts and one LDS atomic per wave (the compiler's
+            // own aggregation of a divergent atomic walks the active lanes).
+            uint32_t nres[GFE], tot = 0;
+            bool anyser = false;
 #pragma unroll
             for (uint32_t q = 0; q < GFE; ++q) {
                 const GfEv& f = g[q];
-                if (!f.valid || f.rank != 0) continue;
-                if (!f.ok) {
-                    atomicAdd(&s_nser, 1u);  // phase A's sequential body takes it
-                    continue;
-                }
-                const uint32_t nf = s_hcnt[f.hl];
+                const bool lead = f.valid && f.rank == 0;
+                const uint32_t nf = s_hcnt[f.hl < HP ? f.hl : 0u];
+                nres[q] = lead && f.ok ? nf * d.load + 1u : 0u;
+                anyser |= lead && !f.ok;  // phase A's sequential body takes it
+                tot += nres[q];
+            }
+            if (anyser) s_nser = 1u;
+            const uint32_t incl = wave_incl_scan_u32(tot);
+            uint32_t rbase = 0;
+            if ((tid & 63) == 63 && incl) rbase = atomicAdd(&s_nsend, incl);
+            rbase = (uint32_t)__builtin_amdgcn_readlane((int)rbase, 63) + incl - tot;
+#pragma unroll
+            for (uint32_t q = 0; q < GFE; ++q) {
+                const GfEv& f = g[q];
+                if (nres[q] == 0) continue;
+                const uint32_t base = rbase, ns = nres[q] - 1u;
+                rbase += nres[q];
                 const uint64_t dig = s_hdig[f.hl];
                 uint32_t sw[GMW];
 #pragma unroll
                 for (uint32_t w = 0; w < GMW; ++w) sw[w] = swx[q][w] | s_hsw[f.hl * GMW + w];
-                const uint32_t j = s_jof[f.hl], ns = nf * d.load;  // the host's active index
-                const uint32_t base = atomicAdd(&s_nsend, ns + 1);
+                const uint32_t j = s_jof[f.hl];  // the host's active index
                 const bool bad = j >= nact || s_act[j < nact ? j : 0u] != f.hl || ns > 0xFFFFu ||
                                  ns >= d.nskip || base + ns + 1 > d.ECAP;
                 if (bad) {
