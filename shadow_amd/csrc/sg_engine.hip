@@ -2301,6 +2301,12 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_TICK8
 #define SG_TICK8 1
 #endif
+// SG_SORT_LB: the PHOLD instantiations' barriers from the partition's loads to
+// its scatter wait for LDS only (1, default), or for every outstanding access (0):
+// configs[3] k_proc 29.5 -> 29.1 us (profiles/r06/g13)
+#ifndef SG_SORT_LB
+#define SG_SORT_LB 1
+#endif
 // SG_ROWS_GLDS: k_proc's path rows go global -> LDS by global_load_lds (1),
 // or through 8 VGPRs per lane held through the sort (0)
 #ifndef SG_ROWS_GLDS
@@ -2511,7 +2517,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     };
     static_assert(K2_T >= NSPEC, "one GSpec id per thread");
     if (p == d.P - 1) gspec_write(d, rs_fold, E);  // the lightest partition; loads beside the rows
-    if (stamp && tid == 0) stamp[20] = wait_stamp();
+    if (stamp && tid == 0) stamp[20] = __builtin_amdgcn_s_memrealtime();
     // the flat pass's host states, loaded as soon as the records are in (the
     // histogram; issued after the scan instead, under the scatter only, the
     // scatter took what the histogram gave back: profiles/r06/g5)
@@ -2529,7 +2535,15 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             }
         }
     };
-    __syncthreads();
+    // Barriers up to the scatter wait for LDS only (SG_SORT_LB): no lane reads
+    // another's global data before the vmcnt(0) after the scatter, so the path
+    // rows' DMA and the flat pass's state loads stay in flight under the
+    // histogram and the scan
+    auto sort_barrier = [&]() __attribute__((always_inline)) {
+        if (SG_SORT_LB && FLAT) lds_barrier();  // (the gossip path measured +0.5 us: profiles/r06/g13)
+        else __syncthreads();
+    };
+    sort_barrier();
     if (in_lds) {
 #pragma unroll
         for (uint32_t q = 0; q < EPTF; ++q) {
@@ -2553,7 +2567,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             else flag(d, OV_BUG);
         }
     }
-    __syncthreads();  // the counts (LDS-only barriers here measured no change: the waits are wave imbalance)
+    sort_barrier();  // the counts
     if (stamp && tid == 0) stamp[21] = __builtin_amdgcn_s_memrealtime();
     // gossip (configs[4]): hosts take the record path (phases B / C resolve
     // their sends one lane each) while the message ids fit the record's 12 bits
@@ -2592,7 +2606,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     uint64_t tot;
-    uint64_t run = block_excl_scan_2x32(mine, s16, &tot);
+    uint64_t run = block_excl_scan_2x32<SG_SORT_LB != 0 && FLAT>(mine, s16, &tot);
     for (uint32_t j = 0; j < per; ++j) {
         const uint32_t h = h0 + j * hs;
         if (h < HP) {
@@ -2610,7 +2624,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     const uint32_t nact = (uint32_t)tot;
-    __syncthreads();
+    sort_barrier();
     if (stamp && tid == 0) stamp[22] = __builtin_amdgcn_s_memrealtime();
     const uint32_t sbase = p * HP;  // the partition's first local slot
     // phase A's first host of every lane: state loads issued now, under the
