@@ -42,14 +42,20 @@ from shadow_amd.roofline import HBM_PEAK_GBS, kernel_line, proc_bytes, scatter_b
 # FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh), corrected per
 # MI355X_MICROARCH.md §HBM by tools/prof_summary.py.  Counters cannot be read
 # from inside a timed run, so the bench quotes the committed measurement.
-PMC_JSON = {w: os.path.join(ROOT, "profiles", "r05", "final3", f"prof_{w}", "pmc.json") for w in ("c4", "c2", "c5")}
+# The driver's own run (--steps 20 --warmup 5) has a profile of that window:
+# its first rounds differ from the default run's steady state.
+PMC_DIR = os.path.join(ROOT, "profiles", "r06", "final")
+PMC_JSON = {w: os.path.join(PMC_DIR, f"prof_{w}", "pmc.json") for w in ("c4", "c2", "c5")}
+PMC_JSON_WINDOW = {("c4", 20, 5): os.path.join(PMC_DIR, "prof_c4_driver", "pmc.json")}
 DOMINANT = "k_proc"
+_PMC_WINDOW = (None, None)
 
 
 def pmc_traffic(workload, n_hosts, kernel=DOMINANT):
     """(corrected PMC bytes per launch of `kernel`, the bytes with FETCH_SIZE as
-    counted, source) from the committed profile of this workload, or Nones."""
-    path = PMC_JSON.get(workload)
+    counted, source) from the committed profile of this workload (of this
+    run's window where one was profiled), or Nones."""
+    path = PMC_JSON_WINDOW.get((workload,) + _PMC_WINDOW, PMC_JSON.get(workload))
     if (workload == "c4" and n_hosts != 1_000_000) or not path or not os.path.exists(path):
         return None, None, None
     ks = json.load(open(path))["kernels"]
@@ -252,6 +258,9 @@ def drop_in_policy(cfg, warmup, rounds, workers, fixture=None):
 
 def run_single(args):
     from shadow_amd.engine import Engine
+
+    global _PMC_WINDOW
+    _PMC_WINDOW = (args.steps, args.warmup)
 
     cfg = args.cfg
     wl = WL.get(args.workload)
