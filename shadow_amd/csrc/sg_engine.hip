@@ -155,6 +155,12 @@ struct Slot {
 #endif
 // SG_RS_LANES: k_scatter's planning thread reads the round state from wave
 // 0's registers (one readlane per word) instead of from its LDS copy.
+// SG_PLAN_TOUCH: k_scatter's planning thread fetches the plan's kernel
+// arguments while the round state is in flight (1, default), or inside the
+// plan (0)
+#ifndef SG_PLAN_TOUCH
+#define SG_PLAN_TOUCH 1
+#endif
 #ifndef SG_RS_LANES
 #define SG_RS_LANES 1
 #endif
@@ -1693,6 +1699,26 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
 }
 #define RSF(f) ((uint32_t)(offsetof(RoundState, f) / 8))
 
+// Forces the scalar loads of the Dev fields step_view / next_window read (an
+// input-only asm operand needs the value in a register here).
+template <class T>
+__device__ __forceinline__ void touch_s(const T& v) {
+    asm volatile("" ::"s"(v));
+}
+__device__ __forceinline__ void touch_plan_args(const Dev& d) {
+    touch_s(d.W);
+    touch_s((uint32_t)d.window_rule);
+    touch_s(d.fixed_jump);
+    touch_s(d.runahead_min);
+    touch_s(d.end_time);
+    touch_s((uint32_t)d.ring32);
+    touch_s(d.R);
+    touch_s(d.NCH);
+    touch_s(d.G);
+    touch_s(d.wdiv.m);
+    touch_s(d.wdiv.s1);
+    touch_s(d.wdiv.s2);
+}
 // mode 0: one shard, after k_proc; 1: several shards, after the all-to-all
 // (hdr: the G blocks' HDR_W header words, LDS); 2: boot (the first window is
 // listed already).  One thread, from the LDS copy of the round state
@@ -1857,7 +1883,9 @@ __device__ __forceinline__ uint64_t load_round_state(const Dev& d, int mode, con
             if (lane + q * 64 < nh) s_hdr[lane + q * 64] = h[q];
         if (h0) *h0 = (uint64_t)h[0];
     }
-    if (lane < RSW) s_rsw[lane] = v;
+    // (with SG_RS_LANES the LDS copy is not read: its store would wait for the
+    // load before thread 0 fetches the plan's kernel arguments)
+    if ((!SG_RS_LANES || !SG_PLAN_TOUCH) && lane < RSW) s_rsw[lane] = v;
     return v;  // the lane's word: thread 0 reads the state by readlane (SG_RS_LANES)
 }
 
@@ -4072,10 +4100,15 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
     // wave 0: the round state (and headers) in one batch of loads, then thread
     // 0 plans the step from LDS and arrives.  The arrival's return is not
     // waited for until the workgroup's end: the last to arrive publishes then.
-    uint64_t ticket = 0, rsv = 0, h0 = 0;
+    uint64_t ticket = 0, rsv = 0, h0 = 0, t_rs = 0, t_sv = 0;
     if (tid < 64) rsv = load_round_state(d, mode, recv, s_rsw, s_hdr, &h0);
     asm volatile("" ::: "memory");  // the copy's stores before thread 0's reads of it
     if (tid == 0) {
+        // the kernel arguments the plan reads, fetched while the round state is
+        // in flight: read first inside the plan, each scalar-cache miss was a
+        // round trip after it (the plan took 1.2 us, profiles/r06/g14)
+        if (SG_PLAN_TOUCH) touch_plan_args(d);
+        if (d.stamps) t_rs = wait_stamp();  // SG_STAMPS: the round state is in
 #if SG_RS_LANES
         // the round state from wave 0's registers (one readlane per word), not
         // through a chain of LDS reads
@@ -4087,6 +4120,7 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
 #else
         step_view(d, mode, reinterpret_cast<const RoundState*>(s_rsw), s_hdr, sv);
 #endif
+        if (d.stamps) t_sv = __builtin_amdgcn_s_memrealtime();  // the step is planned
         // every read of the round state has returned (they are in LDS).  The
         // address is made opaque (divergent to the compiler): for a uniform one
         // the atomic optimizer reads the result back at once, which would wait
@@ -4149,6 +4183,8 @@ __global__ __launch_bounds__(K3_T) void k_scatter(Dev d, const int64_t* recv, in
         st[1] = st[2] = st[3] = st[6] = st[0];
         st[5] = 0;
         st[16] = t_in;
+        st[17] = t_rs;
+        st[18] = t_sv;
     }
     if (blk == nv - 1) {
         uint64_t* s16 = (uint64_t*)lds;

@@ -73,7 +73,9 @@ for r in range(3):
         for role, nm in enumerate(["insert", "received", "gather", "rmin", "refill"]):
             x = sc[sc[:, 4] == role]
             if len(x):
-                print(f"     {nm:<9} prologue median {np.median(x[:, 0] - x[:, 16]) / 100:5.2f} us, "
+                print(f"     {nm:<9} prologue median {np.median(x[:, 0] - x[:, 16]) / 100:5.2f} us "
+                      f"(round state {np.median(x[:, 17] - x[:, 16]) / 100:.2f}, plan "
+                      f"{np.median(x[:, 18] - x[:, 17]) / 100:.2f}, rest {np.median(x[:, 0] - x[:, 18]) / 100:.2f}), "
                       f"entry median {np.median(x[:, 16] - e0) / 100:5.2f} us")
     for role, nm in enumerate(["insert", "received", "gather", "rmin", "refill"]):
         x = sc[sc[:, 4] == role]
