@@ -1536,6 +1536,7 @@ struct SegScan {
 __device__ __forceinline__ SegScan seg_scan(const Rec* seg, uint32_t cnt, uint64_t et, uint64_t ek) {
     SegScan s{0, et, (ek & SEQ_MASK) == 0};
     if (cnt > 1) {
+#pragma unroll 4
         for (uint32_t k = 0; k < cnt; ++k) {
             const Rec r = seg[k];
             const uint64_t rt = r.a & M52;
@@ -2335,6 +2336,14 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 #ifndef SG_SORT_LB
 #define SG_SORT_LB 1
 #endif
+// k_proc's static LDS, at most (the dynamic region is sized around it;
+// sg_engine_boot checks every instantiation against it)
+constexpr uint32_t PROC_LDS_STATIC = 5u << 10;
+// SG_SKIP_LDS: the flat pass reads its skip-ahead table from an LDS copy (1,
+// default) or from global memory (0)
+#ifndef SG_SKIP_LDS
+#define SG_SKIP_LDS 1
+#endif
 // SG_ROWS_GLDS: k_proc's path rows go global -> LDS by global_load_lds (1),
 // or through 8 VGPRs per lane held through the sort (0)
 #ifndef SG_ROWS_GLDS
@@ -2483,6 +2492,12 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     }
     if (tid < MAXG) sh.peer[tid] = 0;
+#if SG_SKIP_LDS
+    // the flat pass's skip-ahead table (ranks below FLAT_CMAX) in LDS: read once
+    // per lane there, behind its rank scan (a global load on that chain before)
+    __shared__ uint2 s_skipf[FLAT_CMAX];
+    if (FLAT && d.skip && tid < FLAT_CMAX) s_skipf[tid] = d.skip[tid < d.nskip ? tid : 0u];
+#endif
     Rec* part2 = d.part2 + (size_t)p * d.CAPP;
     const bool in_lds = n <= d.EVL && (!FLAT || n <= SPEC * K2_T);
     // Flat pass (PHOLD, events in LDS, at most SPEC per lane; see below): the
@@ -3089,7 +3104,11 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
             f.pops_end = pops0 + cnt;
             uint32_t before = 0;  // sends of the host's earlier events (all kept: flat_ok)
             if (use_skip) {  // two draws per earlier event, skipped in one step
+#if SG_SKIP_LDS
+                const uint2 sk = s_skipf[sc.rank];  // rank < cnt <= FLAT_CMAX (flat_ok)
+#else
                 const uint2 sk = d.skip[sc.rank];
+#endif
                 rng = sk.x * rng + sk.y;
                 before = sc.rank;
             } else {
@@ -4838,7 +4857,7 @@ int sg_engine_create(const sg_phold_params* params, const sg_phold_tables* t, in
     {
         uint32_t wgs = d.P > 256 ? 2 : 1, evl = 0;
         for (;;) {
-            const uint32_t dyn = (160u << 10) / wgs - (4u << 10);
+            const uint32_t dyn = (160u << 10) / wgs - PROC_LDS_STATIC;
             evl = dyn > d.ev_off ? (dyn - d.ev_off) / 16 : 0;
             if (wgs == 1 || evl >= 1024) break;
             wgs = 1;
@@ -5172,14 +5191,22 @@ int sg_engine_boot(sg_engine* e) {
     }
     HIPCHK(hipSetDevice(e->device));
     const Dev& d = e->d;
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
-    HIPCHK(hipFuncSetAttribute((const void*)k_proc<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    // each instantiation's dynamic LDS, checked against its static LDS (the
+    // sizing above reserves PROC_LDS_STATIC for it): 160 KB per CU in all
+    const void* procs[] = {(const void*)k_proc<true, true, false>, (const void*)k_proc<true, false, false>,
+                           (const void*)k_proc<false, true, false>, (const void*)k_proc<false, false, false>,
+                           (const void*)k_proc<true, true, true>, (const void*)k_proc<true, false, true>,
+                           (const void*)k_proc<false, true, true>, (const void*)k_proc<false, false, true>};
+    for (const void* f : procs) {
+        hipFuncAttributes fa;
+        HIPCHK(hipFuncGetAttributes(&fa, f));
+        if (fa.sharedSizeBytes > PROC_LDS_STATIC || fa.sharedSizeBytes + d.proc_lds > (160u << 10)) {
+            sg_set_error("sg_engine_boot: k_proc needs %zu B of static LDS beside %u B dynamic (reserved %u)",
+                         (size_t)fa.sharedSizeBytes, d.proc_lds, PROC_LDS_STATIC);
+            return SG_ERR_INVAL;
+        }
+        HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.proc_lds));
+    }
     HIPCHK(hipMemsetAsync(d.btab, 0xFF, (size_t)XS * d.R * d.NCH * sizeof(uint32_t), e->stream));
     HIPCHK(hipMemsetAsync(d.gspec, 0xFF, sizeof(GSpec), e->stream));  // no guess (fold UINT64_MAX)
     const uint32_t n = std::max<uint32_t>(std::max<uint32_t>(d.L, d.NCH),
