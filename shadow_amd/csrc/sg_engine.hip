@@ -1589,7 +1589,7 @@ __device__ __forceinline__ uint64_t wait_stamp() {
 // reservation of its head; avail: the ring's usable end at launch).  k_scatter
 // writes the events into the reserved slots and refills the stashes.  Every
 // thread of the block (T threads) calls it.
-template <int T>
+template <int T, bool STASH_LOOP = false>
 __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint32_t x, const uint32_t* s_bc, const uint32_t* s_bm,
                                 uint64_t bS, uint32_t bSr, uint32_t sid, uint32_t sn, uint64_t avail,
                                 uint32_t* s_ids, uint64_t* s_h, uint64_t* s16) {
@@ -1633,6 +1633,23 @@ __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint
         if (tid == 0) *s_h = atomicAdd((unsigned long long*)&d.rs->fl_head, (unsigned long long)(total - sn));
         lds_barrier();
     }
+    if (STASH_LOOP && total <= sn) {  // uniform: every chunk from the stash (LDS only)
+        // (a separate loop: with the ring's global load in the same loop, its
+        // id register made every LDS-path iteration wait vmcnt(0), i.e. for
+        // all of the wave's outstanding stores, before its btab store;
+        // configs[3] k_proc -0.4 us.  The PHOLD instantiations only: in the
+        // gossip one, at its register limit, the extra loop moved spills into
+        // hot code, +2 us on configs[4], profiles/r06/g30)
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t rb = tid + q * T;
+            for (uint32_t k = 0; k < nn[q]; ++k, ++off) {
+                const uint32_t ci = first[q] + k, id = s_ids[off];
+                if (ci < NCH) d.btab[((size_t)x * R + rb) * NCH + ci] = id;
+                else flag(d, OV_POOL);
+            }
+        }
+    } else {
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
         const uint32_t rb = tid + q * T;
@@ -1649,6 +1666,7 @@ __device__ __forceinline__ void reserve_buckets(const Dev& d, uint32_t row, uint
             if (ci < NCH) d.btab[((size_t)x * R + rb) * NCH + ci] = id;
             else flag(d, OV_POOL);
         }
+    }
     }
     const uint32_t left = total < sn ? sn - (uint32_t)total : 0u;
     if (tid < left) d.stash[(size_t)row * ST + tid] = s_ids[total + tid];
@@ -3806,7 +3824,7 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
         }
     };
     partials();
-    reserve_buckets<K2_T>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
+    reserve_buckets<K2_T, FLAT>(d, p, p % XS, s_bc, s_bm, bS, bSr, stash_id, stash_n, ring_end, s_ids, &s_h, s16);
     if (stamp && tid == 0) stamp[15] = wait_stamp();
     if (tid == 0) {
         if (sh.nloc > d.ECAP || sh.nrem > d.ECAP || s_nsend > d.ECAP) flag(d, OV_PROC);
