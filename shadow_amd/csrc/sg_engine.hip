@@ -2357,6 +2357,11 @@ __device__ __forceinline__ void gspec_write(const Dev& d, uint64_t fold, uint64_
 // k_proc's static LDS, at most (the dynamic region is sized around it;
 // sg_engine_boot checks every instantiation against it)
 constexpr uint32_t PROC_LDS_STATIC = 5u << 10;
+// SG_SGET_WAIT: a send record read from HBM (past the LDS share) is waited
+// for at its load (1, default), or at its first use (0)
+#ifndef SG_SGET_WAIT
+#define SG_SGET_WAIT 1
+#endif
 // SG_SKIP_LDS: the flat pass reads its skip-ahead table from an LDS copy (1,
 // default) or from global memory (0)
 #ifndef SG_SKIP_LDS
@@ -2756,9 +2761,13 @@ __global__ __launch_bounds__(K2_T) void k_proc(Dev d) {
     // vmcnt(0) — for all of the wave's outstanding global stores — behind it
     // (2-3 us of the gossip flat pass and phases B / C, profiles/r06/g8).
     typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+    // The HBM side's load is waited for where it is issued: left pending, its
+    // register made every use of sget's result wait vmcnt(0) on the LDS side
+    // too, i.e. for all of the wave's outstanding stores.
     auto sget = [&](uint32_t i) __attribute__((always_inline)) {
         if (i < lcap) return s_snd[i];
         const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(snd + i));
+        if (SG_SGET_WAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (expcnt, lgkmcnt left)
         return Rec{v.x, v.y};
     };
     auto sput = [&](uint32_t i, const Rec& r) __attribute__((always_inline)) {
