@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=${O:-gpurun_out/r06final2}
+O=${O:-gpurun_out/r06final3}
 mkdir -p $O
 run() {  # name last_n args...
   local name=$1 last=$2; shift 2
