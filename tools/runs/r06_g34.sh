@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 6, thirty-fourth call: bisecting configs[3] between round 5's final tree
+# and this one on one box: nine commits (extracted and built under _bis/, not
+# committed), the driver's command each, in order and then in reverse.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+O=${O:-gpurun_out/r06g34}
+mkdir -p $O
+R=$PWD
+for n in A B C E F H I K L L K I H F E C B A; do
+  (cd $R/_bis/$n && timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-drop-in) > $O/$n.json 2> $O/$n.err || { tail $O/$n.err; exit 3; }
+  python -c "import json;d=json.load(open('$O/$n.json'));print('$n %.4g'%d['value'], round(d['ms_per_step']*1e3,2), 'us/step', {k:round(v,2) for k,v in d['roofline']['kernel_us_per_round'].items()}, d['parity']['match'])"
+done
