@@ -348,3 +348,23 @@ def test_gossip_draws_after_phase_a(skip, cut, monkeypatch):
     assert orc.stats()["drop_reliability"] > 0
     if cut:
         assert gs["null_dst"] > 1000, gs["null_dst"]
+
+
+@pytest.mark.parametrize("workload", ["gossip", "lossy", "gossip_flat_off"])
+def test_send_records_in_hbm(workload, monkeypatch):
+    """Send records past k_proc's LDS share live in HBM (non-temporal stores; a
+    load there is waited for where it is issued, so the LDS side never waits for
+    the wave's stores).  SG_SND_LDS=0 puts every record there: the gossip record
+    path with its flat pass (and with it off, phase A recording), and PHOLD on
+    lossy links (phases B / C apart), against the oracle."""
+    monkeypatch.setenv("SG_SND_LDS", "0")
+    if workload == "gossip_flat_off":
+        monkeypatch.setenv("SG_GFLAT", "0")
+    if workload.startswith("gossip"):
+        cfg = phold.c5_config(n_hosts=2000, V=16, msgs=40, end_time_s=0.6)
+        eng, orc = _run_both(cfg)
+        assert orc.stats()["drop_reliability"] > 0
+    else:
+        cfg = phold.lossy_config(n_hosts=30_000, V=64, end_time_s=0.3)
+        eng, orc = _run_both(cfg, max_rounds=60)
+    _assert_same(eng, orc)
